@@ -1,0 +1,173 @@
+/*
+ * marlsat.h — C-ABI of libmarlsat.so, the MI355X (gfx950) implementation of the
+ * marl-sat data-parallel hot path: the batched multi-agent SAT environment
+ * (reset / step / auto-reset / local observations) and the MAPPO rollout math
+ * around it (GAE + advantage normalisation).
+ *
+ * Every pointer is a DEVICE pointer owned by the caller (torch tensors on the
+ * Python side); dims are passed explicitly; the stream is the last argument and
+ * every call only enqueues work on it (no implicit device synchronisation, no
+ * allocation on the hot path).  Return value: 0 on success, negative on error
+ * (MSAT_EBADARG / MSAT_EHIP); msat_last_error() returns a thread-local message.
+ *
+ * Reference interfaces replaced (paths relative to kongqg/marl-sat):
+ *   msat_pool_pack           <- jnp.abs(clauses)-1 literal decoding shared by
+ *                               src/envs/multi_agent_sat_env.py:135-144 and :100
+ *   msat_env_reset           <- SATEnv.reset               src/envs/multi_agent_sat_env.py:158-181
+ *                               (+ _compute_observation_maps :99-128, get_obs :345-398)
+ *   msat_env_step            <- SATEnv.step_env            src/envs/multi_agent_sat_env.py:225-284
+ *                               (flip decode :230-250, _calculate_satisfaction_explicit
+ *                               :130-156, _calculate_rewards :183-198 / PBRS :201-223)
+ *                               autoreset=1 additionally replaces the rollout's
+ *                               reset-all-then-where-select  src/learners/mappo_gnn_sat_learner.py:422-464
+ *   msat_env_obs             <- SATEnv.get_obs              src/envs/multi_agent_sat_env.py:345-398
+ *   msat_env_masks           <- SATState.agent_clause_masks / agent_neighbor_masks /
+ *                               literal_to_agent_idx        src/envs/multi_agent_sat_env.py:160-161
+ *   msat_clause_features     <- SATDataWrapper._calculate_dynamic_clause_features
+ *                               src/learners/mappo_gnn_sat_learner.py:176-195
+ *   msat_static_var_features <- SATDataWrapper._state_to_gnn_input degrees
+ *                               src/learners/mappo_gnn_sat_learner.py:150-164
+ *   msat_gae                 <- _calculate_gae + global normalisation
+ *                               src/learners/mappo_gnn_sat_learner.py:504-532
+ */
+#ifndef MARLSAT_H
+#define MARLSAT_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSAT_OK 0
+#define MSAT_EBADARG (-1)
+#define MSAT_EHIP (-2)
+#define MSAT_ECOMM (-3)
+
+/* packed literal codes (uint16 per literal slot, clause rows padded to 4 slots) */
+#define MSAT_LIT_NULL 0xFFFFu   /* literal value 0 in the int32 input: always false,  */
+                                /* and (reference quirk) "matches" padded agent slots */
+#define MSAT_LIT_ABSENT 0xFFFEu /* padding slot beyond the clause width: inert        */
+#define MSAT_LIT_SLOTS 4
+
+/* obs element type */
+#define MSAT_OBS_I32 0 /* reference dtype (jnp.int32)                */
+#define MSAT_OBS_I8 1  /* same values {-1,0,1}, 4x fewer bytes        */
+
+/* reward modes */
+#define MSAT_REWARD_SPARSE 0 /* active reference reward: 1.0 on solve else 0 (env:183-198) */
+#define MSAT_REWARD_PBRS 1   /* commented reference variant (env:201-223)                  */
+
+/* Static description of one batch of environments (all envs share V, C, K, A). */
+typedef struct msat_env_desc {
+    int32_t num_envs;           /* B */
+    int32_t num_vars;           /* V  (<= 32000) */
+    int32_t num_clauses;        /* C */
+    int32_t clause_width;       /* K  (1..3) */
+    int32_t num_agents;         /* A  (<= 1000); contiguous partition, first V%A agents get V/A+1 vars */
+    int32_t max_vars_per_agent; /* M = ceil(V/A) */
+    int32_t max_steps;          /* MAX_STEPS */
+    int32_t action_mode;        /* 0 single-flip Discrete(M+1), 1 multi-flip MultiDiscrete([2]*M) */
+    int32_t reward_mode;        /* MSAT_REWARD_* */
+    int32_t obs_dtype;          /* MSAT_OBS_* */
+    int32_t num_problems;       /* N instances in the device problem pool */
+    float r_clause;             /* PBRS only */
+    float r_sat;                /* PBRS only */
+    float gamma;                /* PBRS only */
+} msat_env_desc;
+
+/* Device-resident batch state (structure of arrays, leading dim B). */
+typedef struct msat_env_state {
+    uint8_t *assign;      /* (B,V)   variable_assignments in {0,1}           */
+    uint8_t *clause_sat;  /* (B,C)   clauses_satisfied_status                */
+    uint8_t *clause_ntrue;/* (B,C)   #true literals per clause (nullable)    */
+    int32_t *num_unsat;   /* (B,)    num_unsatisfied                         */
+    int32_t *step;        /* (B,)    step                                    */
+    uint8_t *done;        /* (B,)    done (every agent shares it)            */
+    int32_t *problem_idx; /* (B,)    row of the problem pool this env solves */
+    uint32_t *nbr_mask;   /* (B,A,W) neighbour bitmask, W = ceil(V/32)       */
+} msat_env_state;
+
+/* Step outputs that are NOT state (they describe the transition that was taken). */
+typedef struct msat_step_out {
+    float *reward;          /* (B,)  team reward (identical for every agent)        */
+    uint8_t *done;          /* (B,)  dones["__all__"] of the step (pre-reset)        */
+    uint8_t *solved;        /* (B,)  infos["solved"]                                 */
+    int32_t *num_unsat;     /* (B,)  infos["num_unsatisfied"]  (nullable)            */
+    int32_t *episode_step;  /* (B,)  infos["episode_step"]     (nullable)            */
+} msat_step_out;
+
+const char *msat_last_error(void);
+int msat_version(void);
+
+/* Pack an int32 literal tensor (N,C,K) (signed, 1-based, 0 = null literal) into
+ * the device pool layout uint16 (N,C,4).  Literals with |l| > V set *err_flag
+ * (device int32, caller zeroes it) to 1. */
+int msat_pool_pack(const int32_t *lits, int32_t num_problems, int32_t num_clauses,
+                   int32_t clause_width, int32_t num_vars, uint16_t *pool,
+                   int32_t *err_flag, void *stream);
+
+/* Reset the envs with reset_mask[b] != 0 (NULL: all envs).
+ * new_problem_idx (B,) and new_assign (B,V) are explicit inputs for exact-parity
+ * runs; when NULL they are drawn from the counter-based RNG (Philox4x32-10 keyed
+ * by seed, counter=(rng_counter, env)).  Writes every state field of the reset
+ * envs (step=0, done=0) and their observations obs (B,A,D), D = 2V+C. */
+int msat_env_reset(const msat_env_desc *desc, const uint16_t *pool,
+                   const msat_env_state *state, const uint8_t *reset_mask,
+                   const int32_t *new_problem_idx, const uint8_t *new_assign,
+                   uint64_t seed, uint64_t rng_counter, void *obs, void *stream);
+
+/* One batched SATEnv.step_env.  actions: (B,A) int32 (mode 0) or (B,A,M) int32
+ * (mode 1).  autoreset=0: pure step_env (state/obs are the stepped ones).
+ * autoreset=1: the rollout's auto-reset — envs whose step is done are reset
+ * (problem index / assignment from the explicit arrays or the RNG, exactly as
+ * msat_env_reset) and state/obs hold the post-reset values, while `out` holds
+ * the pre-reset reward/done/info of the step, as in the reference rollout. */
+int msat_env_step(const msat_env_desc *desc, const uint16_t *pool,
+                  const msat_env_state *state, const int32_t *actions,
+                  int32_t autoreset, const int32_t *new_problem_idx,
+                  const uint8_t *new_assign, uint64_t seed, uint64_t rng_counter,
+                  const msat_step_out *out, void *obs, void *stream);
+
+/* SATEnv.get_obs (env:345-398) of the current state, without changing it. */
+int msat_env_obs(const msat_env_desc *desc, const uint16_t *pool,
+                 const msat_env_state *state, void *obs, void *stream);
+
+/* Materialise the reference's per-env static mask tensors (cold path):
+ * agent_clause_masks (B,A,C) int32 +-1, agent_neighbor_masks (B,A,V) int32 +-1,
+ * literal_to_agent_idx (B,C,K) int32.  Any output pointer may be NULL. */
+int msat_env_masks(const msat_env_desc *desc, const uint16_t *pool,
+                   const msat_env_state *state, int32_t *agent_clause_masks,
+                   int32_t *agent_neighbor_masks, int32_t *literal_to_agent_idx,
+                   void *stream);
+
+/* Dynamic clause features (B,C,3) float32 = [is_sat, ntrue/3, 1]. */
+int msat_clause_features(const msat_env_desc *desc, const msat_env_state *state,
+                         float *clause_features, void *stream);
+
+/* Static variable features (N,V,3) float32 = [deg+/C, deg-/C, 0] per pool row. */
+int msat_static_var_features(const uint16_t *pool, int32_t num_problems,
+                             int32_t num_vars, int32_t num_clauses,
+                             float *var_features, void *stream);
+
+/* GAE over a (T,B) rollout + global normalisation over all T*B entries.
+ * reward: team reward with row stride reward_stride (elements) per (t,b)
+ * (reward[...,0] of the reference's (T,B,A) reward; stride 1 for a (T,B) tensor).
+ * done: (T,B) uint8.  value: (T,B).  last_val: (B,).
+ * gamma_lambda is GAMMA*GAE_LAMBDA rounded once to float32 (the reference
+ * multiplies the two Python floats before the fp32 arithmetic).
+ * advantages/targets: (T,B) outputs (advantages normalised when normalize!=0,
+ * targets = raw advantages + value).  workspace: >= msat_gae_workspace_bytes(T,B)
+ * bytes; after the call workspace holds (double) the mean and the std+1e-8 used. */
+size_t msat_gae_workspace_bytes(int32_t T, int32_t B);
+int msat_gae(int32_t T, int32_t B, const float *reward, int32_t reward_stride,
+             const uint8_t *done, const float *value, const float *last_val,
+             float gamma, float gamma_lambda, int32_t normalize, float *advantages,
+             float *targets, void *workspace, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MARLSAT_H */

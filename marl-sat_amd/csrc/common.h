@@ -1,0 +1,77 @@
+// Shared helpers for libmarlsat: error channel, launch checks, Philox RNG,
+// wave/block reductions.  gfx950 only (wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "marlsat.h"
+
+namespace msat {
+
+// ---------------------------------------------------------------- errors ----
+int fail(int code, const char *fmt, ...);  // sets the thread-local message, returns code
+int check_launch(const char *what);        // hipGetLastError -> MSAT_EHIP
+
+#define MSAT_REQUIRE(cond, ...)                      \
+    do {                                             \
+        if (!(cond)) return ::msat::fail(MSAT_EBADARG, __VA_ARGS__); \
+    } while (0)
+
+// --------------------------------------------------------------- Philox ----
+// Philox4x32-10 (Salmon et al., SC'11).  Mirrored bit-exactly by
+// oracle/rng.py so RNG-driven resets can be replayed on the host.
+__host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+__host__ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
+        const uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        k0 += W0;
+        k1 += W1;
+    }
+    return c;
+}
+
+// Stream layout used for resets of env b at call counter `ctr`:
+//   word block w=0, lane 0 -> problem index  ((u64)r * N) >> 32
+//   word block w=1+v/128, lane (v%128)/32, bit v%32 -> assignment of var v
+__host__ __device__ __forceinline__ uint4 reset_rng_block(uint64_t seed, uint64_t ctr, uint32_t env,
+                                                          uint32_t w) {
+    return philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), env, w), (uint32_t)seed,
+                         (uint32_t)(seed >> 32));
+}
+
+// ----------------------------------------------------------- reductions ----
+__device__ __forceinline__ int wave_sum_i32(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float wave_sum_f32(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max_f32(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+}  // namespace msat

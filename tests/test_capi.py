@@ -1,0 +1,88 @@
+"""CPU tests of the C-ABI boundary: the library loads, exports exactly what
+include/marlsat.h declares, and rejects bad arguments through the error channel
+(no GPU work is launched by these calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _header_symbols():
+    text = open(os.path.join(ROOT, "include", "marlsat.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(msat_[a-z_0-9]+)\s*\(", text, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from marlsat import _lib
+
+    syms = _header_symbols()
+    assert len(syms) >= 11
+    for s in syms:
+        assert hasattr(_lib.lib, s), s
+    assert sorted(_lib.EXPORTED) == syms
+    assert _lib.lib.msat_version() >= 1
+
+
+def test_nm_lists_c_abi_symbols():
+    from marlsat import _lib
+
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for s in _header_symbols():
+        assert re.search(rf"\bT {s}$", out, re.M), s
+
+
+def _desc(**kw):
+    from marlsat import _lib
+
+    d = dict(num_envs=4, num_vars=20, num_clauses=91, clause_width=3, num_agents=2, max_vars_per_agent=10,
+             max_steps=512, action_mode=0, reward_mode=0, obs_dtype=0, num_problems=1, r_clause=0.0, r_sat=1.0,
+             gamma=0.99)
+    d.update(kw)
+    return _lib.EnvDesc(**d)
+
+
+@pytest.mark.parametrize("bad,msg", [
+    (dict(num_vars=0), "num_vars"),
+    (dict(clause_width=4), "clause_width"),
+    (dict(num_agents=1001), "num_agents"),
+    (dict(max_vars_per_agent=9), "max_vars_per_agent"),
+    (dict(action_mode=2), "action_mode"),
+    (dict(obs_dtype=3), "obs_dtype"),
+])
+def test_bad_desc_is_rejected_with_message(bad, msg):
+    from marlsat import _lib
+
+    st = _lib.EnvStateC(*([1] * 8))  # never dereferenced: validation fails first
+    rc = _lib.lib.msat_env_reset(ctypes.byref(_desc(**bad)), 1, ctypes.byref(st), None, None, None, 0, 0, 1, None)
+    assert rc == -1
+    assert msg in _lib.lib.msat_last_error().decode()
+
+
+def test_null_state_pointer_rejected():
+    from marlsat import _lib
+
+    st = _lib.EnvStateC(1, 1, None, 1, 1, 1, 1, None)  # nbr_mask missing
+    rc = _lib.lib.msat_env_reset(ctypes.byref(_desc()), 1, ctypes.byref(st), None, None, None, 0, 0, 1, None)
+    assert rc == -1 and "NULL" in _lib.lib.msat_last_error().decode()
+
+
+def test_gae_bad_dims_rejected():
+    from marlsat import _lib
+
+    rc = _lib.lib.msat_gae(0, 4, 1, 1, 1, 1, 1, 0.99, 0.9, 1, 1, 1, 1, None)
+    assert rc == -1 and "bad dims" in _lib.lib.msat_last_error().decode()
+    assert _lib.lib.msat_gae_workspace_bytes(8, 1000) >= 16 * 4
+
+
+def test_product_path_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "marl-sat_amd", "marlsat")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f

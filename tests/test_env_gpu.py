@@ -1,0 +1,267 @@
+"""GPU parity: the HIP env kernels (through the C-ABI) vs the NumPy oracle.
+
+Bit-exact on every integer/byte output (obs, clause status, counts, masks,
+assignments, steps, dones) and on the fp32 rewards / features.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle.rng import reset_draws
+from oracle.sat_env import OracleSATEnv
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [  # name, V, C, vars_per_agent, B, N
+    ("uf20", 20, 91, 10, 8, 6),
+    ("uf50", 50, 218, 10, 12, 6),
+    ("uf100", 100, 430, 10, 12, 6),
+    ("uf200", 200, 860, 8, 12, 6),
+    ("rem23", 23, 97, 10, 7, 5),  # 3 agents of 8,8,7: padded slots
+    ("auto21", 21, 80, None, 5, 4),  # auto grouping 6,5,5,5
+    ("one_agent", 12, 40, 12, 3, 3),
+]
+
+
+def _pool(V, C, N, k=3, seed0=0):
+    from marlsat.utils.generate_cnf_dataset import generate_sat_clauses
+
+    return np.stack([generate_sat_clauses(V, C, k, seed=seed0 + i) for i in range(N)])
+
+
+def _mk(V, C, vpa, max_steps=6, **kw):
+    from marlsat import SATEnv
+
+    env = SATEnv(V, C, max_steps=max_steps, vars_per_agent=vpa, **kw)
+    ora = OracleSATEnv(V, C, max_steps=max_steps, vars_per_agent=vpa,
+                       reward_mode=kw.get("reward_mode", 0), action_mode=kw.get("action_mode", 0),
+                       r_clause=kw.get("r_clause", 0.02), r_sat=kw.get("r_sat", 1.0), gamma=kw.get("gamma", 0.99))
+    return env, ora
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _check_state(env, st, ost, ctx=""):
+    np.testing.assert_array_equal(_np(st.variable_assignments), ost.variable_assignments, err_msg=ctx)
+    np.testing.assert_array_equal(_np(st.clauses_satisfied_status).astype(bool), ost.clauses_satisfied_status,
+                                  err_msg=ctx)
+    np.testing.assert_array_equal(_np(st.num_unsatisfied), ost.num_unsatisfied, err_msg=ctx)
+    np.testing.assert_array_equal(_np(st.step), ost.step, err_msg=ctx)
+    np.testing.assert_array_equal(_np(st.done), ost.done, err_msg=ctx)
+    np.testing.assert_array_equal(_np(st.clauses), ost.clauses, err_msg=ctx)
+    np.testing.assert_array_equal(_np(st.agent_clause_masks), ost.agent_clause_masks, err_msg=ctx)
+    np.testing.assert_array_equal(_np(st.agent_neighbor_masks), ost.agent_neighbor_masks, err_msg=ctx)
+    np.testing.assert_array_equal(_np(st.literal_to_agent_idx), ost.literal_to_agent_idx, err_msg=ctx)
+
+
+def _random_actions(rng, env, B):
+    A, M = env.num_agents, env.max_vars_per_agent
+    if env.action_mode == 0:
+        return rng.integers(0, M + 1, size=(B, A)).astype(np.int32)
+    return rng.integers(0, 2, size=(B, A, M)).astype(np.int32)
+
+
+@pytest.mark.parametrize("name,V,C,vpa,B,N", CONFIGS)
+def test_reset_matches_oracle(name, V, C, vpa, B, N):
+    env, ora = _mk(V, C, vpa)
+    pool = _pool(V, C, N)
+    rng = np.random.default_rng(1)
+    pidx = rng.integers(0, N, B).astype(np.int32)
+    x = rng.integers(0, 2, (B, V)).astype(np.uint8)
+    obs, st = env.reset_from_pool(env.make_pool(pool), B, problem_idx=pidx, assignments=x)
+    oobs, ost = ora.reset(pool[pidx], x.astype(np.int32))
+    np.testing.assert_array_equal(_np(obs), oobs)
+    _check_state(env, st, ost, name)
+    np.testing.assert_array_equal(_np(env.clause_features(st)), ora.clause_features(ost))
+    np.testing.assert_array_equal(_np(st.pool.static_var_features()), ora.static_var_features(pool))
+    # get_obs recomputes the same observation without touching the state
+    np.testing.assert_array_equal(_np(env.get_obs(st).tensor), oobs)
+    _check_state(env, st, ost, name + " after get_obs")
+
+
+@pytest.mark.parametrize("name,V,C,vpa,B,N", CONFIGS)
+@pytest.mark.parametrize("autoreset", [False, True])
+def test_rollout_matches_oracle(name, V, C, vpa, B, N, autoreset):
+    env, ora = _mk(V, C, vpa, max_steps=5)
+    pool = _pool(V, C, N)
+    rng = np.random.default_rng(2)
+    pidx = rng.integers(0, N, B).astype(np.int32)
+    x = rng.integers(0, 2, (B, V)).astype(np.uint8)
+    dpool = env.make_pool(pool)
+    obs, st = env.reset_from_pool(dpool, B, problem_idx=pidx, assignments=x)
+    _, ost = ora.reset(pool[pidx], x.astype(np.int32))
+    for t in range(12):
+        a = _random_actions(rng, env, B)
+        if autoreset:
+            npidx = rng.integers(0, N, B).astype(np.int32)
+            nx = rng.integers(0, 2, (B, V)).astype(np.uint8)
+            obs, out = env.step_raw(st, torch.from_numpy(a).cuda(), autoreset=True, problem_idx=npidx,
+                                    assignments=nx)
+            oobs, ost, r, d, info = ora.step_autoreset(ost, a, pool[npidx], nx.astype(np.int32))
+        else:
+            obs, out = env.step_raw(st, torch.from_numpy(a).cuda())
+            oobs, ost, r, d, info = ora.step(ost, a)
+        ctx = f"{name} t={t}"
+        np.testing.assert_array_equal(_np(obs), oobs, err_msg=ctx)
+        np.testing.assert_array_equal(_np(out["reward"]), r, err_msg=ctx)
+        np.testing.assert_array_equal(_np(out["done"]).astype(bool), d, err_msg=ctx)
+        np.testing.assert_array_equal(_np(out["solved"]).astype(bool), info["solved"], err_msg=ctx)
+        np.testing.assert_array_equal(_np(out["num_unsatisfied"]), info["num_unsatisfied"], err_msg=ctx)
+        np.testing.assert_array_equal(_np(out["episode_step"]), info["episode_step"], err_msg=ctx)
+        _check_state(env, st, ost, ctx)
+
+
+def test_step_env_functional_api_and_solve():
+    """Drive a uf20 instance into its (reference-checker) solution: reward 1, done, solved."""
+    g = np.load(f"{GOLDEN}/clause_truth.npz", allow_pickle=False)
+    cl, sol = g["c0_clauses"], g["c0_x"][6]  # index 6 = brute-force satisfying assignment
+    assert g["c0_formula_sat"][6] == 1
+    env, ora = _mk(20, 91, 10, max_steps=512)
+    x0 = sol.copy()
+    x0[3] ^= 1  # agent 0 (vars 0-9) must flip local var 3
+    obs, st = env.reset(cl[None], assignments=x0[None])
+    acts = {"agent_0": torch.tensor([3], device="cuda"), "agent_1": torch.tensor([10], device="cuda")}  # 10 = no-op
+    obs2, st2, rewards, dones, infos = env.step_env(None, st, acts)
+    assert float(rewards["agent_0"][0]) == 1.0 and bool(dones["__all__"][0]) and bool(infos["solved"][0])
+    assert int(st.step[0]) == 0 and int(st2.step[0]) == 1  # functional: input state untouched
+    oobs, ost = ora.reset(cl[None], x0[None].astype(np.int32))
+    oobs2, _, r, d, _ = ora.step(ost, np.array([[3, 10]]))
+    np.testing.assert_array_equal(_np(obs2.tensor), oobs2)
+    np.testing.assert_array_equal(_np(obs2["agent_1"]), oobs2[:, 1])
+    status, nun = env._calculate_satisfaction_explicit(sol, cl)
+    assert int(nun) == 0 and bool(status.all())
+
+
+@pytest.mark.parametrize("reward_mode", [0, 1])
+@pytest.mark.parametrize("action_mode", [0, 1])
+def test_modes_match_oracle(reward_mode, action_mode):
+    V, C, B, N = 30, 126, 9, 4
+    env, ora = _mk(V, C, 7, max_steps=4, reward_mode=reward_mode, action_mode=action_mode, r_clause=0.03,
+                   r_sat=5.0, gamma=0.97)
+    pool = _pool(V, C, N, seed0=50)
+    rng = np.random.default_rng(3)
+    pidx = rng.integers(0, N, B).astype(np.int32)
+    x = rng.integers(0, 2, (B, V)).astype(np.uint8)
+    obs, st = env.reset_from_pool(env.make_pool(pool), B, problem_idx=pidx, assignments=x)
+    _, ost = ora.reset(pool[pidx], x.astype(np.int32))
+    for t in range(9):
+        a = _random_actions(rng, env, B)
+        npidx = rng.integers(0, N, B).astype(np.int32)
+        nx = rng.integers(0, 2, (B, V)).astype(np.uint8)
+        obs, out = env.step_raw(st, torch.from_numpy(a).cuda(), autoreset=True, problem_idx=npidx, assignments=nx)
+        oobs, ost, r, d, info = ora.step_autoreset(ost, a, pool[npidx], nx.astype(np.int32))
+        np.testing.assert_array_equal(_np(obs), oobs)
+        np.testing.assert_array_equal(_np(out["reward"]), r)  # fp32, same op order -> bitwise
+        _check_state(env, st, ost, f"t={t}")
+
+
+def test_quirk_literals_and_narrow_clauses():
+    """Literal 0 (null), repeated vars, K=2 and K=1 pools, odd partition with padded agent slots."""
+    env, ora = _mk(7, 5, 3, max_steps=3)  # 3 agents: 3,2,2 -> padded slots on agents 1,2
+    cl = np.array([[[1, -2, 0], [3, 3, -1], [-4, 2, 7], [0, 0, 0], [-6, 5, 2]]], np.int32)
+    cl = np.repeat(cl, 4, 0)
+    cl[1, 0] = [5, 0, -7]
+    x = np.random.default_rng(4).integers(0, 2, (4, 7)).astype(np.uint8)
+    obs, st = env.reset(cl, assignments=x)
+    oobs, ost = ora.reset(cl, x.astype(np.int32))
+    np.testing.assert_array_equal(_np(obs.tensor), oobs)
+    _check_state(env, st, ost, "quirk")
+    for K in (1, 2):
+        env2, ora2 = _mk(9, 14, 4)
+        pool = _pool(9, 14, 3, k=K, seed0=9)
+        xx = np.random.default_rng(K).integers(0, 2, (3, 9)).astype(np.uint8)
+        o, s = env2.reset(pool, assignments=xx)
+        oo, os_ = ora2.reset(pool, xx.astype(np.int32))
+        np.testing.assert_array_equal(_np(o.tensor), oo)
+        _check_state(env2, s, os_, f"K={K}")
+
+
+def test_negative_and_out_of_range_actions():
+    env, ora = _mk(23, 97, 10)
+    pool = _pool(23, 97, 2)
+    x = np.zeros((2, 23), np.uint8)
+    obs, st = env.reset(pool, assignments=x)
+    _, ost = ora.reset(pool, x.astype(np.int32))
+    a = np.array([[-1, -9, 7], [9, 100, -3]], np.int32)  # agent 2 has 7 vars (slot 7 padded)
+    obs, out = env.step_raw(st, torch.from_numpy(a).cuda())
+    oobs, ost, *_ = ora.step(ost, a)
+    np.testing.assert_array_equal(_np(obs), oobs)
+    _check_state(env, st, ost)
+
+
+def test_rng_reset_replays_on_host():
+    from marlsat.random import Key
+
+    V, C, B, N = 100, 430, 64, 9
+    env, ora = _mk(V, C, 10)
+    pool = _pool(V, C, N)
+    key = Key(0xDEADBEEF12345, 77)
+    obs, st = env.reset_from_pool(env.make_pool(pool), B, key)
+    pidx, x = reset_draws(key.seed, key.counter, B, V, N)
+    np.testing.assert_array_equal(_np(st.problem_idx), pidx)
+    oobs, ost = ora.reset(pool[pidx], x.astype(np.int32))
+    np.testing.assert_array_equal(_np(obs), oobs)
+    _check_state(env, st, ost)
+    # auto-reset with RNG draws: done envs get reset_draws(seed, counter) rows
+    env5, ora5 = _mk(V, C, 10, max_steps=1)  # every step times out
+    obs, st = env5.reset_from_pool(env5.make_pool(pool), B, problem_idx=pidx, assignments=x)
+    a = np.full((B, env5.num_agents), 10, np.int32)
+    k2 = Key(99, 5)
+    obs, out = env5.step_raw(st, torch.from_numpy(a).cuda(), autoreset=True, key=k2)
+    p2, x2 = reset_draws(k2.seed, k2.counter, B, V, N)
+    _, ost = ora5.reset(pool[pidx], x.astype(np.int32))
+    oobs, ost, *_ = ora5.step_autoreset(ost, a, pool[p2], x2.astype(np.int32))
+    np.testing.assert_array_equal(_np(obs), oobs)
+    _check_state(env5, st, ost)
+
+
+def test_int8_obs_equals_int32_obs():
+    V, C, B = 50, 218, 33
+    pool = _pool(V, C, 4)
+    x = np.random.default_rng(5).integers(0, 2, (B, V)).astype(np.uint8)
+    pidx = np.arange(B) % 4
+    e32, _ = _mk(V, C, 10)
+    e8, _ = _mk(V, C, 10, obs_dtype=torch.int8)
+    o32, s32 = e32.reset_from_pool(e32.make_pool(pool), B, problem_idx=pidx, assignments=x)
+    o8, s8 = e8.reset_from_pool(e8.make_pool(pool), B, problem_idx=pidx, assignments=x)
+    assert o8.dtype == torch.int8
+    np.testing.assert_array_equal(_np(o8).astype(np.int32), _np(o32))
+    a = torch.randint(0, 11, (B, 5), dtype=torch.int32, device="cuda")
+    o32, _ = e32.step_raw(s32, a, autoreset=True)
+    o8, _ = e8.step_raw(s8, a, autoreset=True)
+    np.testing.assert_array_equal(_np(o8).astype(np.int32), _np(o32))
+
+
+def test_full_size_uf200_x4096_properties_and_sampled_parity():
+    """BASELINE config (4): uf200-860, A=25, B=4096, RNG auto-reset — invariants on every env,
+    exact oracle replay on a sample of envs."""
+    from marlsat.random import Key
+
+    V, C, B, N = 200, 860, 4096, 64
+    env, ora = _mk(V, C, 8, max_steps=3)
+    pool = _pool(V, C, N, seed0=3000)
+    dpool = env.make_pool(pool)
+    obs, st = env.reset_from_pool(dpool, B, Key(1, 0))
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    sample = np.random.default_rng(6).choice(B, 48, replace=False)
+    for t in range(5):
+        pidx0, x0 = _np(st.problem_idx).copy(), _np(st.variable_assignments).copy()
+        step0 = _np(st.step).copy()
+        a = torch.randint(0, 9, (B, 25), generator=gen, device="cuda", dtype=torch.int32)
+        key = Key(1, t + 1)
+        obs, out = env.step_raw(st, a, autoreset=True, key=key)
+        sat = st.clauses_satisfied_status.int()
+        assert torch.equal(C - sat.sum(1), st.num_unsatisfied)
+        assert torch.equal(st.clause_ntrue.gt(0).int(), sat)
+        # replay the sampled envs on the oracle
+        _, ost = ora.reset(pool[pidx0[sample]], x0[sample].astype(np.int32))
+        ost.step = step0[sample]
+        p2, x2 = reset_draws(key.seed, key.counter, B, V, N)
+        oobs, ost, r, d, info = ora.step_autoreset(ost, _np(a)[sample], pool[p2[sample]],
+                                                   x2[sample].astype(np.int32))
+        np.testing.assert_array_equal(_np(obs)[sample], oobs)
+        np.testing.assert_array_equal(_np(out["done"])[sample].astype(bool), d)
+        np.testing.assert_array_equal(_np(st.variable_assignments)[sample], ost.variable_assignments)
