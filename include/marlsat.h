@@ -13,6 +13,8 @@
  * Reference interfaces replaced (paths relative to kongqg/marl-sat):
  *   msat_pool_pack           <- jnp.abs(clauses)-1 literal decoding shared by
  *                               src/envs/multi_agent_sat_env.py:135-144 and :100
+ *   msat_pool_agent_tables   <- _compute_observation_maps  src/envs/multi_agent_sat_env.py:99-128
+ *                               (hoisted from every reset to once per pool instance)
  *   msat_env_reset           <- SATEnv.reset               src/envs/multi_agent_sat_env.py:158-181
  *                               (+ _compute_observation_maps :99-128, get_obs :345-398)
  *   msat_env_step            <- SATEnv.step_env            src/envs/multi_agent_sat_env.py:225-284
@@ -77,6 +79,15 @@ typedef struct msat_env_desc {
     float gamma;                /* PBRS only */
 } msat_env_desc;
 
+/* Device problem pool: packed literals + per-instance agent tables.  The tables
+ * depend only on the instance and the agent partition (the reference recomputes
+ * them on every reset, env:99-128), so they are built once per pool. */
+typedef struct msat_pool {
+    const uint16_t *lits; /* (N,C,4)  packed literal codes                          */
+    const uint32_t *rel;  /* (N,A,WC) agent-clause relation bits, WC = 2*ceil(C/64) */
+    const uint32_t *nbr;  /* (N,A,WV) agent neighbour-var bits,  WV = 2*ceil(V/64)  */
+} msat_pool;
+
 /* Device-resident batch state (structure of arrays, leading dim B). */
 typedef struct msat_env_state {
     uint8_t *assign;      /* (B,V)   variable_assignments in {0,1}           */
@@ -86,7 +97,6 @@ typedef struct msat_env_state {
     int32_t *step;        /* (B,)    step                                    */
     uint8_t *done;        /* (B,)    done (every agent shares it)            */
     int32_t *problem_idx; /* (B,)    row of the problem pool this env solves */
-    uint32_t *nbr_mask;   /* (B,A,W) neighbour bitmask, W = ceil(V/32)       */
 } msat_env_state;
 
 /* Step outputs that are NOT state (they describe the transition that was taken). */
@@ -108,12 +118,18 @@ int msat_pool_pack(const int32_t *lits, int32_t num_problems, int32_t num_clause
                    int32_t clause_width, int32_t num_vars, uint16_t *pool,
                    int32_t *err_flag, void *stream);
 
+/* Build the per-instance agent tables of a packed pool for desc's partition
+ * (desc->num_problems rows): rel (N,A,WC) and nbr (N,A,WV) uint32 bit words.
+ * Reproduces _compute_observation_maps (env:99-128) incl. the literal-0 quirk. */
+int msat_pool_agent_tables(const msat_env_desc *desc, const uint16_t *lits,
+                           uint32_t *rel, uint32_t *nbr, void *stream);
+
 /* Reset the envs with reset_mask[b] != 0 (NULL: all envs).
  * new_problem_idx (B,) and new_assign (B,V) are explicit inputs for exact-parity
  * runs; when NULL they are drawn from the counter-based RNG (Philox4x32-10 keyed
  * by seed, counter=(rng_counter, env)).  Writes every state field of the reset
  * envs (step=0, done=0) and their observations obs (B,A,D), D = 2V+C. */
-int msat_env_reset(const msat_env_desc *desc, const uint16_t *pool,
+int msat_env_reset(const msat_env_desc *desc, const msat_pool *pool,
                    const msat_env_state *state, const uint8_t *reset_mask,
                    const int32_t *new_problem_idx, const uint8_t *new_assign,
                    uint64_t seed, uint64_t rng_counter, void *obs, void *stream);
@@ -124,20 +140,20 @@ int msat_env_reset(const msat_env_desc *desc, const uint16_t *pool,
  * (problem index / assignment from the explicit arrays or the RNG, exactly as
  * msat_env_reset) and state/obs hold the post-reset values, while `out` holds
  * the pre-reset reward/done/info of the step, as in the reference rollout. */
-int msat_env_step(const msat_env_desc *desc, const uint16_t *pool,
+int msat_env_step(const msat_env_desc *desc, const msat_pool *pool,
                   const msat_env_state *state, const int32_t *actions,
                   int32_t autoreset, const int32_t *new_problem_idx,
                   const uint8_t *new_assign, uint64_t seed, uint64_t rng_counter,
                   const msat_step_out *out, void *obs, void *stream);
 
 /* SATEnv.get_obs (env:345-398) of the current state, without changing it. */
-int msat_env_obs(const msat_env_desc *desc, const uint16_t *pool,
+int msat_env_obs(const msat_env_desc *desc, const msat_pool *pool,
                  const msat_env_state *state, void *obs, void *stream);
 
 /* Materialise the reference's per-env static mask tensors (cold path):
  * agent_clause_masks (B,A,C) int32 +-1, agent_neighbor_masks (B,A,V) int32 +-1,
  * literal_to_agent_idx (B,C,K) int32.  Any output pointer may be NULL. */
-int msat_env_masks(const msat_env_desc *desc, const uint16_t *pool,
+int msat_env_masks(const msat_env_desc *desc, const msat_pool *pool,
                    const msat_env_state *state, int32_t *agent_clause_masks,
                    int32_t *agent_neighbor_masks, int32_t *literal_to_agent_idx,
                    void *stream);

@@ -1,14 +1,19 @@
 // Batched multi-agent SAT environment on gfx950.
 //
-// One workgroup (256 threads = 4 waves) owns one environment for the whole
-// call: it stages the env's variables in LDS (assignment bit + owning agent,
-// 2 B/var), evaluates every clause once from the L2/MALL-resident packed
-// problem pool (8 B/clause: 4 x uint16 literal codes), reduces the
-// unsatisfied count with wave shuffles, optionally resets the env in place
-// (auto-reset) and finally streams the env's (A, 2V+C) observation block to
-// HBM with 16-byte stores.  The observation write is >90 % of the algorithmic
-// bytes of a step, so everything before it is organised to
-// leave the obs pass a pure LDS-read -> 16 B store stream.
+// One workgroup (kThreads lanes) owns one environment for the whole call:
+//   1. assignment -> LDS bit words (one ballot per 64 vars), agents' flips as
+//      LDS atomic XORs;
+//   2. every clause evaluated once from the L2/MALL-resident packed pool
+//      (8 B/clause), clause status -> LDS bit words by wave ballot, the
+//      unsatisfied count by popcount of the same ballots;
+//   3. done / reward / info, and (auto-reset) an in-place reset of done envs;
+//   4. the instance's agent tables (relation + neighbour bits, built once per
+//      pool instance) staged into LDS;
+//   5. the env's (A, 2V+C) observation block streamed to HBM with 16 B stores,
+//      every 4-element chunk assembled from two LDS words by bit extraction.
+// The observation write is >90 % of a step's algorithmic bytes (SURVEY.md
+// §8(d)); everything before it is sized to keep the obs pass a pure
+// LDS-read -> 16 B store stream.
 //
 // Reference semantics (kongqg/marl-sat, src/envs/multi_agent_sat_env.py):
 //   flip decode             :230-250
@@ -17,24 +22,27 @@
 //   reset + masks           :158-181, :99-128
 //   get_obs                 :345-398
 //   rollout auto-reset      src/learners/mappo_gnn_sat_learner.py:422-464
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace msat {
 
 constexpr int kThreads = 256;
-constexpr uint32_t kNoAgent = 0x3FFu;
 
 struct EnvParams {
-    int B, V, C, K, A, M, W, D;
+    int B, V, C, K, A, M, D;
+    int WV, WC;     // uint32 words per agent row of the nbr / rel tables (even: whole 64-bit ballots)
     int base, rem;  // agent i owns [i*base + min(i,rem), +base+(i<rem))
     int max_steps, action_mode, reward_mode, N;
     float r_clause, r_sat, gamma;
+    int ablate;  // diagnostics only (MARLSAT_ABLATE): 0 full, 1 constant obs, 2 no obs write
 };
 
 enum : int { kModeReset = 0, kModeStep = 1, kModeStepAutoReset = 2, kModeObs = 3 };
 
-__device__ __forceinline__ int agent_lo(const EnvParams &p, int i) { return i * p.base + min(i, p.rem); }
-__device__ __forceinline__ int agent_size(const EnvParams &p, int i) { return p.base + (i < p.rem ? 1 : 0); }
+__host__ __device__ __forceinline__ int agent_lo(const EnvParams &p, int i) { return i * p.base + (i < p.rem ? i : p.rem); }
+__host__ __device__ __forceinline__ int agent_size(const EnvParams &p, int i) { return p.base + (i < p.rem ? 1 : 0); }
 
 __device__ __forceinline__ int agent_of_var(const EnvParams &p, int v) {
     const int split = p.rem * (p.base + 1);
@@ -42,114 +50,128 @@ __device__ __forceinline__ int agent_of_var(const EnvParams &p, int v) {
     return p.rem + (v - split) / p.base;  // base > 0 whenever v >= split
 }
 
-// LDS image of one environment.
+// LDS image of one environment (all uint32 words).
 struct EnvLds {
-    uint32_t *clinfo;  // [C]   a0 | a1<<10 | a2<<20 | nullLit<<30 | sat<<31
-    uint32_t *nbr;     // [A*W] neighbour bits
-    int *red;          // [16]  reduction / broadcast scratch
-    uint16_t *vinfo;   // [V]   agent | x<<15
+    uint32_t *x;    // [WV]    assignment bits
+    uint32_t *sat;  // [WC]    clause-satisfied bits
+    uint32_t *rel;  // [A*WC]  agent-clause relation bits of the env's instance
+    uint32_t *nbr;  // [A*WV]  agent neighbour bits of the env's instance
+    int *red;       // [16]    reduction / broadcast scratch
 };
 
-__device__ __forceinline__ EnvLds carve(unsigned char *smem, const EnvParams &p) {
+__host__ __device__ __forceinline__ size_t env_lds_words(const EnvParams &p) {
+    return (size_t)p.WV + p.WC + (size_t)p.A * (p.WC + p.WV) + 16;
+}
+
+__device__ __forceinline__ EnvLds carve(uint32_t *smem, const EnvParams &p) {
     EnvLds l;
-    l.clinfo = reinterpret_cast<uint32_t *>(smem);
-    l.nbr = l.clinfo + p.C;
-    l.red = reinterpret_cast<int *>(l.nbr + p.A * p.W);
-    l.vinfo = reinterpret_cast<uint16_t *>(l.red + 16);
+    l.x = smem;
+    l.sat = l.x + p.WV;
+    l.rel = l.sat + p.WC;
+    l.nbr = l.rel + (size_t)p.A * p.WC;
+    l.red = reinterpret_cast<int *>(l.nbr + (size_t)p.A * p.WV);
     return l;
 }
 
-// Evaluate every clause of pool row `pidx` against the assignment in LDS.
-// Writes clinfo, clause_sat (and ntrue), accumulates the unsat count (and,
-// for PBRS, newly-satisfied count) into red[0] / red[1]; when `build_nbr`,
-// ORs the neighbour bits of every agent related to each clause.
-template <bool kPbrs, bool kBuildNbr>
-__device__ __forceinline__ void eval_clauses(const EnvParams &p, const EnvLds &l,
-                                             const uint16_t *__restrict__ pool, int pidx,
-                                             uint8_t *__restrict__ sat_g, uint8_t *__restrict__ ntrue_g) {
-    const uint64_t *prow = reinterpret_cast<const uint64_t *>(pool) + (size_t)pidx * p.C;
-    int unsat = 0, newly = 0;
-    for (int c = threadIdx.x; c < p.C; c += kThreads) {
-        const uint64_t w = prow[c];  // pool rows are shared by many envs: keep them cached
-        uint32_t info = 0, nullLit = 0;
-        int ntrue = 0;
-        int vars[3];
-        uint32_t ags[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const uint32_t lit = (uint32_t)(w >> (16 * j)) & 0xFFFFu;
-            uint32_t ag = kNoAgent;
-            int var = -1;
-            if (lit < MSAT_LIT_ABSENT) {
-                var = (int)(lit >> 1);
-                const uint32_t vi = l.vinfo[var];
-                ntrue += (int)(((vi >> 15) ^ lit) & 1u);
-                ag = vi & kNoAgent;
-            } else if (lit == MSAT_LIT_NULL) {
-                nullLit = 1;
-            }
-            vars[j] = var;
-            ags[j] = ag;
-            info |= ag << (10 * j);
-        }
-        const uint32_t sat = ntrue > 0 ? 1u : 0u;
-        info |= (nullLit << 30) | (sat << 31);
-        l.clinfo[c] = info;
-        if (kPbrs) newly += (int)(sat & (sat_g[c] ^ 1u));
-        sat_g[c] = (uint8_t)sat;
-        if (ntrue_g) ntrue_g[c] = (uint8_t)ntrue;
-        unsat += (int)(sat ^ 1u);
-        if (kBuildNbr) {
-            // vars of a related clause that the agent does not own are its neighbours (env:115-126)
+__device__ __forceinline__ uint32_t bit(const uint32_t *w, int i) { return (w[i >> 5] >> (i & 31)) & 1u; }
+
+// Assignment bytes -> LDS bit words, one ballot per 64 vars.
+__device__ __forceinline__ void load_x_bits(const EnvParams &p, const EnvLds &l, const uint8_t *__restrict__ xg) {
+    const int lane = threadIdx.x & 63;
+    for (int v0 = threadIdx.x & ~63; v0 < p.WV * 32; v0 += kThreads) {
+        const int v = v0 + lane;
+        const uint64_t m = __ballot(v < p.V && (xg[v] & 1u));
+        if (lane < 2) l.x[(v0 >> 5) + lane] = (uint32_t)(m >> (32 * lane));
+    }
+}
+
+// Evaluate every clause of pool row `pidx` against l.x: clause bits -> l.sat,
+// bytes -> sat_g / ntrue_g, unsat count (and PBRS newly-satisfied) -> red[0] / red[1].
+template <bool kPbrs>
+__device__ __forceinline__ void eval_clauses(const EnvParams &p, const EnvLds &l, const uint16_t *__restrict__ lits,
+                                             int pidx, uint8_t *__restrict__ sat_g, uint8_t *__restrict__ ntrue_g) {
+    const uint64_t *prow = reinterpret_cast<const uint64_t *>(lits) + (size_t)pidx * p.C;
+    const int lane = threadIdx.x & 63;
+    int unsat = 0, newly = 0;  // wave-uniform
+    for (int c0 = threadIdx.x & ~63; c0 < p.WC * 32; c0 += kThreads) {
+        const int c = c0 + lane;
+        uint32_t sat = 0, ntrue = 0, old = 0;
+        const bool live = c < p.C;
+        if (live) {
+            const uint64_t w = prow[c];  // pool rows are shared by many envs: keep them cached
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
-                if (ags[j] == kNoAgent) continue;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    if (k == j || vars[k] < 0 || ags[k] == ags[j]) continue;
-                    atomicOr(&l.nbr[ags[j] * p.W + (vars[k] >> 5)], 1u << (vars[k] & 31));
-                }
+                const uint32_t lit = (uint32_t)(w >> (16 * j)) & 0xFFFFu;
+                if (lit < MSAT_LIT_ABSENT) ntrue += (bit(l.x, (int)(lit >> 1)) ^ lit) & 1u;
             }
-            if (nullLit && p.rem > 0) {
-                // Reference quirk: literal 0 decodes to var index -1, which equals the -1
-                // padding of agent_vars rows, so the clause is "related" to every agent
-                // that owns fewer than M vars (agents i >= rem).
-                for (int i = p.rem; i < p.A; ++i) {
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        if (vars[k] < 0 || ags[k] == (uint32_t)i) continue;
-                        atomicOr(&l.nbr[i * p.W + (vars[k] >> 5)], 1u << (vars[k] & 31));
-                    }
-                }
-            }
+            sat = ntrue ? 1u : 0u;
+            if (kPbrs) old = sat_g[c];
+            sat_g[c] = (uint8_t)sat;
+            if (ntrue_g) ntrue_g[c] = (uint8_t)ntrue;
         }
+        const uint64_t ms = __ballot(sat);
+        if (lane < 2) l.sat[(c0 >> 5) + lane] = (uint32_t)(ms >> (32 * lane));
+        unsat += __popcll(__ballot(live && !sat));
+        if (kPbrs) newly += __popcll(__ballot(sat && !old));
     }
-    unsat = wave_sum_i32(unsat);
-    if (kPbrs) newly = wave_sum_i32(newly);
-    if ((threadIdx.x & 63) == 0) {
+    if (lane == 0) {
         atomicAdd(&l.red[0], unsat);
         if (kPbrs) atomicAdd(&l.red[1], newly);
     }
 }
 
-// One observation element (env:345-398): own vars | clause status | neighbour vars.
-__device__ __forceinline__ int obs_value(const EnvParams &p, const EnvLds &l, int i, int k) {
-    if (k < p.V) {
-        const int lo = agent_lo(p, i);
-        return (k >= lo && k < lo + agent_size(p, i)) ? (int)(l.vinfo[k] >> 15) : -1;
-    }
+// ---------------------------------------------------------------- obs pass --
+// Element (i, k) of agent i's row (env:345-398): own vars | clause status | neighbour vars.
+__device__ __forceinline__ int obs_elem(const EnvParams &p, const EnvLds &l, int i, int k) {
+    if (k < p.V) return ((unsigned)(k - agent_lo(p, i)) < (unsigned)agent_size(p, i)) ? (int)bit(l.x, k) : -1;
     k -= p.V;
-    if (k < p.C) {
-        const uint32_t info = l.clinfo[k];
-        const uint32_t ui = (uint32_t)i;
-        const bool small = (p.rem > 0) && (i >= p.rem);
-        const bool rel = ((info & kNoAgent) == ui) | (((info >> 10) & kNoAgent) == ui) |
-                         (((info >> 20) & kNoAgent) == ui) | (small && ((info >> 30) & 1u));
-        return rel ? (int)(info >> 31) : -1;
-    }
+    if (k < p.C) return bit(l.rel + i * p.WC, k) ? (int)bit(l.sat, k) : -1;
     k -= p.C;
-    const bool nb = (l.nbr[i * p.W + (k >> 5)] >> (k & 31)) & 1u;
-    return nb ? (int)(l.vinfo[k] >> 15) : -1;
+    return bit(l.nbr + i * p.WV, k) ? (int)bit(l.x, k) : -1;
+}
+
+// 4 consecutive elements (i, k..k+3) of one row.  Fast path when they sit in one
+// region and one 32-bit word: two LDS words, four bit extractions.
+__device__ __forceinline__ void obs_quad(const EnvParams &p, const EnvLds &l, int i, int k, int (&v)[4]) {
+    uint32_t m = 0, x = 0;
+    bool fast = false;
+    if (k + 4 <= p.V) {
+        const int s = k & 31;
+        if (s <= 28) {
+            const int lo = agent_lo(p, i), n = agent_size(p, i);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) m |= ((unsigned)(k + u - lo) < (unsigned)n ? 1u : 0u) << u;
+            x = l.x[k >> 5] >> s;
+            fast = true;
+        }
+    } else if (k >= p.V && k + 4 <= p.V + p.C) {
+        const int c = k - p.V, s = c & 31;
+        if (s <= 28) {
+            m = l.rel[i * p.WC + (c >> 5)] >> s;
+            x = l.sat[c >> 5] >> s;
+            fast = true;
+        }
+    } else if (k >= p.V + p.C && k + 4 <= p.D) {
+        const int vv = k - p.V - p.C, s = vv & 31;
+        if (s <= 28) {
+            m = l.nbr[i * p.WV + (vv >> 5)] >> s;
+            x = l.x[vv >> 5] >> s;
+            fast = true;
+        }
+    }
+    if (fast) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ((m >> u) & 1u) ? (int)((x >> u) & 1u) : -1;
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            v[u] = obs_elem(p, l, i, k);
+            if (++k == p.D) {
+                k = 0;
+                ++i;
+            }
+        }
+    }
 }
 
 template <typename ObsT>
@@ -160,21 +182,20 @@ struct ObsVec<int32_t> {
     __device__ static void store(int32_t *dst, const int (&v)[4]) {
         typedef int v4i __attribute__((ext_vector_type(4)));
         const v4i q = {v[0], v[1], v[2], v[3]};
-        __builtin_nontemporal_store(q, reinterpret_cast<v4i *>(dst));
+        *reinterpret_cast<v4i *>(dst) = q;
     }
 };
 template <>
 struct ObsVec<int8_t> {
     static constexpr int N = 16;
     __device__ static void store(int8_t *dst, const int (&v)[16]) {
-        uint32_t w[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            w[q] = ((uint32_t)(v[4 * q] & 0xFF)) | ((uint32_t)(v[4 * q + 1] & 0xFF) << 8) |
-                   ((uint32_t)(v[4 * q + 2] & 0xFF) << 16) | ((uint32_t)(v[4 * q + 3] & 0xFF) << 24);
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
-        const v4u q4 = {w[0], w[1], w[2], w[3]};
-        __builtin_nontemporal_store(q4, reinterpret_cast<v4u *>(dst));
+        v4u q;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            q[w] = ((uint32_t)(v[4 * w] & 0xFF)) | ((uint32_t)(v[4 * w + 1] & 0xFF) << 8) |
+                   ((uint32_t)(v[4 * w + 2] & 0xFF) << 16) | ((uint32_t)(v[4 * w + 3] & 0xFF) << 24);
+        *reinterpret_cast<v4u *>(dst) = q;
     }
 };
 
@@ -188,37 +209,48 @@ __device__ __forceinline__ void write_obs(const EnvParams &p, const EnvLds &l, O
     head = min(head, total);
     for (int e = threadIdx.x; e < head; e += kThreads) {
         const int i = e / p.D;
-        o[e] = (ObsT)obs_value(p, l, i, e - i * p.D);
+        o[e] = (ObsT)obs_elem(p, l, i, e - i * p.D);
     }
     const int nchunks = (total - head) / VEC;
+    // (i, k) of this lane's first chunk, then advanced by kThreads*VEC elements per iteration
+    const int e0 = head + threadIdx.x * VEC;
+    int i = e0 / p.D;
+    int k = e0 - i * p.D;
     for (int q = threadIdx.x; q < nchunks; q += kThreads) {
-        const int e = head + q * VEC;
-        int i = e / p.D;
-        int k = e - i * p.D;
         int v[VEC];
 #pragma unroll
-        for (int u = 0; u < VEC; ++u) {
-            v[u] = obs_value(p, l, i, k);
-            if (++k == p.D) {
-                k = 0;
-                ++i;
+        for (int u = 0; u < VEC; u += 4) {
+            int kk = k + u, ii = i;
+            while (kk >= p.D) {
+                kk -= p.D;
+                ++ii;
             }
+            int t[4];
+            obs_quad(p, l, ii, kk, t);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) v[u + w] = t[w];
         }
-        ObsVec<ObsT>::store(o + e, v);
+        ObsVec<ObsT>::store(o + head + q * VEC, v);
+        k += kThreads * VEC;
+        while (k >= p.D) {
+            k -= p.D;
+            ++i;
+        }
     }
-    for (int e = head + nchunks * VEC + threadIdx.x; e < total; e += kThreads) {
-        const int i = e / p.D;
-        o[e] = (ObsT)obs_value(p, l, i, e - i * p.D);
+    for (int e2 = head + nchunks * VEC + threadIdx.x; e2 < total; e2 += kThreads) {
+        const int i2 = e2 / p.D;
+        o[e2] = (ObsT)obs_elem(p, l, i2, e2 - i2 * p.D);
     }
 }
 
+// ---------------------------------------------------------------- kernel ----
 template <int MODE, typename ObsT>
 __global__ void __launch_bounds__(kThreads)
-env_kernel(EnvParams p, const uint16_t *__restrict__ pool, msat_env_state st,
-           const int32_t *__restrict__ actions, const uint8_t *__restrict__ reset_mask,
-           const int32_t *__restrict__ new_pidx, const uint8_t *__restrict__ new_assign,
-           uint64_t seed, uint64_t ctr, msat_step_out out, ObsT *__restrict__ obs) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__restrict__ actions,
+           const uint8_t *__restrict__ reset_mask, const int32_t *__restrict__ new_pidx,
+           const uint8_t *__restrict__ new_assign, uint64_t seed, uint64_t ctr, msat_step_out out,
+           ObsT *__restrict__ obs) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const EnvLds l = carve(smem, p);
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -230,10 +262,10 @@ env_kernel(EnvParams p, const uint16_t *__restrict__ pool, msat_env_state st,
     if (tid < 16) l.red[tid] = 0;
 
     bool do_reset = (MODE == kModeReset);
+    int pidx = st.problem_idx[b];
     if (MODE != kModeReset) {
-        // ---- load assignment + apply the agents' flips (env:230-250) ----------
-        for (int v = tid; v < p.V; v += kThreads)
-            l.vinfo[v] = (uint16_t)(agent_of_var(p, v) | ((xg[v] & 1u) << 15));
+        // ---- assignment + the agents' flips (env:230-250) --------------------
+        load_x_bits(p, l, xg);
         __syncthreads();
         if (MODE == kModeObs) {
             // get_obs only: no flips, no state update
@@ -244,22 +276,26 @@ env_kernel(EnvParams p, const uint16_t *__restrict__ pool, msat_env_state st,
                 if (a >= n) continue;  // no-op index (and every action of a var-less agent)
                 int s = a;
                 if (s < 0) s = max(s + p.M, 0);  // jnp index normalisation + clamp
-                if (s < n) l.vinfo[agent_lo(p, i) + s] ^= 0x8000u;
+                if (s < n) {
+                    const int v = agent_lo(p, i) + s;
+                    atomicXor(&l.x[v >> 5], 1u << (v & 31));
+                }
             }
         } else {
             for (int t = tid; t < p.A * p.M; t += kThreads) {
                 const int i = t / p.M, j = t - (t / p.M) * p.M;
-                if (j < agent_size(p, i) && (actions[(size_t)b * p.A * p.M + t] & 1))
-                    l.vinfo[agent_lo(p, i) + j] ^= 0x8000u;
+                if (j < agent_size(p, i) && (actions[(size_t)b * p.A * p.M + t] & 1)) {
+                    const int v = agent_lo(p, i) + j;
+                    atomicXor(&l.x[v >> 5], 1u << (v & 31));
+                }
             }
         }
         __syncthreads();
         // ---- clause scan of the stepped assignment (env:252-254) ------------
-        const int pidx = st.problem_idx[b];
         if (MODE != kModeObs && p.reward_mode == MSAT_REWARD_PBRS)
-            eval_clauses<true, false>(p, l, pool, pidx, sat_g, ntrue_g);
+            eval_clauses<true>(p, l, pool.lits, pidx, sat_g, ntrue_g);
         else
-            eval_clauses<false, false>(p, l, pool, pidx, sat_g, ntrue_g);
+            eval_clauses<false>(p, l, pool.lits, pidx, sat_g, ntrue_g);
         __syncthreads();
         if (MODE != kModeObs && tid == 0) {
             const int u_new = l.red[0];
@@ -293,30 +329,29 @@ env_kernel(EnvParams p, const uint16_t *__restrict__ pool, msat_env_state st,
     }
 
     if (do_reset) {
-        // ---- reset (env:158-181): new problem, new assignment, masks --------
-        int pidx;
+        // ---- reset (env:158-181): new problem, new assignment ---------------
         if (new_pidx != nullptr) {
             pidx = new_pidx[b];
         } else {
             const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 0u);
             pidx = (int)(((uint64_t)r.x * (uint64_t)p.N) >> 32);
         }
-        for (int v = tid; v < p.V; v += kThreads) {
-            uint32_t x;
-            if (new_assign != nullptr) {
-                x = new_assign[(size_t)b * p.V + v] & 1u;
-            } else {
-                const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 1u + (uint32_t)(v >> 7));
-                const int lane = (v >> 5) & 3;
-                const uint32_t wsel = lane == 0 ? r.x : lane == 1 ? r.y : lane == 2 ? r.z : r.w;
-                x = (wsel >> (v & 31)) & 1u;
+        if (new_assign != nullptr) {
+            load_x_bits(p, l, new_assign + (size_t)b * p.V);
+        } else {
+            // word t of the assignment = lane t%4 of the Philox block 1 + t/4 (128 vars per block)
+            for (int t = tid; t < p.WV; t += kThreads) {
+                const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 1u + (uint32_t)(t >> 2));
+                const int lane = t & 3;
+                uint32_t w = lane == 0 ? r.x : lane == 1 ? r.y : lane == 2 ? r.z : r.w;
+                const int hi = p.V - 32 * t;
+                if (hi < 32) w &= hi <= 0 ? 0u : ((1u << hi) - 1u);
+                l.x[t] = w;
             }
-            l.vinfo[v] = (uint16_t)(agent_of_var(p, v) | (x << 15));
         }
-        for (int t = tid; t < p.A * p.W; t += kThreads) l.nbr[t] = 0u;
         if (tid < 2) l.red[tid] = 0;  // red[2] (reset broadcast) may still be read by slower waves
         __syncthreads();
-        eval_clauses<false, true>(p, l, pool, pidx, sat_g, ntrue_g);
+        eval_clauses<false>(p, l, pool.lits, pidx, sat_g, ntrue_g);
         __syncthreads();
         if (tid == 0) {
             st.num_unsat[b] = l.red[0];
@@ -324,15 +359,29 @@ env_kernel(EnvParams p, const uint16_t *__restrict__ pool, msat_env_state st,
             st.done[b] = 0;
             st.problem_idx[b] = pidx;
         }
-        uint32_t *nbr_g = st.nbr_mask + (size_t)b * p.A * p.W;
-        for (int t = tid; t < p.A * p.W; t += kThreads) nbr_g[t] = l.nbr[t];
-    } else {
-        const uint32_t *nbr_g = st.nbr_mask + (size_t)b * p.A * p.W;
-        for (int t = tid; t < p.A * p.W; t += kThreads) l.nbr[t] = nbr_g[t];
     }
-    for (int v = tid; v < p.V; v += kThreads) xg[v] = (uint8_t)(l.vinfo[v] >> 15);
+    if (MODE != kModeObs)
+        for (int v = tid; v < p.V; v += kThreads) xg[v] = (uint8_t)bit(l.x, v);
+    if (p.ablate == 2) return;
+    // ---- stage the instance's agent tables (built once per pool instance) --
+    {
+        const uint32_t *rel_g = pool.rel + (size_t)pidx * p.A * p.WC;
+        const uint32_t *nbr_g = pool.nbr + (size_t)pidx * p.A * p.WV;
+        for (int t = tid; t < p.A * p.WC; t += kThreads) l.rel[t] = rel_g[t];
+        for (int t = tid; t < p.A * p.WV; t += kThreads) l.nbr[t] = nbr_g[t];
+    }
     __syncthreads();
-    write_obs<ObsT>(p, l, obs + (size_t)b * p.A * p.D);
+    ObsT *o = obs + (size_t)b * p.A * p.D;
+    if (p.ablate == 0) {
+        write_obs<ObsT>(p, l, o);
+    } else {
+        constexpr int VEC = ObsVec<ObsT>::N;
+        const int n = (p.A * p.D) / VEC;
+        int v[VEC];
+#pragma unroll
+        for (int u = 0; u < VEC; ++u) v[u] = -1;
+        for (int q = tid; q < n; q += kThreads) ObsVec<ObsT>::store(o + q * VEC, v);
+    }
 }
 
 // ---------------------------------------------------------------- cold path --
@@ -364,48 +413,82 @@ __global__ void pool_pack_kernel(const int32_t *__restrict__ lits, int NC, int K
     reinterpret_cast<uint64_t *>(pool)[t] = w;
 }
 
-// Per-env materialisation of the reference's mask tensors (env:99-128, :160).
+// Per-instance agent tables (env:99-128): rel[i][c] = clause c contains a var of
+// agent i; nbr[i][v] = v appears in a clause related to i and is not i's.
 __global__ void __launch_bounds__(kThreads)
-env_masks_kernel(EnvParams p, const uint16_t *__restrict__ pool, msat_env_state st,
-                 int32_t *__restrict__ acm, int32_t *__restrict__ anm, int32_t *__restrict__ l2a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const EnvLds l = carve(smem, p);
-    const int b = blockIdx.x;
-    for (int v = threadIdx.x; v < p.V; v += kThreads) l.vinfo[v] = (uint16_t)agent_of_var(p, v);
-    const uint32_t *nbr_g = st.nbr_mask + (size_t)b * p.A * p.W;
-    for (int t = threadIdx.x; t < p.A * p.W; t += kThreads) l.nbr[t] = nbr_g[t];
+agent_tables_kernel(EnvParams p, const uint16_t *__restrict__ lits, uint32_t *__restrict__ rel_g,
+                    uint32_t *__restrict__ nbr_g) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *rel = smem;
+    uint32_t *nbr = rel + (size_t)p.A * p.WC;
+    const int n = blockIdx.x;
+    for (int t = threadIdx.x; t < p.A * (p.WC + p.WV); t += kThreads) smem[t] = 0u;
     __syncthreads();
-    const uint64_t *prow = reinterpret_cast<const uint64_t *>(pool) + (size_t)st.problem_idx[b] * p.C;
-    const int last_agent = agent_of_var(p, p.V - 1);  // var2agent[-1] wraps to the last var
+    const uint64_t *prow = reinterpret_cast<const uint64_t *>(lits) + (size_t)n * p.C;
     for (int c = threadIdx.x; c < p.C; c += kThreads) {
         const uint64_t w = prow[c];
-        uint32_t info = 0, nullLit = 0;
+        int vars[3], ags[3];
+        bool nullLit = false;
+#pragma unroll
         for (int j = 0; j < 3; ++j) {
             const uint32_t lit = (uint32_t)(w >> (16 * j)) & 0xFFFFu;
-            uint32_t ag = kNoAgent;
-            if (lit < MSAT_LIT_ABSENT) ag = l.vinfo[lit >> 1];
-            if (lit == MSAT_LIT_NULL) nullLit = 1;
-            info |= ag << (10 * j);
-            if (l2a && j < p.K)
-                l2a[((size_t)b * p.C + c) * p.K + j] = (lit == MSAT_LIT_NULL) ? last_agent : (int)ag;
+            vars[j] = lit < MSAT_LIT_ABSENT ? (int)(lit >> 1) : -1;
+            ags[j] = vars[j] >= 0 ? agent_of_var(p, vars[j]) : -1;
+            nullLit |= (lit == MSAT_LIT_NULL);
         }
-        l.clinfo[c] = info | (nullLit << 30);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if (ags[j] < 0) continue;
+            atomicOr(&rel[ags[j] * p.WC + (c >> 5)], 1u << (c & 31));
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                if (k == j || vars[k] < 0 || ags[k] == ags[j]) continue;
+                atomicOr(&nbr[ags[j] * p.WV + (vars[k] >> 5)], 1u << (vars[k] & 31));
+            }
+        }
+        if (nullLit && p.rem > 0) {
+            // Reference quirk: literal 0 decodes to var index -1, equal to the -1 padding of
+            // agent_vars rows, so the clause is "related" to every agent owning fewer than M vars.
+            for (int i = p.rem; i < p.A; ++i) {
+                atomicOr(&rel[i * p.WC + (c >> 5)], 1u << (c & 31));
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    if (vars[k] < 0 || ags[k] == i) continue;
+                    atomicOr(&nbr[i * p.WV + (vars[k] >> 5)], 1u << (vars[k] & 31));
+                }
+            }
+        }
     }
     __syncthreads();
-    if (acm) {
+    for (int t = threadIdx.x; t < p.A * p.WC; t += kThreads) rel_g[(size_t)n * p.A * p.WC + t] = rel[t];
+    for (int t = threadIdx.x; t < p.A * p.WV; t += kThreads) nbr_g[(size_t)n * p.A * p.WV + t] = nbr[t];
+}
+
+// Per-env materialisation of the reference's mask tensors (env:99-128, :160).
+__global__ void __launch_bounds__(kThreads)
+env_masks_kernel(EnvParams p, msat_pool pool, const int32_t *__restrict__ problem_idx, int32_t *__restrict__ acm,
+                 int32_t *__restrict__ anm, int32_t *__restrict__ l2a) {
+    const int b = blockIdx.x;
+    const int pidx = problem_idx[b];
+    const uint32_t *rel = pool.rel + (size_t)pidx * p.A * p.WC;
+    const uint32_t *nbr = pool.nbr + (size_t)pidx * p.A * p.WV;
+    if (acm)
         for (int t = threadIdx.x; t < p.A * p.C; t += kThreads) {
-            const int i = t / p.C, c = t - (t / p.C) * p.C;
-            const uint32_t info = l.clinfo[c], ui = (uint32_t)i;
-            const bool small = (p.rem > 0) && (i >= p.rem);
-            const bool rel = ((info & kNoAgent) == ui) | (((info >> 10) & kNoAgent) == ui) |
-                             (((info >> 20) & kNoAgent) == ui) | (small && ((info >> 30) & 1u));
-            acm[(size_t)b * p.A * p.C + t] = rel ? 1 : -1;
+            const int i = t / p.C, c = t - i * p.C;
+            acm[(size_t)b * p.A * p.C + t] = bit(rel + i * p.WC, c) ? 1 : -1;
         }
-    }
-    if (anm) {
+    if (anm)
         for (int t = threadIdx.x; t < p.A * p.V; t += kThreads) {
-            const int i = t / p.V, v = t - (t / p.V) * p.V;
-            anm[(size_t)b * p.A * p.V + t] = ((l.nbr[i * p.W + (v >> 5)] >> (v & 31)) & 1u) ? 1 : -1;
+            const int i = t / p.V, v = t - i * p.V;
+            anm[(size_t)b * p.A * p.V + t] = bit(nbr + i * p.WV, v) ? 1 : -1;
+        }
+    if (l2a) {
+        const uint64_t *prow = reinterpret_cast<const uint64_t *>(pool.lits) + (size_t)pidx * p.C;
+        const int last_agent = agent_of_var(p, p.V - 1);  // var2agent[-1] wraps to the last var
+        for (int t = threadIdx.x; t < p.C * p.K; t += kThreads) {
+            const int c = t / p.K, j = t - c * p.K;
+            const uint32_t lit = (uint32_t)(prow[c] >> (16 * j)) & 0xFFFFu;
+            l2a[(size_t)b * p.C * p.K + t] = lit == MSAT_LIT_NULL ? last_agent : agent_of_var(p, (int)(lit >> 1));
         }
     }
 }
@@ -421,7 +504,7 @@ __global__ void clause_features_kernel(int BC, const uint8_t *__restrict__ sat,
 
 __global__ void __launch_bounds__(kThreads)
 static_var_features_kernel(const uint16_t *__restrict__ pool, int V, int C, float *__restrict__ f) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     int *deg = reinterpret_cast<int *>(smem);  // [2V]
     const int n = blockIdx.x;
     for (int t = threadIdx.x; t < 2 * V; t += kThreads) deg[t] = 0;
@@ -466,7 +549,8 @@ static int make_params(const msat_env_desc *d, EnvParams *p) {
     p->M = p->base + (p->rem > 0 ? 1 : 0);
     MSAT_REQUIRE(d->max_vars_per_agent == p->M, "max_vars_per_agent %d != ceil(V/A)=%d",
                  d->max_vars_per_agent, p->M);
-    p->W = (p->V + 31) / 32;
+    p->WV = 2 * ((p->V + 63) / 64);
+    p->WC = 2 * ((p->C + 63) / 64);
     p->D = 2 * p->V + p->C;
     p->max_steps = d->max_steps;
     p->action_mode = d->action_mode;
@@ -475,37 +559,39 @@ static int make_params(const msat_env_desc *d, EnvParams *p) {
     p->r_clause = d->r_clause;
     p->r_sat = d->r_sat;
     p->gamma = d->gamma;
+    const char *ab = getenv("MARLSAT_ABLATE");
+    p->ablate = ab ? atoi(ab) : 0;
     return MSAT_OK;
-}
-
-static size_t env_lds_bytes(const EnvParams &p) {
-    return (size_t)p.C * 4 + (size_t)p.A * p.W * 4 + 16 * 4 + (((size_t)p.V * 2 + 15) & ~(size_t)15);
 }
 
 static int check_state(const msat_env_state *st) {
     MSAT_REQUIRE(st != nullptr, "state is NULL");
-    MSAT_REQUIRE(st->assign && st->clause_sat && st->num_unsat && st->step && st->done &&
-                     st->problem_idx && st->nbr_mask,
+    MSAT_REQUIRE(st->assign && st->clause_sat && st->num_unsat && st->step && st->done && st->problem_idx,
                  "a required state pointer is NULL");
     return MSAT_OK;
 }
 
+static int check_pool(const msat_pool *pool) {
+    MSAT_REQUIRE(pool != nullptr && pool->lits && pool->rel && pool->nbr, "pool (lits/rel/nbr) is NULL");
+    return MSAT_OK;
+}
+
 template <int MODE>
-static int launch_env(const EnvParams &p, const msat_env_desc *d, const uint16_t *pool,
+static int launch_env(const EnvParams &p, const msat_env_desc *d, const msat_pool *pool,
                       const msat_env_state *st, const int32_t *actions, const uint8_t *mask,
                       const int32_t *npidx, const uint8_t *nassign, uint64_t seed, uint64_t ctr,
                       const msat_step_out *out, void *obs, hipStream_t s) {
-    const size_t lds = env_lds_bytes(p);
+    const size_t lds = env_lds_words(p) * 4;
     MSAT_REQUIRE(lds <= 160 * 1024, "env needs %zu B of LDS (> 160 KiB)", lds);
     msat_step_out o{};
     if (out) o = *out;
     if (p.B == 0) return MSAT_OK;
     if (d->obs_dtype == MSAT_OBS_I32)
-        hipLaunchKernelGGL((env_kernel<MODE, int32_t>), dim3(p.B), dim3(kThreads), lds, s, p, pool, *st,
-                           actions, mask, npidx, nassign, seed, ctr, o, (int32_t *)obs);
+        hipLaunchKernelGGL((env_kernel<MODE, int32_t>), dim3(p.B), dim3(kThreads), lds, s, p, *pool, *st, actions,
+                           mask, npidx, nassign, seed, ctr, o, (int32_t *)obs);
     else
-        hipLaunchKernelGGL((env_kernel<MODE, int8_t>), dim3(p.B), dim3(kThreads), lds, s, p, pool, *st,
-                           actions, mask, npidx, nassign, seed, ctr, o, (int8_t *)obs);
+        hipLaunchKernelGGL((env_kernel<MODE, int8_t>), dim3(p.B), dim3(kThreads), lds, s, p, *pool, *st, actions,
+                           mask, npidx, nassign, seed, ctr, o, (int8_t *)obs);
     return check_launch("env_kernel");
 }
 
@@ -526,28 +612,40 @@ extern "C" int msat_pool_pack(const int32_t *lits, int32_t num_problems, int32_t
     return check_launch("pool_pack_kernel");
 }
 
-extern "C" int msat_env_reset(const msat_env_desc *desc, const uint16_t *pool,
+extern "C" int msat_pool_agent_tables(const msat_env_desc *desc, const uint16_t *lits, uint32_t *rel, uint32_t *nbr,
+                                      void *stream) {
+    EnvParams p;
+    int rc = make_params(desc, &p);
+    if (rc) return rc;
+    MSAT_REQUIRE(lits && rel && nbr, "NULL pointer");
+    const size_t lds = (size_t)p.A * (p.WC + p.WV) * 4;
+    MSAT_REQUIRE(lds <= 160 * 1024, "agent tables need %zu B of LDS (> 160 KiB)", lds);
+    hipLaunchKernelGGL(agent_tables_kernel, dim3(p.N), dim3(kThreads), lds, (hipStream_t)stream, p, lits, rel, nbr);
+    return check_launch("agent_tables_kernel");
+}
+
+extern "C" int msat_env_reset(const msat_env_desc *desc, const msat_pool *pool,
                               const msat_env_state *state, const uint8_t *reset_mask,
                               const int32_t *new_problem_idx, const uint8_t *new_assign,
                               uint64_t seed, uint64_t rng_counter, void *obs, void *stream) {
     EnvParams p;
     int rc = make_params(desc, &p);
     if (rc) return rc;
-    if ((rc = check_state(state))) return rc;
-    MSAT_REQUIRE(pool && obs, "NULL pool/obs");
+    if ((rc = check_state(state)) || (rc = check_pool(pool))) return rc;
+    MSAT_REQUIRE(obs, "NULL obs");
     return launch_env<kModeReset>(p, desc, pool, state, nullptr, reset_mask, new_problem_idx, new_assign,
                                   seed, rng_counter, nullptr, obs, (hipStream_t)stream);
 }
 
-extern "C" int msat_env_step(const msat_env_desc *desc, const uint16_t *pool,
+extern "C" int msat_env_step(const msat_env_desc *desc, const msat_pool *pool,
                              const msat_env_state *state, const int32_t *actions, int32_t autoreset,
                              const int32_t *new_problem_idx, const uint8_t *new_assign, uint64_t seed,
                              uint64_t rng_counter, const msat_step_out *out, void *obs, void *stream) {
     EnvParams p;
     int rc = make_params(desc, &p);
     if (rc) return rc;
-    if ((rc = check_state(state))) return rc;
-    MSAT_REQUIRE(pool && obs && actions, "NULL pool/obs/actions");
+    if ((rc = check_state(state)) || (rc = check_pool(pool))) return rc;
+    MSAT_REQUIRE(obs && actions, "NULL obs/actions");
     MSAT_REQUIRE(out && out->reward && out->done && out->solved, "NULL step outputs");
     if (autoreset)
         return launch_env<kModeStepAutoReset>(p, desc, pool, state, actions, nullptr, new_problem_idx,
@@ -556,29 +654,28 @@ extern "C" int msat_env_step(const msat_env_desc *desc, const uint16_t *pool,
                                  rng_counter, out, obs, (hipStream_t)stream);
 }
 
-extern "C" int msat_env_obs(const msat_env_desc *desc, const uint16_t *pool, const msat_env_state *state,
+extern "C" int msat_env_obs(const msat_env_desc *desc, const msat_pool *pool, const msat_env_state *state,
                             void *obs, void *stream) {
     EnvParams p;
     int rc = make_params(desc, &p);
     if (rc) return rc;
-    if ((rc = check_state(state))) return rc;
-    MSAT_REQUIRE(pool && obs, "NULL pool/obs");
+    if ((rc = check_state(state)) || (rc = check_pool(pool))) return rc;
+    MSAT_REQUIRE(obs, "NULL obs");
     return launch_env<kModeObs>(p, desc, pool, state, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, obs,
                                 (hipStream_t)stream);
 }
 
-extern "C" int msat_env_masks(const msat_env_desc *desc, const uint16_t *pool,
+extern "C" int msat_env_masks(const msat_env_desc *desc, const msat_pool *pool,
                               const msat_env_state *state, int32_t *agent_clause_masks,
                               int32_t *agent_neighbor_masks, int32_t *literal_to_agent_idx,
                               void *stream) {
     EnvParams p;
     int rc = make_params(desc, &p);
     if (rc) return rc;
-    if ((rc = check_state(state))) return rc;
-    MSAT_REQUIRE(pool, "NULL pool");
+    if ((rc = check_state(state)) || (rc = check_pool(pool))) return rc;
     if (p.B == 0) return MSAT_OK;
-    hipLaunchKernelGGL(env_masks_kernel, dim3(p.B), dim3(kThreads), env_lds_bytes(p), (hipStream_t)stream, p,
-                       pool, *state, agent_clause_masks, agent_neighbor_masks, literal_to_agent_idx);
+    hipLaunchKernelGGL(env_masks_kernel, dim3(p.B), dim3(kThreads), 0, (hipStream_t)stream, p, *pool,
+                       state->problem_idx, agent_clause_masks, agent_neighbor_masks, literal_to_agent_idx);
     return check_launch("env_masks_kernel");
 }
 

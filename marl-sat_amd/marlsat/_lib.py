@@ -47,8 +47,11 @@ class EnvStateC(ctypes.Structure):
         ("step", c_void_p),
         ("done", c_void_p),
         ("problem_idx", c_void_p),
-        ("nbr_mask", c_void_p),
     ]
+
+
+class PoolC(ctypes.Structure):
+    _fields_ = [("lits", c_void_p), ("rel", c_void_p), ("nbr", c_void_p)]
 
 
 class StepOutC(ctypes.Structure):
@@ -73,13 +76,17 @@ def _load():
         "msat_last_error": (ctypes.c_char_p, []),
         "msat_version": (c_int32, []),
         "msat_pool_pack": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P]),
-        "msat_env_reset": (c_int32, [POINTER(EnvDesc), P, POINTER(EnvStateC), P, P, P, c_uint64, c_uint64, P, P]),
+        "msat_pool_agent_tables": (c_int32, [POINTER(EnvDesc), P, P, P, P]),
+        "msat_env_reset": (
+            c_int32, [POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, P, P, c_uint64, c_uint64, P, P]
+        ),
         "msat_env_step": (
             c_int32,
-            [POINTER(EnvDesc), P, POINTER(EnvStateC), P, c_int32, P, P, c_uint64, c_uint64, POINTER(StepOutC), P, P],
+            [POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, c_int32, P, P, c_uint64, c_uint64,
+             POINTER(StepOutC), P, P],
         ),
-        "msat_env_obs": (c_int32, [POINTER(EnvDesc), P, POINTER(EnvStateC), P, P]),
-        "msat_env_masks": (c_int32, [POINTER(EnvDesc), P, POINTER(EnvStateC), P, P, P, P]),
+        "msat_env_obs": (c_int32, [POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, P]),
+        "msat_env_masks": (c_int32, [POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, P, P, P]),
         "msat_clause_features": (c_int32, [POINTER(EnvDesc), POINTER(EnvStateC), P, P]),
         "msat_static_var_features": (c_int32, [P, c_int32, c_int32, c_int32, P, P]),
         "msat_gae_workspace_bytes": (c_size_t, [c_int32, c_int32]),
@@ -88,6 +95,8 @@ def _load():
             [c_int32, c_int32, P, c_int32, P, P, P, c_float, c_float, c_int32, P, P, P, P],
         ),
     }
+    sig["msat_debug_fill"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])  # marlsat_debug.h
+    sig["msat_debug_fill_chunked"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
@@ -102,6 +111,7 @@ EXPORTED = (
     "msat_last_error",
     "msat_version",
     "msat_pool_pack",
+    "msat_pool_agent_tables",
     "msat_env_reset",
     "msat_env_step",
     "msat_env_obs",

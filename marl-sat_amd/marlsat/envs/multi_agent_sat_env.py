@@ -92,6 +92,27 @@ class ProblemPool:
         if int(err.item()) != 0:
             raise ValueError(f"problem pool has a literal with |l| > num_vars={num_vars}")
         self._svf = None
+        self._tables = {}  # num_agents -> (rel (N,A,WC), nbr (N,A,WV)) int32 bit words
+
+    def agent_tables(self, env: "SATEnv"):
+        """Per-instance relation / neighbour bit tables for env's agent partition
+        (_compute_observation_maps, env:99-128, hoisted from every reset to once per pool)."""
+        key = env.num_agents
+        if key not in self._tables:
+            WC = 2 * ((self.num_clauses + 63) // 64)
+            WV = 2 * ((self.num_vars + 63) // 64)
+            rel = torch.empty((self.num_problems, env.num_agents, WC), dtype=torch.int32, device=self.device)
+            nbr = torch.empty((self.num_problems, env.num_agents, WV), dtype=torch.int32, device=self.device)
+            desc = env._desc(0, self)
+            _lib.check(_lib.lib.msat_pool_agent_tables(ctypes.byref(desc), self.packed.data_ptr(), rel.data_ptr(),
+                                                       nbr.data_ptr(), _lib.stream_ptr(self.device)),
+                       "msat_pool_agent_tables")
+            self._tables[key] = (rel, nbr)
+        return self._tables[key]
+
+    def c(self, env: "SATEnv") -> _lib.PoolC:
+        rel, nbr = self.agent_tables(env)
+        return _lib.PoolC(self.packed.data_ptr(), rel.data_ptr(), nbr.data_ptr())
 
     @property
     def device(self):
@@ -119,7 +140,6 @@ class SATState:
     step: torch.Tensor  # (B,) int32
     env_done: torch.Tensor  # (B,) uint8
     problem_idx: torch.Tensor  # (B,) int32
-    nbr_mask: torch.Tensor  # (B,A,W) int32 bit words
     pool: ProblemPool
     env: "SATEnv" = field(repr=False)
     _masks: Optional[tuple] = field(default=None, repr=False)
@@ -149,7 +169,7 @@ class SATState:
             acm = torch.empty((B, e.num_agents, e.num_clauses), dtype=torch.int32, device=dev)
             anm = torch.empty((B, e.num_agents, e.num_vars), dtype=torch.int32, device=dev)
             l2a = torch.empty((B, e.num_clauses, self.pool.clause_width), dtype=torch.int32, device=dev)
-            _lib.check(_lib.lib.msat_env_masks(e._desc(B, self.pool), self.pool.packed.data_ptr(), self._c(),
+            _lib.check(_lib.lib.msat_env_masks(e._desc(B, self.pool), self.pool.c(e), self._c(),
                                                acm.data_ptr(), anm.data_ptr(), l2a.data_ptr(), _lib.stream_ptr(dev)),
                        "msat_env_masks")
             self._masks = (acm, anm, l2a)
@@ -171,14 +191,14 @@ class SATState:
         return _lib.EnvStateC(
             self.variable_assignments.data_ptr(), self.clauses_satisfied_status.data_ptr(),
             self.clause_ntrue.data_ptr(), self.num_unsatisfied.data_ptr(), self.step.data_ptr(),
-            self.env_done.data_ptr(), self.problem_idx.data_ptr(), self.nbr_mask.data_ptr(),
+            self.env_done.data_ptr(), self.problem_idx.data_ptr(),
         )
 
     def clone(self) -> "SATState":
         return SATState(
             self.variable_assignments.clone(), self.clauses_satisfied_status.clone(), self.clause_ntrue.clone(),
             self.num_unsatisfied.clone(), self.step.clone(), self.env_done.clone(), self.problem_idx.clone(),
-            self.nbr_mask.clone(), self.pool, self.env,
+            self.pool, self.env,
         )
 
     def replace(self, **kw) -> "SATState":
@@ -228,7 +248,6 @@ class SATEnv:
             self.action_spaces = {a: MultiDiscrete([2] * M) for a in self.agents}
         self.obs_dim = 2 * self.num_vars + self.num_clauses  # env:340-343
         self.observation_spaces = {a: Box(-1, 1, (self.obs_dim,)) for a in self.agents}
-        self.nbr_words = (self.num_vars + 31) // 32
 
     # ------------------------------------------------------------ props ----
     @property
@@ -261,8 +280,7 @@ class SATEnv:
         B, V, C = num_envs, self.num_vars, self.num_clauses
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)
         return SATState(z((B, V), torch.uint8), z((B, C), torch.uint8), z((B, C), torch.uint8), z((B,), torch.int32),
-                        z((B,), torch.int32), z((B,), torch.uint8), z((B,), torch.int32),
-                        z((B, self.num_agents, self.nbr_words), torch.int32), pool, self)
+                        z((B,), torch.int32), z((B,), torch.uint8), z((B,), torch.int32), pool, self)
 
     def alloc_obs(self, num_envs: int) -> torch.Tensor:
         return torch.empty((num_envs, self.num_agents, self.obs_dim), dtype=self.obs_dtype, device=self.device)
@@ -300,7 +318,7 @@ class SATEnv:
         m = None
         if reset_mask is not None:
             m = torch.as_tensor(reset_mask, device=self.device).to(torch.uint8).contiguous()
-        _lib.check(_lib.lib.msat_env_reset(self._desc(num_envs, pool), pool.packed.data_ptr(), state._c(), _lib.ptr(m),
+        _lib.check(_lib.lib.msat_env_reset(self._desc(num_envs, pool), pool.c(self), state._c(), _lib.ptr(m),
                                            _lib.ptr(pidx), _lib.ptr(x), k.seed, k.counter, obs.data_ptr(),
                                            _lib.stream_ptr(self.device)),
                    "msat_env_reset")
@@ -340,7 +358,7 @@ class SATEnv:
         k = as_key(key)
         so = _lib.StepOutC(out["reward"].data_ptr(), out["done"].data_ptr(), out["solved"].data_ptr(),
                            out["num_unsatisfied"].data_ptr(), out["episode_step"].data_ptr())
-        _lib.check(_lib.lib.msat_env_step(self._desc(B, state.pool), state.pool.packed.data_ptr(), state._c(),
+        _lib.check(_lib.lib.msat_env_step(self._desc(B, state.pool), state.pool.c(self), state._c(),
                                           a.data_ptr(), 1 if autoreset else 0, _lib.ptr(pidx), _lib.ptr(x), k.seed,
                                           k.counter, so, obs.data_ptr(), _lib.stream_ptr(self.device)),
                    "msat_env_step")
@@ -357,20 +375,21 @@ class SATEnv:
         so = _lib.StepOutC(out["reward"].data_ptr(), out["done"].data_ptr(), out["solved"].data_ptr(),
                            out["num_unsatisfied"].data_ptr(), out["episode_step"].data_ptr())
         fn = _lib.lib.msat_env_step
-        pool_p, obs_p, s = state.pool.packed.data_ptr(), obs.data_ptr(), _lib.stream_ptr(self.device)
+        cpool = state.pool.c(self)
+        obs_p, s = obs.data_ptr(), _lib.stream_ptr(self.device)
         ar = 1 if autoreset else 0
         want = (B, self.num_agents) if self.action_mode == 0 else (B, self.num_agents, self.max_vars_per_agent)
-        dref, sref, oref = ctypes.byref(desc), ctypes.byref(cst), ctypes.byref(so)
+        dref, pref, sref, oref = ctypes.byref(desc), ctypes.byref(cpool), ctypes.byref(cst), ctypes.byref(so)
 
         def step(actions: torch.Tensor, counter: int) -> None:
             if actions.shape != want or actions.dtype != torch.int32:
                 raise ValueError(f"actions must be int32 {want}")
-            rc = fn(dref, pool_p, sref, actions.data_ptr(), ar, None, None, seed, counter, oref, obs_p, s)
+            rc = fn(dref, pref, sref, actions.data_ptr(), ar, None, None, seed, counter, oref, obs_p, s)
             state._masks = None
             if rc:
                 _lib.check(rc, "msat_env_step")
 
-        step._keepalive = (desc, cst, so, state, obs, out)
+        step._keepalive = (desc, cpool, cst, so, state, obs, out)
         return step
 
     def step_env(self, key, state: SATState, actions, *, inplace: bool = False):
@@ -402,7 +421,7 @@ class SATEnv:
         """env:345-398."""
         B = state.num_envs
         obs = self.alloc_obs(B)
-        _lib.check(_lib.lib.msat_env_obs(self._desc(B, state.pool), state.pool.packed.data_ptr(), state._c(),
+        _lib.check(_lib.lib.msat_env_obs(self._desc(B, state.pool), state.pool.c(self), state._c(),
                                          obs.data_ptr(), _lib.stream_ptr(self.device)),
                    "msat_env_obs")
         return ObsDict(self.agents, obs)

@@ -57,8 +57,10 @@ def _desc(**kw):
 def test_bad_desc_is_rejected_with_message(bad, msg):
     from marlsat import _lib
 
-    st = _lib.EnvStateC(*([1] * 8))  # never dereferenced: validation fails first
-    rc = _lib.lib.msat_env_reset(ctypes.byref(_desc(**bad)), 1, ctypes.byref(st), None, None, None, 0, 0, 1, None)
+    st = _lib.EnvStateC(*([1] * 7))  # never dereferenced: validation fails first
+    pool = _lib.PoolC(1, 1, 1)
+    rc = _lib.lib.msat_env_reset(ctypes.byref(_desc(**bad)), ctypes.byref(pool), ctypes.byref(st), None, None, None, 0,
+                                 0, 1, None)
     assert rc == -1
     assert msg in _lib.lib.msat_last_error().decode()
 
@@ -66,9 +68,16 @@ def test_bad_desc_is_rejected_with_message(bad, msg):
 def test_null_state_pointer_rejected():
     from marlsat import _lib
 
-    st = _lib.EnvStateC(1, 1, None, 1, 1, 1, 1, None)  # nbr_mask missing
-    rc = _lib.lib.msat_env_reset(ctypes.byref(_desc()), 1, ctypes.byref(st), None, None, None, 0, 0, 1, None)
+    st = _lib.EnvStateC(1, 1, None, 1, 1, 1, None)  # problem_idx missing
+    pool = _lib.PoolC(1, 1, 1)
+    rc = _lib.lib.msat_env_reset(ctypes.byref(_desc()), ctypes.byref(pool), ctypes.byref(st), None, None, None, 0, 0,
+                                 1, None)
     assert rc == -1 and "NULL" in _lib.lib.msat_last_error().decode()
+    st = _lib.EnvStateC(1, 1, None, 1, 1, 1, 1)
+    pool = _lib.PoolC(1, None, 1)  # relation table missing
+    rc = _lib.lib.msat_env_reset(ctypes.byref(_desc()), ctypes.byref(pool), ctypes.byref(st), None, None, None, 0, 0,
+                                 1, None)
+    assert rc == -1 and "pool" in _lib.lib.msat_last_error().decode()
 
 
 def test_gae_bad_dims_rejected():
