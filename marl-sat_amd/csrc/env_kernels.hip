@@ -36,7 +36,8 @@ struct EnvParams {
     int base, rem;  // agent i owns [i*base + min(i,rem), +base+(i<rem))
     int max_steps, action_mode, reward_mode, N;
     float r_clause, r_sat, gamma;
-    int ablate;  // diagnostics only (MARLSAT_ABLATE): 0 full, 1 constant obs, 2 no obs write
+    int ablate;  // diagnostics only (MARLSAT_ABLATE): bits 0-1: 0 full, 1 constant obs, 2 no obs write;
+                 // bit 2: disable the XCD-major env order
 };
 
 enum : int { kModeReset = 0, kModeStep = 1, kModeStepAutoReset = 2, kModeObs = 3 };
@@ -56,11 +57,15 @@ struct EnvLds {
     uint32_t *sat;  // [WC]    clause-satisfied bits
     uint32_t *rel;  // [A*WC]  agent-clause relation bits of the env's instance
     uint32_t *nbr;  // [A*WV]  agent neighbour bits of the env's instance
+    uint32_t *fm;   // [NW]    obs image: element is not -1   (NW = A*D/32 + 2)
+    uint32_t *fx;   // [NW]    obs image: element value bit
     int *red;       // [16]    reduction / broadcast scratch
 };
 
+__host__ __device__ __forceinline__ int obs_image_words(const EnvParams &p) { return (p.A * p.D) / 32 + 2; }
+
 __host__ __device__ __forceinline__ size_t env_lds_words(const EnvParams &p) {
-    return (size_t)p.WV + p.WC + (size_t)p.A * (p.WC + p.WV) + 16;
+    return (size_t)p.WV + p.WC + (size_t)p.A * (p.WC + p.WV) + 2 * (size_t)obs_image_words(p) + 16;
 }
 
 __device__ __forceinline__ EnvLds carve(uint32_t *smem, const EnvParams &p) {
@@ -69,7 +74,9 @@ __device__ __forceinline__ EnvLds carve(uint32_t *smem, const EnvParams &p) {
     l.sat = l.x + p.WV;
     l.rel = l.sat + p.WC;
     l.nbr = l.rel + (size_t)p.A * p.WC;
-    l.red = reinterpret_cast<int *>(l.nbr + (size_t)p.A * p.WV);
+    l.fm = l.nbr + (size_t)p.A * p.WV;
+    l.fx = l.fm + obs_image_words(p);
+    l.red = reinterpret_cast<int *>(l.fx + obs_image_words(p));
     return l;
 }
 
@@ -85,34 +92,59 @@ __device__ __forceinline__ void load_x_bits(const EnvParams &p, const EnvLds &l,
     }
 }
 
+// Prefetch depth (per lane) of the step path: pool-row words (covers C <= kPfClause*kThreads
+// clauses) and agent-table words, all issued right after problem_idx is known so the
+// preamble costs ~2 dependent memory round trips instead of ~4.
+constexpr int kPfClause = 4;
+constexpr int kPfRel = 4;
+constexpr int kPfNbr = 2;
+
+// One 64-clause wave slice of the clause scan: c0 wave-uniform, w = this lane's pool word.
+template <bool kPbrs>
+__device__ __forceinline__ void clause_slice(const EnvParams &p, const EnvLds &l, int c0, uint64_t w,
+                                             uint8_t *__restrict__ sat_g, uint8_t *__restrict__ ntrue_g, int &unsat,
+                                             int &newly) {
+    const int lane = threadIdx.x & 63;
+    const int c = c0 + lane;
+    uint32_t sat = 0, ntrue = 0, old = 0;
+    const bool live = c < p.C;
+    if (live) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint32_t lit = (uint32_t)(w >> (16 * j)) & 0xFFFFu;
+            if (lit < MSAT_LIT_ABSENT) ntrue += (bit(l.x, (int)(lit >> 1)) ^ lit) & 1u;
+        }
+        sat = ntrue ? 1u : 0u;
+        if (kPbrs) old = sat_g[c];
+        sat_g[c] = (uint8_t)sat;
+        if (ntrue_g) ntrue_g[c] = (uint8_t)ntrue;
+    }
+    const uint64_t ms = __ballot(sat);
+    if (lane < 2) l.sat[(c0 >> 5) + lane] = (uint32_t)(ms >> (32 * lane));
+    unsat += __popcll(__ballot(live && !sat));
+    if (kPbrs) newly += __popcll(__ballot(sat && !old));
+}
+
 // Evaluate every clause of pool row `pidx` against l.x: clause bits -> l.sat,
 // bytes -> sat_g / ntrue_g, unsat count (and PBRS newly-satisfied) -> red[0] / red[1].
-template <bool kPbrs>
+// The first NPF slices use the lane's prefetched pool words pw[].
+template <bool kPbrs, int NPF>
 __device__ __forceinline__ void eval_clauses(const EnvParams &p, const EnvLds &l, const uint16_t *__restrict__ lits,
-                                             int pidx, uint8_t *__restrict__ sat_g, uint8_t *__restrict__ ntrue_g) {
+                                             int pidx, uint8_t *__restrict__ sat_g, uint8_t *__restrict__ ntrue_g,
+                                             const uint64_t (&pw)[kPfClause]) {
     const uint64_t *prow = reinterpret_cast<const uint64_t *>(lits) + (size_t)pidx * p.C;
     const int lane = threadIdx.x & 63;
     int unsat = 0, newly = 0;  // wave-uniform
-    for (int c0 = threadIdx.x & ~63; c0 < p.WC * 32; c0 += kThreads) {
-        const int c = c0 + lane;
-        uint32_t sat = 0, ntrue = 0, old = 0;
-        const bool live = c < p.C;
-        if (live) {
-            const uint64_t w = prow[c];  // pool rows are shared by many envs: keep them cached
+    const int cend = p.WC * 32;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const uint32_t lit = (uint32_t)(w >> (16 * j)) & 0xFFFFu;
-                if (lit < MSAT_LIT_ABSENT) ntrue += (bit(l.x, (int)(lit >> 1)) ^ lit) & 1u;
-            }
-            sat = ntrue ? 1u : 0u;
-            if (kPbrs) old = sat_g[c];
-            sat_g[c] = (uint8_t)sat;
-            if (ntrue_g) ntrue_g[c] = (uint8_t)ntrue;
-        }
-        const uint64_t ms = __ballot(sat);
-        if (lane < 2) l.sat[(c0 >> 5) + lane] = (uint32_t)(ms >> (32 * lane));
-        unsat += __popcll(__ballot(live && !sat));
-        if (kPbrs) newly += __popcll(__ballot(sat && !old));
+    for (int j = 0; j < NPF; ++j) {
+        const int c0 = (threadIdx.x & ~63) + j * kThreads;
+        if (c0 < cend) clause_slice<kPbrs>(p, l, c0, pw[j], sat_g, ntrue_g, unsat, newly);
+    }
+    for (int c0 = (threadIdx.x & ~63) + NPF * kThreads; c0 < cend; c0 += kThreads) {
+        const int c = c0 + lane;
+        const uint64_t w = c < p.C ? prow[c] : 0ull;  // pool rows are shared by many envs: keep them cached
+        clause_slice<kPbrs>(p, l, c0, w, sat_g, ntrue_g, unsat, newly);
     }
     if (lane == 0) {
         atomicAdd(&l.red[0], unsat);
@@ -121,57 +153,67 @@ __device__ __forceinline__ void eval_clauses(const EnvParams &p, const EnvLds &l
 }
 
 // ---------------------------------------------------------------- obs pass --
-// Element (i, k) of agent i's row (env:345-398): own vars | clause status | neighbour vars.
-__device__ __forceinline__ int obs_elem(const EnvParams &p, const EnvLds &l, int i, int k) {
-    if (k < p.V) return ((unsigned)(k - agent_lo(p, i)) < (unsigned)agent_size(p, i)) ? (int)bit(l.x, k) : -1;
-    k -= p.V;
-    if (k < p.C) return bit(l.rel + i * p.WC, k) ? (int)bit(l.sat, k) : -1;
-    k -= p.C;
-    return bit(l.nbr + i * p.WV, k) ? (int)bit(l.x, k) : -1;
+// The env's (A, D) observation block as two flat bit images over its A*D
+// elements: FM (element != -1) and FX (its 0/1 value).  Row i, element k
+// (env:345-398): k < V own vars (FM = owned, FX = x), V <= k < V+C clause
+// status (FM = rel_i, FX = sat), k >= V+C neighbour vars (FM = nbr_i, FX = x).
+// Built once per env from the LDS bit words (OR of shifted source words), then
+// every 16 B store is a funnel-shifted extraction at its flat bit offset: no
+// row/region logic and no divergence in the store loop, for any (V, C, A).
+
+__device__ __forceinline__ uint32_t low_mask(int n) { return n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u); }
+
+__device__ __forceinline__ void or_bits(uint32_t *img, int dst, uint32_t bits) {
+    if (!bits) return;
+    const int w = dst >> 5, s = dst & 31;
+    atomicOr(&img[w], bits << s);
+    if (s) {
+        const uint32_t hi = bits >> (32 - s);
+        if (hi) atomicOr(&img[w + 1], hi);
+    }
 }
 
-// 4 consecutive elements (i, k..k+3) of one row.  Fast path when they sit in one
-// region and one 32-bit word: two LDS words, four bit extractions.
-__device__ __forceinline__ void obs_quad(const EnvParams &p, const EnvLds &l, int i, int k, int (&v)[4]) {
-    uint32_t m = 0, x = 0;
-    bool fast = false;
-    if (k + 4 <= p.V) {
-        const int s = k & 31;
-        if (s <= 28) {
-            const int lo = agent_lo(p, i), n = agent_size(p, i);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) m |= ((unsigned)(k + u - lo) < (unsigned)n ? 1u : 0u) << u;
-            x = l.x[k >> 5] >> s;
-            fast = true;
+__device__ __forceinline__ void build_obs_images(const EnvParams &p, const EnvLds &l) {
+    const int nwV = (p.V + 31) >> 5, nwC = (p.C + 31) >> 5;
+    const int U = 2 * nwV + nwC;  // source words per row
+    for (int t = threadIdx.x; t < p.A * U; t += kThreads) {
+        const int i = t / U;
+        int s = t - i * U;
+        int len, off;
+        uint32_t m, x;
+        if (s < nwV) {  // own vars
+            len = min(32, p.V - 32 * s);
+            const int lo = agent_lo(p, i) - 32 * s, hi = lo + agent_size(p, i);
+            const int a = max(lo, 0), z = min(hi, 32);
+            m = z > a ? (low_mask(z) & ~low_mask(a)) : 0u;
+            x = l.x[s];
+            off = 32 * s;
+        } else if ((s -= nwV) < nwC) {  // clause status
+            len = min(32, p.C - 32 * s);
+            m = l.rel[i * p.WC + s];
+            x = l.sat[s];
+            off = p.V + 32 * s;
+        } else {  // neighbour vars
+            s -= nwC;
+            len = min(32, p.V - 32 * s);
+            m = l.nbr[i * p.WV + s];
+            x = l.x[s];
+            off = p.V + p.C + 32 * s;
         }
-    } else if (k >= p.V && k + 4 <= p.V + p.C) {
-        const int c = k - p.V, s = c & 31;
-        if (s <= 28) {
-            m = l.rel[i * p.WC + (c >> 5)] >> s;
-            x = l.sat[c >> 5] >> s;
-            fast = true;
-        }
-    } else if (k >= p.V + p.C && k + 4 <= p.D) {
-        const int vv = k - p.V - p.C, s = vv & 31;
-        if (s <= 28) {
-            m = l.nbr[i * p.WV + (vv >> 5)] >> s;
-            x = l.x[vv >> 5] >> s;
-            fast = true;
-        }
+        const uint32_t keep = low_mask(len);
+        const int dst = i * p.D + off;
+        or_bits(l.fm, dst, m & keep);
+        or_bits(l.fx, dst, x & m & keep);  // value bits only where the element is live
     }
-    if (fast) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = ((m >> u) & 1u) ? (int)((x >> u) & 1u) : -1;
-    } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            v[u] = obs_elem(p, l, i, k);
-            if (++k == p.D) {
-                k = 0;
-                ++i;
-            }
-        }
-    }
+}
+
+__device__ __forceinline__ uint32_t bits_at(const uint32_t *img, int e) {
+    const int w = e >> 5, s = e & 31;
+    return (uint32_t)((((uint64_t)img[w + 1] << 32) | img[w]) >> s);
+}
+
+__device__ __forceinline__ int elem_val(uint32_t m, uint32_t x, int u) {
+    return ((m >> u) & 1u) ? (int)((x >> u) & 1u) : -1;
 }
 
 template <typename ObsT>
@@ -179,27 +221,31 @@ struct ObsVec;
 template <>
 struct ObsVec<int32_t> {
     static constexpr int N = 4;
-    __device__ static void store(int32_t *dst, const int (&v)[4]) {
+    __device__ static void store(int32_t *dst, uint32_t m, uint32_t x) {
         typedef int v4i __attribute__((ext_vector_type(4)));
-        const v4i q = {v[0], v[1], v[2], v[3]};
+        const v4i q = {elem_val(m, x, 0), elem_val(m, x, 1), elem_val(m, x, 2), elem_val(m, x, 3)};
         *reinterpret_cast<v4i *>(dst) = q;
     }
 };
 template <>
 struct ObsVec<int8_t> {
     static constexpr int N = 16;
-    __device__ static void store(int8_t *dst, const int (&v)[16]) {
+    __device__ static void store(int8_t *dst, uint32_t m, uint32_t x) {
+        // byte u = m_u ? x_u : 0xFF  (-1)
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
         v4u q;
 #pragma unroll
-        for (int w = 0; w < 4; ++w)
-            q[w] = ((uint32_t)(v[4 * w] & 0xFF)) | ((uint32_t)(v[4 * w + 1] & 0xFF) << 8) |
-                   ((uint32_t)(v[4 * w + 2] & 0xFF) << 16) | ((uint32_t)(v[4 * w + 3] & 0xFF) << 24);
+        for (int w = 0; w < 4; ++w) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) word |= ((uint32_t)elem_val(m, x, 4 * w + u) & 0xFFu) << (8 * u);
+            q[w] = word;
+        }
         *reinterpret_cast<v4u *>(dst) = q;
     }
 };
 
-// Stream the env's (A, D) observation block: unaligned head, 16 B body, tail.
+// Stream the env's (A, D) observation block from the bit images: unaligned head, 16 B body, tail.
 template <typename ObsT>
 __device__ __forceinline__ void write_obs(const EnvParams &p, const EnvLds &l, ObsT *__restrict__ o) {
     constexpr int VEC = ObsVec<ObsT>::N;
@@ -207,40 +253,14 @@ __device__ __forceinline__ void write_obs(const EnvParams &p, const EnvLds &l, O
     int head = (int)((reinterpret_cast<uintptr_t>(o) / sizeof(ObsT)) % VEC);
     head = head ? VEC - head : 0;
     head = min(head, total);
-    for (int e = threadIdx.x; e < head; e += kThreads) {
-        const int i = e / p.D;
-        o[e] = (ObsT)obs_elem(p, l, i, e - i * p.D);
-    }
+    for (int e = threadIdx.x; e < head; e += kThreads) o[e] = (ObsT)elem_val(bits_at(l.fm, e), bits_at(l.fx, e), 0);
     const int nchunks = (total - head) / VEC;
-    // (i, k) of this lane's first chunk, then advanced by kThreads*VEC elements per iteration
-    const int e0 = head + threadIdx.x * VEC;
-    int i = e0 / p.D;
-    int k = e0 - i * p.D;
     for (int q = threadIdx.x; q < nchunks; q += kThreads) {
-        int v[VEC];
-#pragma unroll
-        for (int u = 0; u < VEC; u += 4) {
-            int kk = k + u, ii = i;
-            while (kk >= p.D) {
-                kk -= p.D;
-                ++ii;
-            }
-            int t[4];
-            obs_quad(p, l, ii, kk, t);
-#pragma unroll
-            for (int w = 0; w < 4; ++w) v[u + w] = t[w];
-        }
-        ObsVec<ObsT>::store(o + head + q * VEC, v);
-        k += kThreads * VEC;
-        while (k >= p.D) {
-            k -= p.D;
-            ++i;
-        }
+        const int e = head + q * VEC;
+        ObsVec<ObsT>::store(o + e, bits_at(l.fm, e), bits_at(l.fx, e));
     }
-    for (int e2 = head + nchunks * VEC + threadIdx.x; e2 < total; e2 += kThreads) {
-        const int i2 = e2 / p.D;
-        o[e2] = (ObsT)obs_elem(p, l, i2, e2 - i2 * p.D);
-    }
+    for (int e = head + nchunks * VEC + threadIdx.x; e < total; e += kThreads)
+        o[e] = (ObsT)elem_val(bits_at(l.fm, e), bits_at(l.fx, e), 0);
 }
 
 // ---------------------------------------------------------------- kernel ----
@@ -252,7 +272,10 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
            ObsT *__restrict__ obs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const EnvLds l = carve(smem, p);
-    const int b = blockIdx.x;
+    int b = blockIdx.x;
+    // XCD-major env order: blocks b and b+8 share an XCD (round-robin dispatch, speed only),
+    // so consecutive envs -- adjacent obs blocks in HBM -- are written through one XCD's L2.
+    if (!(p.ablate & 4) && (p.B & 7) == 0) b = (blockIdx.x & 7) * (p.B >> 3) + (blockIdx.x >> 3);
     const int tid = threadIdx.x;
     if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
 
@@ -263,7 +286,34 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
 
     bool do_reset = (MODE == kModeReset);
     int pidx = st.problem_idx[b];
+    uint64_t pw[kPfClause];
+    uint32_t prel[kPfRel], pnbr[kPfNbr];
+    int step0 = 0, u_old = 0;
     if (MODE != kModeReset) {
+        // ---- prefetch the instance's pool row and agent tables ----------------
+        const uint64_t *prow = reinterpret_cast<const uint64_t *>(pool.lits) + (size_t)pidx * p.C;
+        const uint32_t *rel_g = pool.rel + (size_t)pidx * p.A * p.WC;
+        const uint32_t *nbr_g = pool.nbr + (size_t)pidx * p.A * p.WV;
+#pragma unroll
+        for (int j = 0; j < kPfClause; ++j) {
+            const int c = tid + j * kThreads;
+            pw[j] = c < p.C ? prow[c] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < kPfRel; ++j) {
+            const int t = tid + j * kThreads;
+            prel[j] = t < p.A * p.WC ? rel_g[t] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kPfNbr; ++j) {
+            const int t = tid + j * kThreads;
+            pnbr[j] = t < p.A * p.WV ? nbr_g[t] : 0u;
+        }
+        // step-0 / unsat-0 and this lane's first action, loaded with the prefetch
+        step0 = st.step[b];
+        u_old = st.num_unsat[b];
+        int a0 = 0;
+        if (MODE != kModeObs && p.action_mode == 0 && tid < p.A) a0 = actions[(size_t)b * p.A + tid];
         // ---- assignment + the agents' flips (env:230-250) --------------------
         load_x_bits(p, l, xg);
         __syncthreads();
@@ -271,7 +321,7 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
             // get_obs only: no flips, no state update
         } else if (p.action_mode == 0) {
             for (int i = tid; i < p.A; i += kThreads) {
-                const int a = actions[(size_t)b * p.A + i];
+                const int a = i == tid ? a0 : actions[(size_t)b * p.A + i];
                 const int n = agent_size(p, i);
                 if (a >= n) continue;  // no-op index (and every action of a var-less agent)
                 int s = a;
@@ -293,18 +343,17 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
         __syncthreads();
         // ---- clause scan of the stepped assignment (env:252-254) ------------
         if (MODE != kModeObs && p.reward_mode == MSAT_REWARD_PBRS)
-            eval_clauses<true>(p, l, pool.lits, pidx, sat_g, ntrue_g);
+            eval_clauses<true, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
         else
-            eval_clauses<false>(p, l, pool.lits, pidx, sat_g, ntrue_g);
+            eval_clauses<false, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
         __syncthreads();
         if (MODE != kModeObs && tid == 0) {
             const int u_new = l.red[0];
-            const int step0 = st.step[b];
             const bool solved = (u_new == 0);
             const bool done = solved || (step0 + 1 >= p.max_steps);
             float r;
             if (p.reward_mode == MSAT_REWARD_PBRS) {
-                const float pot_new = (float)(-u_new), pot_old = (float)(-st.num_unsat[b]);
+                const float pot_new = (float)(-u_new), pot_old = (float)(-u_old);
                 const float r_pbrs = __fsub_rn(__fmul_rn(p.gamma, pot_new), pot_old);
                 const float r_cl = __fmul_rn((float)l.red[1], p.r_clause);
                 r = __fadd_rn(__fadd_rn(r_pbrs, r_cl), solved ? p.r_sat : 0.0f);
@@ -351,7 +400,7 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
         }
         if (tid < 2) l.red[tid] = 0;  // red[2] (reset broadcast) may still be read by slower waves
         __syncthreads();
-        eval_clauses<false>(p, l, pool.lits, pidx, sat_g, ntrue_g);
+        eval_clauses<false, 0>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
         __syncthreads();
         if (tid == 0) {
             st.num_unsat[b] = l.red[0];
@@ -362,25 +411,37 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
     }
     if (MODE != kModeObs)
         for (int v = tid; v < p.V; v += kThreads) xg[v] = (uint8_t)bit(l.x, v);
-    if (p.ablate == 2) return;
+    if ((p.ablate & 3) == 2) return;
     // ---- stage the instance's agent tables (built once per pool instance) --
     {
         const uint32_t *rel_g = pool.rel + (size_t)pidx * p.A * p.WC;
         const uint32_t *nbr_g = pool.nbr + (size_t)pidx * p.A * p.WV;
-        for (int t = tid; t < p.A * p.WC; t += kThreads) l.rel[t] = rel_g[t];
-        for (int t = tid; t < p.A * p.WV; t += kThreads) l.nbr[t] = nbr_g[t];
+        const bool pf = (MODE != kModeReset) && !do_reset;  // prefetched words belong to pidx
+        int t0r = 0, t0n = 0;
+        if (pf) {
+#pragma unroll
+            for (int j = 0; j < kPfRel; ++j)
+                if (tid + j * kThreads < p.A * p.WC) l.rel[tid + j * kThreads] = prel[j];
+#pragma unroll
+            for (int j = 0; j < kPfNbr; ++j)
+                if (tid + j * kThreads < p.A * p.WV) l.nbr[tid + j * kThreads] = pnbr[j];
+            t0r = kPfRel * kThreads;
+            t0n = kPfNbr * kThreads;
+        }
+        for (int t = t0r + tid; t < p.A * p.WC; t += kThreads) l.rel[t] = rel_g[t];
+        for (int t = t0n + tid; t < p.A * p.WV; t += kThreads) l.nbr[t] = nbr_g[t];
+        for (int t = tid; t < 2 * obs_image_words(p); t += kThreads) l.fm[t] = 0u;  // fm, fx contiguous
     }
     __syncthreads();
     ObsT *o = obs + (size_t)b * p.A * p.D;
-    if (p.ablate == 0) {
+    if ((p.ablate & 3) == 0) {
+        build_obs_images(p, l);
+        __syncthreads();
         write_obs<ObsT>(p, l, o);
     } else {
         constexpr int VEC = ObsVec<ObsT>::N;
         const int n = (p.A * p.D) / VEC;
-        int v[VEC];
-#pragma unroll
-        for (int u = 0; u < VEC; ++u) v[u] = -1;
-        for (int q = tid; q < n; q += kThreads) ObsVec<ObsT>::store(o + q * VEC, v);
+        for (int q = tid; q < n; q += kThreads) ObsVec<ObsT>::store(o + q * VEC, 0u, 0u);
     }
 }
 

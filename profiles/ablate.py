@@ -42,7 +42,7 @@ def time_fill(nt, grid, n=40):
 
 res = {}
 for rnd in range(3):
-    for mode, name in ((0, "full"), (1, "constobs"), (2, "noobs")):
+    for mode, name in ((0, "full"), (1, "constobs"), (2, "noobs"), (4, "full-noxcd")):
         os.environ["MARLSAT_ABLATE"] = str(mode)
         time_steps(5)
         res.setdefault(name, []).append(time_steps())
