@@ -1,0 +1,108 @@
+/*
+ * marlsat_net.h — C-ABI of the MAPPO network / update kernels in libmarlsat.so
+ * (gfx950).  Same conventions as marlsat.h: device pointers owned by the caller,
+ * explicit dims, stream last, 0 on success / negative + msat_last_error().
+ *
+ * Reference computations replaced (kongqg/marl-sat):
+ *   msat_gemm / msat_gemm_wgrad  <- every flax nn.Dense / nn.GRUCell matmul of
+ *        GNN_ActorCritic (src/learners/mappo_gnn_sat_learner.py:44-80, :213-240,
+ *        :311-349) and their jax.value_and_grad transposes (:647-649)
+ */
+#ifndef MARLSAT_NET_H
+#define MARLSAT_NET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* C[M,N] (+)= A[M,K] @ op(B) (+ bias[N]); op(B) = B[K,N] (transB=0) or B[N,K]^T (transB=1).
+ * Row-major with leading dims; fp32 in / fp32 accumulate on the matrix cores. */
+int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ldb, int32_t transB, float *C,
+              int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, int32_t accumulate,
+              void *stream);
+
+/* W[K,N] (+)= A[M,K]^T @ G[M,N]: split over M, partial slabs reduced in a fixed order. */
+size_t msat_gemm_wgrad_workspace_bytes(int32_t M, int32_t K, int32_t N);
+int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
+                    int32_t M, int32_t K, int32_t N, int32_t accumulate, void *workspace, void *stream);
+
+/* ---- graph batch assembly (learner:148-195 features + the agents' local graphs) ----
+ * Block per sample: instantiate the per-instance templates (marlsat/learners/graphs.py) at the
+ * sample's row bases (sample_bases (S,3) = var row, clause row, incidence starts) and compute the
+ * node features from the sample's assignment x (S,V): vfeat (Nv,4) = [x, deg+/C, deg-/C, 0],
+ * cfeat (Nc,3) = [is_sat, ntrue/3, 1].  G = 1 (critic graph only) or A+1. */
+int msat_assemble_graph_batch(
+    int32_t S, int32_t G, int32_t A, int32_t V, int32_t C, const int32_t *inst, const uint8_t *x, const float *svf,
+    const uint16_t *pool, const int32_t *sample_bases, const int32_t *t_vgid, const int32_t *t_cgid,
+    const int32_t *t_slots, const int32_t *t_ptr, const int32_t *t_inc, const int32_t *voff, const int32_t *coff,
+    const int32_t *eoff, const int32_t *poff, const int32_t *gv, const int32_t *gc, float *vfeat, float *cfeat,
+    int32_t *slots, int32_t *ptr, int32_t *inc, int32_t *g_vbase, int32_t *g_nv, int32_t *g_cbase, int32_t *g_nc,
+    int32_t Nv, int32_t nnz, void *stream);
+
+/* ---- message passing: signed literal gathers (the encoder's A^T M and A M, learner:66-74) ----
+ * clause_gather: dst[c] (+)= [sum_{pos slots} src[v][0:H] | sum_{neg slots} src[v][H:2H]],
+ *                slots (Nc,3) = (var_row << 1) | neg, or -1.
+ * var_gather:    dst[v] (+)= [sum_{pos entries} src[c][0:H] | sum_{neg entries} src[c][H:2H]],
+ *                CSR ptr (Nv+1), entries (clause_row << 1) | neg.  Each is the other's transpose. */
+int msat_clause_gather(const float *src, int32_t ld_src, const int32_t *slots, float *dst, int32_t ld_dst,
+                       int32_t num_clause_rows, int32_t H, int32_t accumulate, void *stream);
+int msat_var_gather(const float *src, int32_t ld_src, const int32_t *ptr, const int32_t *inc, float *dst,
+                    int32_t ld_dst, int32_t num_var_rows, int32_t H, int32_t accumulate, void *stream);
+
+/* ---- fused flax GRUCell + LayerNorm (learner:69-80) ----
+ * Gi = x Wi + bi, Gh = h Wh + [0,0,b_hn] (gates [r|z|n]); out = LN(GRU(h, x)).
+ * Backward: dGi, dGh, dhprev (+=), LN scale/bias grads ([scale|bias] contiguous, (+)=). */
+int msat_gru_ln_fwd(const float *Gi, int32_t ldi, const float *Gh, int32_t ldh, const float *hprev,
+                    int32_t ldp, const float *ln_scale, const float *ln_bias, float *out, int32_t ldo,
+                    int32_t R, int32_t H, void *stream);
+size_t msat_gru_ln_bwd_partial_floats(int32_t R, int32_t H);
+int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, int32_t ldi, const float *Gh, int32_t ldh,
+                    const float *hprev, int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi,
+                    float *dGh, int32_t lddh, float *dhprev, int32_t lddp, float *dln_scale,
+                    float *dln_bias, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
+                    void *stream);
+int msat_relu(float *x, size_t n, void *stream);
+int msat_relu_bwd(float *dy, const float *y, size_t n, void *stream);
+
+/* ---- heads (learner:264-350): graph batch = per sample G graphs (0 critic, 1+i agent i) ---- */
+int msat_critic_pool(const float *Hp, const float *Hn, const float *Hc, int32_t H, const int32_t *vbase,
+                     const int32_t *nv, const int32_t *cbase, const int32_t *nc, int32_t G, int32_t S,
+                     float *pooled, void *stream);
+int msat_critic_pool_bwd(const float *Hp, const float *Hn, const float *Hc, int32_t H, const int32_t *vbase,
+                         const int32_t *nv, const int32_t *cbase, const int32_t *nc, int32_t G, int32_t S,
+                         const float *dpooled, float *dHp, float *dHn, float *dHc, void *stream);
+int msat_actor_pool(const float *Hp, const float *Hn, const float *Hc, int32_t H, const int32_t *vbase,
+                    const int32_t *nv, const int32_t *cbase, const int32_t *nc, int32_t G, int32_t S,
+                    int32_t A, int32_t M, int32_t base_sz, int32_t rem, const float *id_emb, int32_t E,
+                    float *my_emb, float *ctx, void *stream);
+int msat_actor_pool_bwd(int32_t H, const int32_t *vbase, const int32_t *nv, const int32_t *cbase,
+                        const int32_t *nc, int32_t G, int32_t S, int32_t A, int32_t M, int32_t base_sz,
+                        int32_t rem, int32_t E, const float *dmy, const float *dctx, float *dHp, float *dHn,
+                        float *dHc, float *did, void *stream);
+int msat_bcast_add_relu(float *Q, const float *P, int32_t R, int32_t M, int32_t W, void *stream);
+int msat_group_sum(const float *dQ, int32_t R, int32_t M, int32_t W, float *dP, void *stream);
+int msat_assemble_logits(const float *flip, const float *noop, int32_t SA, int32_t A, int32_t M,
+                         int32_t base_sz, int32_t rem, float *logits, void *stream);
+int msat_mask_var_logits(float *logits, int32_t SA, int32_t A, int32_t M, int32_t base_sz, int32_t rem,
+                         void *stream);
+int msat_split_dlogits(const float *dlogits, int32_t SA, int32_t M, float *dflip, float *dnoop, void *stream);
+
+/* ---- policy / loss / optimiser (learner:397-403, :597-650; mappo_runner.py:198) ---- */
+int msat_sample_actions(const float *logits, int32_t R, int32_t W, int32_t greedy, uint64_t seed,
+                        uint64_t counter, int32_t *action, float *logp, void *stream);
+int msat_ppo_loss(const float *logits, int32_t S, int32_t A, int32_t M, int32_t action_mode,
+                  int32_t base_sz, int32_t rem, const int32_t *action, const float *old_logp,
+                  const float *gae, const float *value, const float *old_value, const float *targets,
+                  float clip_eps, float vf_clip, float ent_coef, float vf_coef, int32_t minibatch,
+                  float *dlogits, float *dvalue, float *row_terms, double *loss_sums, void *stream);
+int msat_adam(float *params, const float *grads, float *m, float *v, size_t n, float lr, float b1, float b2,
+              float eps, int32_t count, float grad_scale, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MARLSAT_NET_H */

@@ -1,0 +1,251 @@
+// fp32 GEMMs on the gfx950 matrix cores (v_mfma_f32_32x32x2_f32: exact fp32, a
+// k-ordered fmaf chain per output -- the 1e-5 parity bar rules out bf16/xf32).
+//
+//   msat_gemm        C[M,N] (+)= A[M,K] @ op(B) (+ bias[N])      op(B) = B[K,N] or B[N,K]^T
+//   msat_gemm_wgrad  W[K,N] (+)= A[M,K]^T @ G[M,N]                (weight gradients, M huge)
+//
+// One 256-thread workgroup computes a 128x128 output tile; wave w owns the 64x64
+// quadrant (w>>1, w&1) as 2x2 MFMA 32x32 tiles (64 accumulator registers).  The
+// reduction dimension is staged through LDS 16 deep, k-major on both operands
+// ([red][out], rows padded to 132 words: conflict-free ds_read_b32 operand fetches),
+// double-buffered with the next slab held in registers while the current one is
+// consumed.  The weight-gradient GEMM splits M over `splits` workgroups per output
+// tile, writes fp32 partial slabs and reduces them in a fixed order
+// (bitwise reproducible, no float atomics).
+#include <algorithm>
+
+#include "common.h"
+
+namespace msat {
+
+constexpr int kGT = 256;      // threads
+constexpr int kTM = 128;      // output tile rows
+constexpr int kTN = 128;      // output tile cols
+constexpr int kKS = 16;       // reduction slab depth
+constexpr int kLdsLd = 132;   // padded LDS row (words)
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// One operand slab: LDS[r][o] for r < 16 (reduction), o < 128 (output index).
+// src(o, r) addressing is either "direct" (src[r][o], row-major over the reduction
+// index) or "transposed" (src[o][r]).  Each thread moves 8 elements.
+struct Slab {
+    float v[8];
+};
+
+__device__ __forceinline__ void load_slab(Slab &s, const float *__restrict__ src, int ld, bool trans, int o0, int omax,
+                                          int r0, int rmax, bool vec_ok) {
+    const int t = threadIdx.x;
+    if (!trans) {
+        // direct: thread -> (r = t>>4, o = (t&15)*8 .. +8): 8 consecutive outputs of one reduction row
+        const int r = r0 + (t >> 4), o = o0 + (t & 15) * 8;
+        const float *p = src + (size_t)r * ld + o;
+        if (r < rmax && vec_ok && o + 8 <= omax) {
+            const float4 a = *reinterpret_cast<const float4 *>(p);
+            const float4 b = *reinterpret_cast<const float4 *>(p + 4);
+            s.v[0] = a.x; s.v[1] = a.y; s.v[2] = a.z; s.v[3] = a.w;
+            s.v[4] = b.x; s.v[5] = b.y; s.v[6] = b.z; s.v[7] = b.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s.v[j] = (r < rmax && o + j < omax) ? p[j] : 0.0f;
+        }
+    } else {
+        // transposed: thread -> (o = t>>1, r = (t&1)*8 .. +8): 8 consecutive reduction elems of one output row
+        const int o = o0 + (t >> 1), r = r0 + (t & 1) * 8;
+        const float *p = src + (size_t)o * ld + r;
+        if (o < omax && vec_ok && r + 8 <= rmax) {
+            const float4 a = *reinterpret_cast<const float4 *>(p);
+            const float4 b = *reinterpret_cast<const float4 *>(p + 4);
+            s.v[0] = a.x; s.v[1] = a.y; s.v[2] = a.z; s.v[3] = a.w;
+            s.v[4] = b.x; s.v[5] = b.y; s.v[6] = b.z; s.v[7] = b.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s.v[j] = (o < omax && r + j < rmax) ? p[j] : 0.0f;
+        }
+    }
+}
+
+__device__ __forceinline__ void store_slab(const Slab &s, float *lds, bool trans) {
+    const int t = threadIdx.x;
+    if (!trans) {
+        float *q = lds + (t >> 4) * kLdsLd + (t & 15) * 8;
+        *reinterpret_cast<float4 *>(q) = make_float4(s.v[0], s.v[1], s.v[2], s.v[3]);
+        *reinterpret_cast<float4 *>(q + 4) = make_float4(s.v[4], s.v[5], s.v[6], s.v[7]);
+    } else {
+        const int o = t >> 1, r = (t & 1) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lds[(r + j) * kLdsLd + o] = s.v[j];
+    }
+}
+
+// acc[i][j] += As[:, wr+32i ..] x Bs[:, wc+32j ..] over one 16-deep slab
+__device__ __forceinline__ void mfma_slab(const float *As, const float *Bs, int wr, int wc, f32x16 (&acc)[2][2]) {
+    const int lane = threadIdx.x & 63;
+    const int li = lane & 31, lk = lane >> 5;
+#pragma unroll
+    for (int kk = 0; kk < kKS; kk += 2) {
+        const float *a = As + (kk + lk) * kLdsLd + wr + li;
+        const float *b = Bs + (kk + lk) * kLdsLd + wc + li;
+        const float a0 = a[0], a1 = a[32], b0 = b[0], b1 = b[32];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+}
+
+// Generic tile: out[o_a][o_b] = sum_r SA(o_a, r) * SB(o_b, r) for r in [rbeg, rend)
+__device__ __forceinline__ void tile_accumulate(const float *__restrict__ A, int lda, bool transA, int oa0, int oamax,
+                                                const float *__restrict__ B, int ldb, bool transB, int ob0, int obmax,
+                                                int rbeg, int rend, bool vecA, bool vecB, f32x16 (&acc)[2][2],
+                                                float *lds) {
+    float *As[2] = {lds, lds + kKS * kLdsLd};
+    float *Bs[2] = {lds + 2 * kKS * kLdsLd, lds + 3 * kKS * kLdsLd};
+    const int w = threadIdx.x >> 6;
+    const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
+    Slab sa, sb;
+    if (rbeg >= rend) return;
+    load_slab(sa, A, lda, transA, oa0, oamax, rbeg, rend, vecA);
+    load_slab(sb, B, ldb, transB, ob0, obmax, rbeg, rend, vecB);
+    store_slab(sa, As[0], transA);
+    store_slab(sb, Bs[0], transB);
+    __syncthreads();
+    int buf = 0;
+    for (int r = rbeg; r < rend; r += kKS) {
+        const bool more = r + kKS < rend;
+        if (more) {
+            load_slab(sa, A, lda, transA, oa0, oamax, r + kKS, rend, vecA);
+            load_slab(sb, B, ldb, transB, ob0, obmax, r + kKS, rend, vecB);
+        }
+        mfma_slab(As[buf], Bs[buf], wr, wc, acc);
+        if (more) {
+            store_slab(sa, As[buf ^ 1], transA);
+            store_slab(sb, Bs[buf ^ 1], transB);
+        }
+        __syncthreads();
+        buf ^= 1;
+    }
+}
+
+// C[M,N] (+)= A[M,K] @ op(B) + bias   (A is "transposed" in slab terms: o = m, r = k)
+__global__ void __launch_bounds__(kGT)
+gemm_kernel(const float *__restrict__ A, int lda, const float *__restrict__ B, int ldb, int transB,
+            float *__restrict__ C, int ldc, const float *__restrict__ bias, int M, int N, int K, int accumulate) {
+    __shared__ __attribute__((aligned(16))) float lds[4 * kKS * kLdsLd];
+    const int m0 = blockIdx.x * kTM, n0 = blockIdx.y * kTN;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    const bool vecA = (lda % 4 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+    const bool vecB = (ldb % 4 == 0) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+    // slab terms: A(o=m, r=k) is src[m][k] -> transposed; B(o=n, r=k): B[k][n] direct, B[n][k] transposed
+    tile_accumulate(A, lda, true, m0, M, B, ldb, transB != 0, n0, N, 0, K, vecA, vecB, acc, lds);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wr = m0 + (w >> 1) * 64, wc = n0 + (w & 1) * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = wc + 32 * j + (lane & 31);
+            if (col >= N) continue;
+            const float bv = bias ? bias[col] : 0.0f;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = wr + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+                if (row >= M) continue;
+                float *c = C + (size_t)row * ldc + col;
+                const float v = acc[i][j][reg] + bv;
+                *c = accumulate ? *c + v : v;
+            }
+        }
+}
+
+// partial[s][k][n] = sum_{m in split s} A[m][k] G[m][n]   (A(o=k, r=m) direct, G(o=n, r=m) direct)
+__global__ void __launch_bounds__(kGT)
+gemm_wgrad_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G, int ldg, float *__restrict__ part,
+                  int M, int K, int N, int rows_per_split) {
+    __shared__ __attribute__((aligned(16))) float lds[4 * kKS * kLdsLd];
+    const int k0 = blockIdx.x * kTM, n0 = blockIdx.y * kTN, s = blockIdx.z;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    const bool vecA = (lda % 4 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+    const bool vecG = (ldg % 4 == 0) && ((reinterpret_cast<uintptr_t>(G) & 15) == 0);
+    const int rb = s * rows_per_split, re = min(M, rb + rows_per_split);
+    tile_accumulate(A, lda, false, k0, K, G, ldg, false, n0, N, rb, re, vecA, vecG, acc, lds);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wr = k0 + (w >> 1) * 64, wc = n0 + (w & 1) * 64;
+    float *P = part + (size_t)s * K * N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = wc + 32 * j + (lane & 31);
+            if (col >= N) continue;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = wr + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+                if (row < K) P[(size_t)row * N + col] = acc[i][j][reg];
+            }
+        }
+}
+
+// W[k][n] (+)= sum_s part[s][k][n]  (fixed split order -> reproducible)
+__global__ void wgrad_reduce_kernel(const float *__restrict__ part, int splits, int K, int N, float *__restrict__ W,
+                                    int ldw, int accumulate) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= K * N) return;
+    float s = 0.0f;
+    for (int i = 0; i < splits; ++i) s += part[(size_t)i * K * N + t];
+    const int k = t / N, n = t - k * N;
+    float *w = W + (size_t)k * ldw + n;
+    *w = accumulate ? *w + s : s;
+}
+
+static int wgrad_splits(int M, int K, int N) {
+    const int tiles = ((K + kTM - 1) / kTM) * ((N + kTN - 1) / kTN);
+    int splits = std::max(1, std::min(512 / std::max(tiles, 1), (M + 1023) / 1024));
+    return splits;
+}
+
+}  // namespace msat
+
+using namespace msat;
+
+extern "C" int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ldb, int32_t transB, float *C,
+                         int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, int32_t accumulate,
+                         void *stream) {
+    MSAT_REQUIRE(A && B && C, "NULL operand");
+    MSAT_REQUIRE(M >= 0 && N >= 1 && K >= 0, "bad dims M=%d N=%d K=%d", M, N, K);
+    MSAT_REQUIRE(lda >= K && ldc >= N && ldb >= (transB ? K : N), "leading dims too small");
+    if (M == 0) return MSAT_OK;
+    dim3 grid((M + kTM - 1) / kTM, (N + kTN - 1) / kTN);
+    hipLaunchKernelGGL(gemm_kernel, grid, dim3(kGT), 0, (hipStream_t)stream, A, lda, B, ldb, transB, C, ldc, bias, M,
+                       N, K, accumulate);
+    return check_launch("gemm_kernel");
+}
+
+extern "C" size_t msat_gemm_wgrad_workspace_bytes(int32_t M, int32_t K, int32_t N) {
+    return (size_t)wgrad_splits(M, K, N) * K * N * sizeof(float);
+}
+
+extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
+                               int32_t M, int32_t K, int32_t N, int32_t accumulate, void *workspace, void *stream) {
+    MSAT_REQUIRE(A && G && W && workspace, "NULL operand");
+    MSAT_REQUIRE(M >= 0 && K >= 1 && N >= 1 && lda >= K && ldg >= N && ldw >= N, "bad dims");
+    hipStream_t s = (hipStream_t)stream;
+    const int splits = wgrad_splits(M, K, N);
+    const int rows = (M + splits - 1) / splits;
+    const int rows16 = ((rows + kKS - 1) / kKS) * kKS;
+    dim3 grid((K + kTM - 1) / kTM, (N + kTN - 1) / kTN, splits);
+    hipLaunchKernelGGL(gemm_wgrad_kernel, grid, dim3(kGT), 0, s, A, lda, G, ldg, (float *)workspace, M, K, N, rows16);
+    int rc = check_launch("gemm_wgrad_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((K * N + 255) / 256), dim3(256), 0, s, (const float *)workspace,
+                       splits, K, N, W, ldw, accumulate);
+    return check_launch("wgrad_reduce_kernel");
+}

@@ -1,0 +1,380 @@
+// GNN encoder / actor-critic building blocks for the MAPPO update (gfx950).
+//
+// The reference's encoder (src/learners/mappo_gnn_sat_learner.py:19-82) multiplies
+// DENSE V x C adjacency matrices; a 3-SAT clause has <= 3 literals, so here both
+// message directions are signed gathers over the literal incidence of a ragged
+// batch of graphs (each sample contributes its critic graph plus one local graph
+// per agent, see marlsat/learners/graphs.py):
+//   clause side  m_c = [sum_{pos lits} src_v[:H], sum_{neg lits} src_v[H:]]   (A^T M)
+//   var side     n_v = [sum_{pos occ} src_c[:H], sum_{neg occ} src_c[H:]]     (A M)
+// and each is the other's transpose, so the backward pass reuses them.
+// GRU + LayerNorm (flax nn.GRUCell / nn.LayerNorm semantics) are fused row kernels
+// (one wave per row) on top of the fp32 MFMA GEMMs of gemm.hip.
+#include "common.h"
+
+namespace msat {
+
+constexpr int kRowThreads = 256;  // 4 waves -> 4 rows per block iteration
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// ------------------------------------------------------------------ gathers --
+// slots: (Nc, 3) int32, (var_row << 1) | neg, or -1.  One wave per clause row.
+__global__ void __launch_bounds__(kRowThreads)
+clause_gather_kernel(const float *__restrict__ src, int lds_, const int *__restrict__ slots, float *__restrict__ dst,
+                     int ldd, int Nc, int H, int accumulate) {
+    const int lane = threadIdx.x & 63;
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < Nc; c += gridDim.x * 4) {
+        const int s0 = slots[3 * (size_t)c], s1 = slots[3 * (size_t)c + 1], s2 = slots[3 * (size_t)c + 2];
+        for (int j = lane * 4; j < 2 * H; j += 256) {
+            const int want = j < H ? 0 : 1;  // first half: positive literals, second: negative
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#define MSAT_ADD_SLOT(S)                                                                          \
+    if ((S) >= 0 && ((S)&1) == want) {                                                            \
+        const float4 v = *reinterpret_cast<const float4 *>(src + (size_t)((S) >> 1) * lds_ + j);  \
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;                                   \
+    }
+            MSAT_ADD_SLOT(s0) MSAT_ADD_SLOT(s1) MSAT_ADD_SLOT(s2)
+#undef MSAT_ADD_SLOT
+            float4 *d = reinterpret_cast<float4 *>(dst + (size_t)c * ldd + j);
+            if (accumulate) {
+                const float4 o = *d;
+                acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+            }
+            *d = acc;
+        }
+    }
+}
+
+// CSR over var rows: entries (clause_row << 1) | neg.
+__global__ void __launch_bounds__(kRowThreads)
+var_gather_kernel(const float *__restrict__ src, int lds_, const int *__restrict__ ptr, const int *__restrict__ inc,
+                  float *__restrict__ dst, int ldd, int Nv, int H, int accumulate) {
+    const int lane = threadIdx.x & 63;
+    for (int v = blockIdx.x * 4 + (threadIdx.x >> 6); v < Nv; v += gridDim.x * 4) {
+        const int e0 = ptr[v], e1 = ptr[v + 1];
+        for (int j = lane * 4; j < 2 * H; j += 256) {
+            const int want = j < H ? 0 : 1;
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int e = e0; e < e1; ++e) {
+                const int s = inc[e];
+                if ((s & 1) != want) continue;
+                const float4 x = *reinterpret_cast<const float4 *>(src + (size_t)(s >> 1) * lds_ + j);
+                acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+            }
+            float4 *d = reinterpret_cast<float4 *>(dst + (size_t)v * ldd + j);
+            if (accumulate) {
+                const float4 o = *d;
+                acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+            }
+            *d = acc;
+        }
+    }
+}
+
+// ------------------------------------------------------------- GRU + LN fwd --
+// Gi = x Wi + bi ([r|z|n], 3H), Gh = h Wh + bh ([r|z|n], bh = [0,0,b_hn]).
+// h' = (1-z) n + z h,  r = s(Gi_r+Gh_r), z = s(Gi_z+Gh_z), n = tanh(Gi_n + r Gh_n)
+// y = (h' - mean) * (rsqrt(var + 1e-6) * scale) + bias,  var = E[h'^2] - mean^2.
+template <int PER>
+__global__ void __launch_bounds__(kRowThreads)
+gru_ln_fwd_kernel(const float *__restrict__ Gi, int ldi, const float *__restrict__ Gh, int ldh,
+                  const float *__restrict__ hp, int ldp, const float *__restrict__ scale,
+                  const float *__restrict__ bias, float *__restrict__ out, int ldo, int R, int H) {
+    const int lane = threadIdx.x & 63;
+    for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < R; r += gridDim.x * 4) {
+        const float *gi = Gi + (size_t)r * ldi, *gh = Gh + (size_t)r * ldh, *h = hp + (size_t)r * ldp;
+        float hn[PER];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int j = lane + 64 * u;
+            const float rg = sigmoidf_(gi[j] + gh[j]);
+            const float zg = sigmoidf_(gi[H + j] + gh[H + j]);
+            const float ng = tanhf(gi[2 * H + j] + rg * gh[2 * H + j]);
+            hn[u] = (1.0f - zg) * ng + zg * h[j];
+            s1 += hn[u];
+            s2 += hn[u] * hn[u];
+        }
+        s1 = wave_sum_f32(s1);
+        s2 = wave_sum_f32(s2);
+        const float mean = s1 / (float)H;
+        const float var = fmaxf(s2 / (float)H - mean * mean, 0.0f);
+        const float rs = rsqrtf(var + 1e-6f);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int j = lane + 64 * u;
+            out[(size_t)r * ldo + j] = (hn[u] - mean) * (rs * scale[j]) + bias[j];
+        }
+    }
+}
+
+// ------------------------------------------------------------- GRU + LN bwd --
+// dy -> dGi, dGh (3H each), dh (+=), and per-block partial sums of dscale / dbias
+// (part[block][0:H] = sum dy*xhat, part[block][H:2H] = sum dy), reduced later in a
+// fixed order.
+template <int PER>
+__global__ void __launch_bounds__(kRowThreads)
+gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
+                  const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
+                  const float *__restrict__ scale, float *__restrict__ dGi, int lddi, float *__restrict__ dGh, int lddh,
+                  float *__restrict__ dh, int lddh_prev, float *__restrict__ part, int R, int H) {
+    __shared__ float s_part[4][2 * 64 * PER];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float ps[PER], pb[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) ps[u] = pb[u] = 0.f;
+    for (int r = blockIdx.x * 4 + w; r < R; r += gridDim.x * 4) {
+        const float *gi = Gi + (size_t)r * ldi, *gh = Gh + (size_t)r * ldh, *h = hp + (size_t)r * ldp;
+        const float *g = dy + (size_t)r * ldy;
+        float rg[PER], zg[PER], ng[PER], hn[PER], hv[PER], ghn[PER], dyv[PER];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int j = lane + 64 * u;
+            rg[u] = sigmoidf_(gi[j] + gh[j]);
+            zg[u] = sigmoidf_(gi[H + j] + gh[H + j]);
+            ghn[u] = gh[2 * H + j];
+            ng[u] = tanhf(gi[2 * H + j] + rg[u] * ghn[u]);
+            hv[u] = h[j];
+            hn[u] = (1.0f - zg[u]) * ng[u] + zg[u] * hv[u];
+            dyv[u] = g[j];
+            s1 += hn[u];
+            s2 += hn[u] * hn[u];
+        }
+        s1 = wave_sum_f32(s1);
+        s2 = wave_sum_f32(s2);
+        const float mean = s1 / (float)H;
+        const float var = fmaxf(s2 / (float)H - mean * mean, 0.0f);
+        const float rs = rsqrtf(var + 1e-6f);
+        float xh[PER], dxh[PER];
+        float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int j = lane + 64 * u;
+            xh[u] = (hn[u] - mean) * rs;
+            dxh[u] = dyv[u] * scale[j];
+            a1 += dxh[u];
+            a2 += dxh[u] * xh[u];
+            ps[u] += dyv[u] * xh[u];
+            pb[u] += dyv[u];
+        }
+        a1 = wave_sum_f32(a1) / (float)H;
+        a2 = wave_sum_f32(a2) / (float)H;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int j = lane + 64 * u;
+            const float dhn = rs * (dxh[u] - a1 - xh[u] * a2);
+            const float dn = dhn * (1.0f - zg[u]);
+            const float dz = dhn * (hv[u] - ng[u]);
+            const float dan = dn * (1.0f - ng[u] * ng[u]);
+            const float dr = dan * ghn[u];
+            const float dar = dr * rg[u] * (1.0f - rg[u]);
+            const float daz = dz * zg[u] * (1.0f - zg[u]);
+            float *di = dGi + (size_t)r * lddi, *dhh = dGh + (size_t)r * lddh;
+            di[j] = dar;
+            di[H + j] = daz;
+            di[2 * H + j] = dan;
+            dhh[j] = dar;
+            dhh[H + j] = daz;
+            dhh[2 * H + j] = dan * rg[u];
+            dh[(size_t)r * lddh_prev + j] += dhn * zg[u];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        s_part[w][lane + 64 * u] = ps[u];
+        s_part[w][64 * PER + lane + 64 * u] = pb[u];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < 2 * 64 * PER; j += kRowThreads) {
+        const float v = s_part[0][j] + s_part[1][j] + s_part[2][j] + s_part[3][j];
+        // part layout per block: [dscale (H) | dbias (H)]
+        const int half = j / (64 * PER), jj = j - half * 64 * PER;
+        if (jj < H) part[(size_t)blockIdx.x * 2 * H + half * H + jj] = v;
+    }
+}
+
+// dst[j] (+)= sum_b part[b][j]  (fixed order)
+__global__ void partial_reduce_kernel(const float *__restrict__ part, int nblocks, int width, float *__restrict__ dst,
+                                      int accumulate) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= width) return;
+    float s = 0.f;
+    for (int b = 0; b < nblocks; ++b) s += part[(size_t)b * width + j];
+    dst[j] = accumulate ? dst[j] + s : s;
+}
+
+// ------------------------------------------------------------ elementwise --
+__global__ void relu_fwd_kernel(float *__restrict__ x, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i] = fmaxf(x[i], 0.0f);
+}
+
+// dx = dy * (y > 0), in place on dy
+__global__ void relu_bwd_kernel(float *__restrict__ dy, const float *__restrict__ y, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && !(y[i] > 0.0f)) dy[i] = 0.0f;
+}
+
+// ---------------------------------------------------------- batch assembly --
+// Block per sample: instantiate the instance's graph templates at the sample's row
+// bases and compute its node features from the sample's assignment.
+__global__ void __launch_bounds__(256)
+assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__restrict__ inst,
+                            const uint8_t *__restrict__ x, const float *__restrict__ svf,
+                            const uint64_t *__restrict__ pool, const int *__restrict__ sb,
+                            const int *__restrict__ t_vgid, const int *__restrict__ t_cgid,
+                            const int *__restrict__ t_slots, const int *__restrict__ t_ptr,
+                            const int *__restrict__ t_inc, const int *__restrict__ voff, const int *__restrict__ coff,
+                            const int *__restrict__ eoff, const int *__restrict__ poff, const int *__restrict__ gv,
+                            const int *__restrict__ gc, float *__restrict__ vfeat, float *__restrict__ cfeat,
+                            int *__restrict__ slots, int *__restrict__ ptr, int *__restrict__ inc,
+                            int *__restrict__ g_vbase, int *__restrict__ g_nv, int *__restrict__ g_cbase,
+                            int *__restrict__ g_nc, int Nv, int nnz) {
+    const int s = blockIdx.x;
+    const int n = inst[s];
+    const int vr0 = sb[3 * s], cr0 = sb[3 * s + 1], e0 = sb[3 * s + 2];
+    const int tv0 = voff[n], tc0 = coff[n], te0 = eoff[n], tp0 = poff[n];
+    const int *gvn = gv + (size_t)n * (A + 2), *gcn = gc + (size_t)n * (A + 2);
+    const int nvr = gvn[G], ncr = gcn[G];
+    const int ne = t_ptr[tp0 + nvr];
+    const uint8_t *xs = x + (size_t)s * V;
+    for (int t = threadIdx.x; t < nvr; t += blockDim.x) {
+        const int gid = t_vgid[tv0 + t];
+        float *f = vfeat + (size_t)(vr0 + t) * 4;
+        const float *sv = svf + ((size_t)n * V + gid) * 3;
+        f[0] = (float)(xs[gid] & 1u);
+        f[1] = sv[0];
+        f[2] = sv[1];
+        f[3] = sv[2];
+        ptr[vr0 + t] = e0 + t_ptr[tp0 + t];
+    }
+    for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+        const int ent = t_inc[te0 + e];
+        inc[e0 + e] = ((cr0 + (ent >> 1)) << 1) | (ent & 1);
+    }
+    for (int t = threadIdx.x; t < ncr; t += blockDim.x) {
+        const int gcid = t_cgid[tc0 + t];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int sl = t_slots[(size_t)(tc0 + t) * 3 + j];
+            slots[(size_t)(cr0 + t) * 3 + j] = sl < 0 ? -1 : (((vr0 + (sl >> 1)) << 1) | (sl & 1));
+        }
+        const uint64_t w = pool[(size_t)n * C + gcid];
+        int ntrue = 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint32_t lit = (uint32_t)(w >> (16 * j)) & 0xFFFFu;
+            if (lit < MSAT_LIT_ABSENT) ntrue += (int)(((xs[lit >> 1] & 1u) ^ lit) & 1u);
+        }
+        float *f = cfeat + (size_t)(cr0 + t) * 3;
+        f[0] = ntrue > 0 ? 1.0f : 0.0f;
+        f[1] = (float)ntrue / 3.0f;
+        f[2] = 1.0f;
+    }
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        g_vbase[s * G + g] = vr0 + gvn[g];
+        g_nv[s * G + g] = gvn[g + 1] - gvn[g];
+        g_cbase[s * G + g] = cr0 + gcn[g];
+        g_nc[s * G + g] = gcn[g + 1] - gcn[g];
+    }
+    if (s == 0 && threadIdx.x == 0) ptr[Nv] = nnz;
+}
+
+}  // namespace msat
+
+using namespace msat;
+
+static int grid_rows(long rows) { return (int)std::min<long>((rows + 3) / 4, 8192); }
+
+extern "C" int msat_clause_gather(const float *src, int32_t ld_src, const int32_t *slots, float *dst, int32_t ld_dst,
+                                  int32_t num_clause_rows, int32_t H, int32_t accumulate, void *stream) {
+    MSAT_REQUIRE(src && slots && dst && H % 32 == 0 && ld_src % 4 == 0 && ld_dst % 4 == 0, "bad clause_gather args");
+    if (num_clause_rows == 0) return MSAT_OK;
+    hipLaunchKernelGGL(clause_gather_kernel, dim3(grid_rows(num_clause_rows)), dim3(kRowThreads), 0,
+                       (hipStream_t)stream, src, ld_src, slots, dst, ld_dst, num_clause_rows, H, accumulate);
+    return check_launch("clause_gather_kernel");
+}
+
+extern "C" int msat_var_gather(const float *src, int32_t ld_src, const int32_t *ptr, const int32_t *inc, float *dst,
+                               int32_t ld_dst, int32_t num_var_rows, int32_t H, int32_t accumulate, void *stream) {
+    MSAT_REQUIRE(src && ptr && inc && dst && H % 32 == 0 && ld_src % 4 == 0 && ld_dst % 4 == 0, "bad var_gather args");
+    if (num_var_rows == 0) return MSAT_OK;
+    hipLaunchKernelGGL(var_gather_kernel, dim3(grid_rows(num_var_rows)), dim3(kRowThreads), 0, (hipStream_t)stream,
+                       src, ld_src, ptr, inc, dst, ld_dst, num_var_rows, H, accumulate);
+    return check_launch("var_gather_kernel");
+}
+
+extern "C" int msat_gru_ln_fwd(const float *Gi, int32_t ldi, const float *Gh, int32_t ldh, const float *hprev,
+                               int32_t ldp, const float *ln_scale, const float *ln_bias, float *out, int32_t ldo,
+                               int32_t R, int32_t H, void *stream) {
+    MSAT_REQUIRE(Gi && Gh && hprev && ln_scale && ln_bias && out, "NULL pointer");
+    MSAT_REQUIRE(H == 64 || H == 128 || H == 256, "gru_ln: H must be 64, 128 or 256 (got %d)", H);
+    if (R == 0) return MSAT_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 g(grid_rows(R)), b(kRowThreads);
+    if (H == 64) hipLaunchKernelGGL(gru_ln_fwd_kernel<1>, g, b, 0, s, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, ln_bias, out, ldo, R, H);
+    else if (H == 128) hipLaunchKernelGGL(gru_ln_fwd_kernel<2>, g, b, 0, s, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, ln_bias, out, ldo, R, H);
+    else hipLaunchKernelGGL(gru_ln_fwd_kernel<4>, g, b, 0, s, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, ln_bias, out, ldo, R, H);
+    return check_launch("gru_ln_fwd_kernel");
+}
+
+extern "C" size_t msat_gru_ln_bwd_partial_floats(int32_t R, int32_t H) { return (size_t)grid_rows(R) * 2 * H; }
+
+extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, int32_t ldi, const float *Gh, int32_t ldh,
+                               const float *hprev, int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi,
+                               float *dGh, int32_t lddh, float *dhprev, int32_t lddp, float *dln_scale,
+                               float *dln_bias, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
+                               void *stream) {
+    MSAT_REQUIRE(dy && Gi && Gh && hprev && ln_scale && dGi && dGh && dhprev && dln_scale && dln_bias && partial,
+                 "NULL pointer");
+    MSAT_REQUIRE(H == 64 || H == 128 || H == 256, "gru_ln: H must be 64, 128 or 256 (got %d)", H);
+    MSAT_REQUIRE(dln_bias == dln_scale + H, "dln_bias must follow dln_scale (contiguous [scale|bias] grads)");
+    if (R == 0) return MSAT_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = grid_rows(R);
+    const dim3 g(nb), b(kRowThreads);
+    if (H == 64) hipLaunchKernelGGL(gru_ln_bwd_kernel<1>, g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    else if (H == 128) hipLaunchKernelGGL(gru_ln_bwd_kernel<2>, g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    else hipLaunchKernelGGL(gru_ln_bwd_kernel<4>, g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    int rc = check_launch("gru_ln_bwd_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((2 * H + 255) / 256), dim3(256), 0, s, partial, nb, 2 * H, dln_scale,
+                       accumulate_ln);
+    return check_launch("partial_reduce_kernel");
+}
+
+extern "C" int msat_assemble_graph_batch(
+    int32_t S, int32_t G, int32_t A, int32_t V, int32_t C, const int32_t *inst, const uint8_t *x, const float *svf,
+    const uint16_t *pool, const int32_t *sample_bases, const int32_t *t_vgid, const int32_t *t_cgid,
+    const int32_t *t_slots, const int32_t *t_ptr, const int32_t *t_inc, const int32_t *voff, const int32_t *coff,
+    const int32_t *eoff, const int32_t *poff, const int32_t *gv, const int32_t *gc, float *vfeat, float *cfeat,
+    int32_t *slots, int32_t *ptr, int32_t *inc, int32_t *g_vbase, int32_t *g_nv, int32_t *g_cbase, int32_t *g_nc,
+    int32_t Nv, int32_t nnz, void *stream) {
+    MSAT_REQUIRE(inst && x && svf && pool && sample_bases && t_vgid && t_cgid && t_slots && t_ptr && t_inc && voff &&
+                     coff && eoff && poff && gv && gc && vfeat && cfeat && slots && ptr && inc && g_vbase && g_nv &&
+                     g_cbase && g_nc,
+                 "NULL pointer");
+    MSAT_REQUIRE(G >= 1 && G <= A + 1, "G must be 1 (critic only) or A+1");
+    if (!S) return MSAT_OK;
+    hipLaunchKernelGGL(assemble_graph_batch_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, S, G, A, V, C, inst, x,
+                       svf, reinterpret_cast<const uint64_t *>(pool), sample_bases, t_vgid, t_cgid, t_slots, t_ptr,
+                       t_inc, voff, coff, eoff, poff, gv, gc, vfeat, cfeat, slots, ptr, inc, g_vbase, g_nv, g_cbase,
+                       g_nc, Nv, nnz);
+    return check_launch("assemble_graph_batch_kernel");
+}
+
+extern "C" int msat_relu(float *x, size_t n, void *stream) {
+    MSAT_REQUIRE(x, "NULL pointer");
+    if (!n) return MSAT_OK;
+    hipLaunchKernelGGL(relu_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, n);
+    return check_launch("relu_fwd_kernel");
+}
+
+extern "C" int msat_relu_bwd(float *dy, const float *y, size_t n, void *stream) {
+    MSAT_REQUIRE(dy && y, "NULL pointer");
+    if (!n) return MSAT_OK;
+    hipLaunchKernelGGL(relu_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dy, y, n);
+    return check_launch("relu_bwd_kernel");
+}

@@ -95,6 +95,32 @@ def _load():
             [c_int32, c_int32, P, c_int32, P, P, P, c_float, c_float, c_int32, P, P, P, P],
         ),
     }
+    # marlsat_net.h
+    sig["msat_gemm"] = (c_int32, [P, c_int32, P, c_int32, c_int32, P, c_int32, P, c_int32, c_int32, c_int32, c_int32,
+                                  P])
+    sig["msat_gemm_wgrad_workspace_bytes"] = (c_size_t, [c_int32, c_int32, c_int32])
+    sig["msat_gemm_wgrad"] = (c_int32, [P, c_int32, P, c_int32, P, c_int32, c_int32, c_int32, c_int32, c_int32, P, P])
+    I, F, Z, U = c_int32, c_float, c_size_t, c_uint64
+    sig["msat_assemble_graph_batch"] = (I, [I, I, I, I, I] + [P] * 25 + [I, I, P])
+    sig["msat_clause_gather"] = (I, [P, I, P, P, I, I, I, I, P])
+    sig["msat_var_gather"] = (I, [P, I, P, P, P, I, I, I, I, P])
+    sig["msat_gru_ln_fwd"] = (I, [P, I, P, I, P, I, P, P, P, I, I, I, P])
+    sig["msat_gru_ln_bwd_partial_floats"] = (Z, [I, I])
+    sig["msat_gru_ln_bwd"] = (I, [P, I, P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, I, I, I, P])
+    sig["msat_relu"] = (I, [P, Z, P])
+    sig["msat_relu_bwd"] = (I, [P, P, Z, P])
+    sig["msat_critic_pool"] = (I, [P, P, P, I, P, P, P, P, I, I, P, P])
+    sig["msat_critic_pool_bwd"] = (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, P, P])
+    sig["msat_actor_pool"] = (I, [P, P, P, I, P, P, P, P, I, I, I, I, I, I, P, I, P, P, P])
+    sig["msat_actor_pool_bwd"] = (I, [I, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P, P, P])
+    sig["msat_bcast_add_relu"] = (I, [P, P, I, I, I, P])
+    sig["msat_group_sum"] = (I, [P, I, I, I, P, P])
+    sig["msat_assemble_logits"] = (I, [P, P, I, I, I, I, I, P, P])
+    sig["msat_mask_var_logits"] = (I, [P, I, I, I, I, I, P])
+    sig["msat_split_dlogits"] = (I, [P, I, I, P, P, P])
+    sig["msat_sample_actions"] = (I, [P, I, I, I, U, U, P, P, P])
+    sig["msat_ppo_loss"] = (I, [P, I, I, I, I, I, I, P, P, P, P, P, P, F, F, F, F, I, P, P, P, P, P])
+    sig["msat_adam"] = (I, [P, P, P, P, Z, F, F, F, F, I, F, P])
     sig["msat_debug_fill"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])  # marlsat_debug.h
     sig["msat_debug_fill_chunked"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])
     for name, (res, args) in sig.items():
@@ -106,8 +132,33 @@ def _load():
 
 lib = _load()
 
-# Every symbol include/marlsat.h declares (checked by tests/test_capi.py).
+# Every symbol include/marlsat*.h declares (checked by tests/test_capi.py).
 EXPORTED = (
+    "msat_assemble_graph_batch",
+    "msat_clause_gather",
+    "msat_var_gather",
+    "msat_gru_ln_fwd",
+    "msat_gru_ln_bwd_partial_floats",
+    "msat_gru_ln_bwd",
+    "msat_relu",
+    "msat_relu_bwd",
+    "msat_critic_pool",
+    "msat_critic_pool_bwd",
+    "msat_actor_pool",
+    "msat_actor_pool_bwd",
+    "msat_bcast_add_relu",
+    "msat_group_sum",
+    "msat_assemble_logits",
+    "msat_mask_var_logits",
+    "msat_split_dlogits",
+    "msat_sample_actions",
+    "msat_ppo_loss",
+    "msat_adam",
+    "msat_gemm",
+    "msat_gemm_wgrad_workspace_bytes",
+    "msat_gemm_wgrad",
+    "msat_debug_fill",
+    "msat_debug_fill_chunked",
     "msat_last_error",
     "msat_version",
     "msat_pool_pack",

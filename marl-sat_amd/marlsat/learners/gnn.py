@@ -1,0 +1,462 @@
+"""GNN actor-critic on the device: forward, backward and Adam over the HIP kernels.
+
+Mirrors ``GNN_ActorCritic`` (src/learners/mappo_gnn_sat_learner.py:198-355) and
+``GNNEncoder`` (:19-82) on a ragged graph batch (graphs.py).  Every matmul is the
+fp32 MFMA GEMM of gemm.hip, the message passing is the signed literal gathers,
+GRU + LayerNorm and the heads are fused kernels; torch only allocates memory.
+
+Per message step l the forward keeps, for the backward pass, the step inputs
+(Hp, Hn, Hc), the gathered clause input, the var-side messages and the six GRU
+gate pre-activations; the backward walks the steps in reverse, accumulating
+every weight gradient through the split-M weight-gradient GEMM (fixed reduction
+order: the whole update is bitwise reproducible).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .. import _lib
+from . import params as P
+from .graphs import GraphBatch
+
+L_ = _lib.lib
+
+
+def _chk(rc, what):
+    if rc:
+        _lib.check(rc, what)
+
+
+class _Scratch:
+    """Grow-only device scratch (ones vector, wgrad workspace, LN partials)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.ones = torch.ones(1, device=device)
+        self.ws = torch.empty(1, device=device)
+        self.part = torch.empty(1, device=device)
+
+    def get_ones(self, n):
+        if self.ones.numel() < n:
+            self.ones = torch.ones(max(n, 2 * self.ones.numel()), device=self.device)
+        return self.ones
+
+    def get_ws(self, nbytes):
+        n = (nbytes + 3) // 4 + 1
+        if self.ws.numel() < n:
+            self.ws = torch.empty(max(n, 2 * self.ws.numel()), device=self.device)
+        return self.ws
+
+    def get_part(self, n):
+        if self.part.numel() < n:
+            self.part = torch.empty(max(n, 2 * self.part.numel()), device=self.device)
+        return self.part
+
+
+@dataclass
+class StepTape:
+    Hp: torch.Tensor
+    Hn: torch.Tensor
+    Hc: torch.Tensor
+    GIN: torch.Tensor  # (Nc, 2H) gathered clause input
+    GIc: torch.Tensor
+    GHc: torch.Tensor
+    NV: torch.Tensor  # (Nv, 2H) var-side messages
+    GIp: torch.Tensor
+    GHp: torch.Tensor
+    GIn: torch.Tensor
+    GHn: torch.Tensor
+
+
+@dataclass
+class HeadTape:
+    pooled: Optional[torch.Tensor] = None
+    c0: Optional[torch.Tensor] = None
+    c1: Optional[torch.Tensor] = None
+    my: Optional[torch.Tensor] = None
+    ctx: Optional[torch.Tensor] = None
+    h1: Optional[torch.Tensor] = None
+    n1: Optional[torch.Tensor] = None
+    h2: Optional[torch.Tensor] = None  # mode 1 second hidden layer
+
+
+class GNNActorCritic:
+    """Device GNN_ActorCritic with flat parameters (params.py layout)."""
+
+    def __init__(self, gnn_hidden_dim: int, gnn_num_message_passing_steps: int, num_agents: int,
+                 max_vars_per_agent: int, action_mode: int, num_vars: int, agent_id_embed_dim: int = 16,
+                 device=None, seed: int = 0):
+        self.H, self.L = gnn_hidden_dim, gnn_num_message_passing_steps
+        self.A, self.M, self.mode, self.E = num_agents, max_vars_per_agent, action_mode, agent_id_embed_dim
+        self.V = num_vars
+        self.base, self.rem = divmod(num_vars, num_agents)
+        self.CW = 5 * self.H + self.E
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.layout = P.layout(self.H, self.L, self.A, self.M, self.mode, self.E)
+        self.tab, self.size = P.offsets(self.layout)
+        self.params = torch.from_numpy(P.init_flat(self.H, self.L, self.A, self.M, self.mode, self.E, seed)).to(self.device)
+        self.grads = torch.zeros_like(self.params)
+        self.adam_m = torch.zeros_like(self.params)
+        self.adam_v = torch.zeros_like(self.params)
+        self.adam_count = 0
+        self.scr = _Scratch(self.device)
+
+    # ----------------------------------------------------------- plumbing ----
+    def load_flax(self, tree):
+        self.params.copy_(torch.from_numpy(P.from_flax(tree, self.H, self.L, self.A, self.M, self.mode, self.E)))
+
+    def to_flax(self, grads: bool = False):
+        t = (self.grads if grads else self.params).detach().cpu().numpy()
+        return P.to_flax(t, self.H, self.L, self.A, self.M, self.mode, self.E)
+
+    def p(self, name: str) -> torch.Tensor:
+        o, shp = self.tab[name]
+        return self.params[o: o + int(np.prod(shp))].view(shp)
+
+    def g(self, name: str) -> torch.Tensor:
+        o, shp = self.tab[name]
+        return self.grads[o: o + int(np.prod(shp))].view(shp)
+
+    @property
+    def stream(self):
+        return _lib.stream_ptr(self.device)
+
+    def _gemm(self, A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc=0):
+        _chk(L_.msat_gemm(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, self.stream), "msat_gemm")
+
+    def _wgrad(self, A, lda, G, ldg, W, ldw, M, K, N, acc=1):
+        if M == 0:
+            return
+        ws = self.scr.get_ws(int(L_.msat_gemm_wgrad_workspace_bytes(M, K, N)))
+        _chk(L_.msat_gemm_wgrad(A, lda, G, ldg, W, ldw, M, K, N, acc, ws.data_ptr(), self.stream), "msat_gemm_wgrad")
+
+    def _colsum(self, G, ldg, M, N, out, acc=1):
+        self._wgrad(self.scr.get_ones(M).data_ptr(), 1, G, ldg, out, N, M, 1, N, acc)
+
+    @staticmethod
+    def _ptr(t: torch.Tensor, col: int = 0) -> int:
+        return t.data_ptr() + col * t.element_size()
+
+    # ---------------------------------------------------------- encoder ----
+    def encode(self, b: GraphBatch, save: bool):
+        H, dev = self.H, self.device
+        Nv, Nc = b.Nv, b.Nc
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)
+        pp = self._ptr
+        Hp, Hn, Hc = e(Nv, H), e(Nv, H), e(Nc, H)
+        # literal / clause embeddings (learner:57-59): vfeat = [x | svf(3)]
+        self._gemm(pp(b.vfeat, 1), 4, self.p("enc.lpe_w").data_ptr(), H, 0, Hp.data_ptr(), H,
+                   self.p("enc.lpe_b").data_ptr(), Nv, H, 3)
+        self._gemm(pp(b.vfeat, 1), 4, self.p("enc.lne_w").data_ptr(), H, 0, Hn.data_ptr(), H,
+                   self.p("enc.lne_b").data_ptr(), Nv, H, 3)
+        self._gemm(b.cfeat.data_ptr(), 3, self.p("enc.ce_w").data_ptr(), H, 0, Hc.data_ptr(), H,
+                   self.p("enc.ce_b").data_ptr(), Nc, H, 3)
+        tape: List[StepTape] = []
+        ln = self.p("enc.ln")
+        for l in range(self.L):
+            MV = e(Nv, 2 * H)
+            self._gemm(Hp.data_ptr(), H, self.p("enc.phi_cp_w").data_ptr(), H, 0, MV.data_ptr(), 2 * H,
+                       self.p("enc.phi_cp_b").data_ptr(), Nv, H, H)
+            self._gemm(Hn.data_ptr(), H, self.p("enc.phi_cn_w").data_ptr(), H, 0, pp(MV, H), 2 * H,
+                       self.p("enc.phi_cn_b").data_ptr(), Nv, H, H)
+            GIN = e(Nc, 2 * H)
+            _chk(L_.msat_clause_gather(MV.data_ptr(), 2 * H, b.slots.data_ptr(), GIN.data_ptr(), 2 * H, Nc, H, 0,
+                                       self.stream), "clause_gather")
+            GIc, GHc, Hc1 = e(Nc, 3 * H), e(Nc, 3 * H), e(Nc, H)
+            self._gemm(GIN.data_ptr(), 2 * H, self.p("enc.gru_c_wi").data_ptr(), 3 * H, 0, GIc.data_ptr(), 3 * H,
+                       self.p("enc.gru_c_bi").data_ptr(), Nc, 3 * H, 2 * H)
+            self._gemm(Hc.data_ptr(), H, self.p("enc.gru_c_wh").data_ptr(), 3 * H, 0, GHc.data_ptr(), 3 * H,
+                       self.p("enc.gru_c_bh").data_ptr(), Nc, 3 * H, H)
+            _chk(L_.msat_gru_ln_fwd(GIc.data_ptr(), 3 * H, GHc.data_ptr(), 3 * H, Hc.data_ptr(), H, pp(ln[3 * l]),
+                                    pp(ln[3 * l], H), Hc1.data_ptr(), H, Nc, H, self.stream), "gru_ln_fwd")
+            TPN = e(Nc, 2 * H)
+            self._gemm(Hc1.data_ptr(), H, self.p("enc.phi_v_w").data_ptr(), 2 * H, 0, TPN.data_ptr(), 2 * H,
+                       self.p("enc.phi_v_b").data_ptr(), Nc, 2 * H, H)
+            NV = e(Nv, 2 * H)
+            _chk(L_.msat_var_gather(TPN.data_ptr(), 2 * H, b.ptr.data_ptr(), b.inc.data_ptr(), NV.data_ptr(), 2 * H,
+                                    Nv, H, 0, self.stream), "var_gather")
+            outs = []
+            for half, cell, Hx, k in ((0, "gru_vp", Hp, 3 * l + 1), (1, "gru_vn", Hn, 3 * l + 2)):
+                GI, GH, Hx1 = e(Nv, 3 * H), e(Nv, 3 * H), e(Nv, H)
+                wi = self.p(f"enc.{cell}_wi")
+                # input [n_v | x | svf] (learner:75,78): two GEMMs into the same gates
+                self._gemm(pp(NV, half * H), 2 * H, wi.data_ptr(), 3 * H, 0, GI.data_ptr(), 3 * H,
+                           self.p(f"enc.{cell}_bi").data_ptr(), Nv, 3 * H, H)
+                self._gemm(b.vfeat.data_ptr(), 4, pp(wi[H]), 3 * H, 0, GI.data_ptr(), 3 * H, None, Nv, 3 * H, 4, acc=1)
+                self._gemm(Hx.data_ptr(), H, self.p(f"enc.{cell}_wh").data_ptr(), 3 * H, 0, GH.data_ptr(), 3 * H,
+                           self.p(f"enc.{cell}_bh").data_ptr(), Nv, 3 * H, H)
+                _chk(L_.msat_gru_ln_fwd(GI.data_ptr(), 3 * H, GH.data_ptr(), 3 * H, Hx.data_ptr(), H, pp(ln[k]),
+                                        pp(ln[k], H), Hx1.data_ptr(), H, Nv, H, self.stream), "gru_ln_fwd")
+                outs.append((GI, GH, Hx1))
+            if save:
+                tape.append(StepTape(Hp, Hn, Hc, GIN, GIc, GHc, NV, outs[0][0], outs[0][1], outs[1][0], outs[1][1]))
+            Hp, Hn, Hc = outs[0][2], outs[1][2], Hc1
+        return Hp, Hn, Hc, tape
+
+    def encode_backward(self, b: GraphBatch, tape: List[StepTape], Hc_final, dHp, dHn, dHc):
+        H, dev = self.H, self.device
+        Nv, Nc = b.Nv, b.Nc
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)
+        pp = self._ptr
+        ln, dln = self.p("enc.ln"), self.g("enc.ln")
+        for l in range(self.L - 1, -1, -1):
+            t = tape[l]
+            Hc1 = tape[l + 1].Hc if l + 1 < self.L else Hc_final
+            dNV = e(Nv, 2 * H)
+            dprev = {}
+            for half, cell, Hx, GI, GH, dHx, k in ((0, "gru_vp", t.Hp, t.GIp, t.GHp, dHp, 3 * l + 1),
+                                                  (1, "gru_vn", t.Hn, t.GIn, t.GHn, dHn, 3 * l + 2)):
+                dGI, dGH = e(Nv, 3 * H), e(Nv, 3 * H)
+                dHx0 = torch.zeros((Nv, H), dtype=torch.float32, device=dev)
+                part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nv, H)))
+                _chk(L_.msat_gru_ln_bwd(dHx.data_ptr(), H, GI.data_ptr(), 3 * H, GH.data_ptr(), 3 * H, Hx.data_ptr(), H,
+                                        pp(ln[k]), dGI.data_ptr(), 3 * H, dGH.data_ptr(), 3 * H, dHx0.data_ptr(), H,
+                                        pp(dln[k]), pp(dln[k], H), part.data_ptr(), Nv, H, 1, self.stream),
+                     "gru_ln_bwd")
+                wi, wh = self.p(f"enc.{cell}_wi"), self.p(f"enc.{cell}_wh")
+                gwi, gwh = self.g(f"enc.{cell}_wi"), self.g(f"enc.{cell}_wh")
+                # hidden path
+                self._gemm(dGH.data_ptr(), 3 * H, wh.data_ptr(), 3 * H, 1, dHx0.data_ptr(), H, None, Nv, H, 3 * H, 1)
+                self._wgrad(Hx.data_ptr(), H, dGH.data_ptr(), 3 * H, gwh.data_ptr(), 3 * H, Nv, H, 3 * H)
+                self._colsum(pp(dGH, 2 * H), 3 * H, Nv, H, pp(self.g(f"enc.{cell}_bh"), 2 * H))
+                # input path [n_v | x | svf]
+                self._gemm(dGI.data_ptr(), 3 * H, wi.data_ptr(), 3 * H, 1, pp(dNV, half * H), 2 * H, None, Nv, H,
+                           3 * H, 0)
+                self._wgrad(pp(t.NV, half * H), 2 * H, dGI.data_ptr(), 3 * H, gwi.data_ptr(), 3 * H, Nv, H, 3 * H)
+                self._wgrad(b.vfeat.data_ptr(), 4, dGI.data_ptr(), 3 * H, pp(gwi[H]), 3 * H, Nv, 4, 3 * H)
+                self._colsum(dGI.data_ptr(), 3 * H, Nv, 3 * H, self.g(f"enc.{cell}_bi").data_ptr())
+                dprev[half] = dHx0
+            # var gather backward = clause gather of dNV
+            dTPN = e(Nc, 2 * H)
+            _chk(L_.msat_clause_gather(dNV.data_ptr(), 2 * H, b.slots.data_ptr(), dTPN.data_ptr(), 2 * H, Nc, H, 0,
+                                       self.stream), "clause_gather")
+            self._gemm(dTPN.data_ptr(), 2 * H, self.p("enc.phi_v_w").data_ptr(), 2 * H, 1, dHc.data_ptr(), H, None,
+                       Nc, H, 2 * H, 1)
+            self._wgrad(Hc1.data_ptr(), H, dTPN.data_ptr(), 2 * H, self.g("enc.phi_v_w").data_ptr(), 2 * H, Nc, H,
+                        2 * H)
+            self._colsum(dTPN.data_ptr(), 2 * H, Nc, 2 * H, self.g("enc.phi_v_b").data_ptr())
+            # clause GRU
+            dGI, dGH = e(Nc, 3 * H), e(Nc, 3 * H)
+            dHc0 = torch.zeros((Nc, H), dtype=torch.float32, device=dev)
+            part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nc, H)))
+            _chk(L_.msat_gru_ln_bwd(dHc.data_ptr(), H, t.GIc.data_ptr(), 3 * H, t.GHc.data_ptr(), 3 * H,
+                                    t.Hc.data_ptr(), H, pp(ln[3 * l]), dGI.data_ptr(), 3 * H, dGH.data_ptr(), 3 * H,
+                                    dHc0.data_ptr(), H, pp(dln[3 * l]), pp(dln[3 * l], H), part.data_ptr(), Nc, H, 1,
+                                    self.stream), "gru_ln_bwd")
+            self._gemm(dGH.data_ptr(), 3 * H, self.p("enc.gru_c_wh").data_ptr(), 3 * H, 1, dHc0.data_ptr(), H, None,
+                       Nc, H, 3 * H, 1)
+            self._wgrad(t.Hc.data_ptr(), H, dGH.data_ptr(), 3 * H, self.g("enc.gru_c_wh").data_ptr(), 3 * H, Nc, H,
+                        3 * H)
+            self._colsum(pp(dGH, 2 * H), 3 * H, Nc, H, pp(self.g("enc.gru_c_bh"), 2 * H))
+            dGIN = e(Nc, 2 * H)
+            self._gemm(dGI.data_ptr(), 3 * H, self.p("enc.gru_c_wi").data_ptr(), 3 * H, 1, dGIN.data_ptr(), 2 * H,
+                       None, Nc, 2 * H, 3 * H, 0)
+            self._wgrad(t.GIN.data_ptr(), 2 * H, dGI.data_ptr(), 3 * H, self.g("enc.gru_c_wi").data_ptr(), 3 * H, Nc,
+                        2 * H, 3 * H)
+            self._colsum(dGI.data_ptr(), 3 * H, Nc, 3 * H, self.g("enc.gru_c_bi").data_ptr())
+            # clause gather backward = var gather of dGIN
+            dMV = e(Nv, 2 * H)
+            _chk(L_.msat_var_gather(dGIN.data_ptr(), 2 * H, b.ptr.data_ptr(), b.inc.data_ptr(), dMV.data_ptr(),
+                                    2 * H, Nv, H, 0, self.stream), "var_gather")
+            for half, nm, Hx, dst in ((0, "phi_cp", t.Hp, dprev[0]), (1, "phi_cn", t.Hn, dprev[1])):
+                self._gemm(pp(dMV, half * H), 2 * H, self.p(f"enc.{nm}_w").data_ptr(), H, 1, dst.data_ptr(), H,
+                           None, Nv, H, H, 1)
+                self._wgrad(Hx.data_ptr(), H, pp(dMV, half * H), 2 * H, self.g(f"enc.{nm}_w").data_ptr(), H, Nv, H, H)
+                self._colsum(pp(dMV, half * H), 2 * H, Nv, H, self.g(f"enc.{nm}_b").data_ptr())
+            dHp, dHn, dHc = dprev[0], dprev[1], dHc0
+        # embeddings
+        self._wgrad(pp(b.vfeat, 1), 4, dHp.data_ptr(), H, self.g("enc.lpe_w").data_ptr(), H, Nv, 3, H)
+        self._colsum(dHp.data_ptr(), H, Nv, H, self.g("enc.lpe_b").data_ptr())
+        self._wgrad(pp(b.vfeat, 1), 4, dHn.data_ptr(), H, self.g("enc.lne_w").data_ptr(), H, Nv, 3, H)
+        self._colsum(dHn.data_ptr(), H, Nv, H, self.g("enc.lne_b").data_ptr())
+        self._wgrad(b.cfeat.data_ptr(), 3, dHc.data_ptr(), H, self.g("enc.ce_w").data_ptr(), H, Nc, 3, H)
+        self._colsum(dHc.data_ptr(), H, Nc, H, self.g("enc.ce_b").data_ptr())
+
+    # ------------------------------------------------------------ heads ----
+    def _gr(self, b: GraphBatch):
+        return b.vbase.data_ptr(), b.nv.data_ptr(), b.cbase.data_ptr(), b.nc.data_ptr()
+
+    def critic_head(self, b: GraphBatch, Hp, Hn, Hc, ht: HeadTape):
+        H, S = self.H, b.S
+        pooled = torch.empty((S, 6 * H), device=self.device)
+        _chk(L_.msat_critic_pool(Hp.data_ptr(), Hn.data_ptr(), Hc.data_ptr(), H, *self._gr(b), b.G, S,
+                                 pooled.data_ptr(), self.stream), "critic_pool")
+        c0 = torch.empty((S, 128), device=self.device)
+        self._gemm(pooled.data_ptr(), 6 * H, self.p("crit.d0_w").data_ptr(), 128, 0, c0.data_ptr(), 128,
+                   self.p("crit.d0_b").data_ptr(), S, 128, 6 * H)
+        _chk(L_.msat_relu(c0.data_ptr(), c0.numel(), self.stream), "relu")
+        c1 = torch.empty((S, 64), device=self.device)
+        self._gemm(c0.data_ptr(), 128, self.p("crit.d1_w").data_ptr(), 64, 0, c1.data_ptr(), 64,
+                   self.p("crit.d1_b").data_ptr(), S, 64, 128)
+        _chk(L_.msat_relu(c1.data_ptr(), c1.numel(), self.stream), "relu")
+        val = torch.empty((S,), device=self.device)
+        self._gemm(c1.data_ptr(), 64, self.p("crit.out_w").data_ptr(), 1, 0, val.data_ptr(), 1,
+                   self.p("crit.out_b").data_ptr(), S, 1, 64)
+        ht.pooled, ht.c0, ht.c1 = pooled, c0, c1
+        return val
+
+    def critic_head_backward(self, b, Hp, Hn, Hc, ht: HeadTape, dval, dHp, dHn, dHc):
+        H, S, dev = self.H, b.S, self.device
+        dc1 = torch.empty((S, 64), device=dev)
+        self._gemm(dval.data_ptr(), 1, self.p("crit.out_w").data_ptr(), 1, 1, dc1.data_ptr(), 64, None, S, 64, 1)
+        self._wgrad(ht.c1.data_ptr(), 64, dval.data_ptr(), 1, self.g("crit.out_w").data_ptr(), 1, S, 64, 1)
+        self._colsum(dval.data_ptr(), 1, S, 1, self.g("crit.out_b").data_ptr())
+        _chk(L_.msat_relu_bwd(dc1.data_ptr(), ht.c1.data_ptr(), dc1.numel(), self.stream), "relu_bwd")
+        dc0 = torch.empty((S, 128), device=dev)
+        self._gemm(dc1.data_ptr(), 64, self.p("crit.d1_w").data_ptr(), 64, 1, dc0.data_ptr(), 128, None, S, 128, 64)
+        self._wgrad(ht.c0.data_ptr(), 128, dc1.data_ptr(), 64, self.g("crit.d1_w").data_ptr(), 64, S, 128, 64)
+        self._colsum(dc1.data_ptr(), 64, S, 64, self.g("crit.d1_b").data_ptr())
+        _chk(L_.msat_relu_bwd(dc0.data_ptr(), ht.c0.data_ptr(), dc0.numel(), self.stream), "relu_bwd")
+        dpooled = torch.empty((S, 6 * H), device=dev)
+        self._gemm(dc0.data_ptr(), 128, self.p("crit.d0_w").data_ptr(), 128, 1, dpooled.data_ptr(), 6 * H, None, S,
+                   6 * H, 128)
+        self._wgrad(ht.pooled.data_ptr(), 6 * H, dc0.data_ptr(), 128, self.g("crit.d0_w").data_ptr(), 128, S, 6 * H,
+                    128)
+        self._colsum(dc0.data_ptr(), 128, S, 128, self.g("crit.d0_b").data_ptr())
+        _chk(L_.msat_critic_pool_bwd(Hp.data_ptr(), Hn.data_ptr(), Hc.data_ptr(), H, *self._gr(b), b.G, S,
+                                     dpooled.data_ptr(), dHp.data_ptr(), dHn.data_ptr(), dHc.data_ptr(), self.stream),
+             "critic_pool_bwd")
+
+    def actor_head(self, b: GraphBatch, Hp, Hn, Hc, ht: HeadTape):
+        H, S, A, M, CW, dev = self.H, b.S, self.A, self.M, self.CW, self.device
+        SA = S * A
+        my = torch.empty((SA * M, 2 * H), device=dev)
+        ctx = torch.empty((SA, CW), device=dev)
+        _chk(L_.msat_actor_pool(Hp.data_ptr(), Hn.data_ptr(), Hc.data_ptr(), H, *self._gr(b), b.G, S, A, M, self.base,
+                                self.rem, self.p("actor.id_emb").data_ptr(), self.E, my.data_ptr(), ctx.data_ptr(),
+                                self.stream), "actor_pool")
+        ht.my, ht.ctx = my, ctx
+        pp = self._ptr
+        if self.mode == 0:
+            w1 = self.p("actor.flip_d_w")
+            Pm = torch.empty((SA, 128), device=dev)
+            self._gemm(ctx.data_ptr(), CW, pp(w1[2 * H]), 128, 0, Pm.data_ptr(), 128, None, SA, 128, CW)
+            h1 = torch.empty((SA * M, 128), device=dev)
+            self._gemm(my.data_ptr(), 2 * H, w1.data_ptr(), 128, 0, h1.data_ptr(), 128,
+                       self.p("actor.flip_d_b").data_ptr(), SA * M, 128, 2 * H)
+            _chk(L_.msat_bcast_add_relu(h1.data_ptr(), Pm.data_ptr(), SA, M, 128, self.stream), "bcast_add_relu")
+            fl = torch.empty((SA * M,), device=dev)
+            self._gemm(h1.data_ptr(), 128, self.p("actor.flip_o_w").data_ptr(), 1, 0, fl.data_ptr(), 1,
+                       self.p("actor.flip_o_b").data_ptr(), SA * M, 1, 128)
+            n1 = torch.empty((SA, 64), device=dev)
+            self._gemm(ctx.data_ptr(), CW, self.p("actor.noop_d_w").data_ptr(), 64, 0, n1.data_ptr(), 64,
+                       self.p("actor.noop_d_b").data_ptr(), SA, 64, CW)
+            _chk(L_.msat_relu(n1.data_ptr(), n1.numel(), self.stream), "relu")
+            no = torch.empty((SA,), device=dev)
+            self._gemm(n1.data_ptr(), 64, self.p("actor.noop_o_w").data_ptr(), 1, 0, no.data_ptr(), 1,
+                       self.p("actor.noop_o_b").data_ptr(), SA, 1, 64)
+            logits = torch.empty((S, A, M + 1), device=dev)
+            _chk(L_.msat_assemble_logits(fl.data_ptr(), no.data_ptr(), SA, A, M, self.base, self.rem,
+                                         logits.data_ptr(), self.stream), "assemble_logits")
+            ht.h1, ht.n1 = h1, n1
+            return logits
+        w0 = self.p("actor.d0_w")
+        Pm = torch.empty((SA, 128), device=dev)
+        self._gemm(pp(ctx, 5 * H), CW, pp(w0[2 * H]), 128, 0, Pm.data_ptr(), 128, None, SA, 128, self.E)
+        h1 = torch.empty((SA * M, 128), device=dev)
+        self._gemm(my.data_ptr(), 2 * H, w0.data_ptr(), 128, 0, h1.data_ptr(), 128, self.p("actor.d0_b").data_ptr(),
+                   SA * M, 128, 2 * H)
+        _chk(L_.msat_bcast_add_relu(h1.data_ptr(), Pm.data_ptr(), SA, M, 128, self.stream), "bcast_add_relu")
+        h2 = torch.empty((SA * M, 64), device=dev)
+        self._gemm(h1.data_ptr(), 128, self.p("actor.d1_w").data_ptr(), 64, 0, h2.data_ptr(), 64,
+                   self.p("actor.d1_b").data_ptr(), SA * M, 64, 128)
+        _chk(L_.msat_relu(h2.data_ptr(), h2.numel(), self.stream), "relu")
+        logits = torch.empty((S, A, M, 2), device=dev)
+        self._gemm(h2.data_ptr(), 64, self.p("actor.out_w").data_ptr(), 2, 0, logits.data_ptr(), 2,
+                   self.p("actor.out_b").data_ptr(), SA * M, 2, 64)
+        _chk(L_.msat_mask_var_logits(logits.data_ptr(), SA, A, M, self.base, self.rem, self.stream), "mask_logits")
+        ht.h1, ht.h2 = h1, h2
+        return logits
+
+    def actor_head_backward(self, b, ht: HeadTape, dlogits, dHp, dHn, dHc):
+        H, S, A, M, CW, dev = self.H, b.S, self.A, self.M, self.CW, self.device
+        SA = S * A
+        pp = self._ptr
+        dmy = torch.empty((SA * M, 2 * H), device=dev)
+        dctx = torch.empty((SA, CW), device=dev)
+        if self.mode == 0:
+            dfl = torch.empty((SA * M,), device=dev)
+            dno = torch.empty((SA,), device=dev)
+            _chk(L_.msat_split_dlogits(dlogits.data_ptr(), SA, M, dfl.data_ptr(), dno.data_ptr(), self.stream),
+                 "split_dlogits")
+            dh1 = torch.empty((SA * M, 128), device=dev)
+            self._gemm(dfl.data_ptr(), 1, self.p("actor.flip_o_w").data_ptr(), 1, 1, dh1.data_ptr(), 128, None,
+                       SA * M, 128, 1)
+            self._wgrad(ht.h1.data_ptr(), 128, dfl.data_ptr(), 1, self.g("actor.flip_o_w").data_ptr(), 1, SA * M, 128, 1)
+            self._colsum(dfl.data_ptr(), 1, SA * M, 1, self.g("actor.flip_o_b").data_ptr())
+            _chk(L_.msat_relu_bwd(dh1.data_ptr(), ht.h1.data_ptr(), dh1.numel(), self.stream), "relu_bwd")
+            dP = torch.empty((SA, 128), device=dev)
+            _chk(L_.msat_group_sum(dh1.data_ptr(), SA, M, 128, dP.data_ptr(), self.stream), "group_sum")
+            w1, gw1 = self.p("actor.flip_d_w"), self.g("actor.flip_d_w")
+            self._gemm(dh1.data_ptr(), 128, w1.data_ptr(), 128, 1, dmy.data_ptr(), 2 * H, None, SA * M, 2 * H, 128)
+            self._wgrad(ht.my.data_ptr(), 2 * H, dh1.data_ptr(), 128, gw1.data_ptr(), 128, SA * M, 2 * H, 128)
+            self._colsum(dh1.data_ptr(), 128, SA * M, 128, self.g("actor.flip_d_b").data_ptr())
+            self._gemm(dP.data_ptr(), 128, pp(w1[2 * H]), 128, 1, dctx.data_ptr(), CW, None, SA, CW, 128)
+            self._wgrad(ht.ctx.data_ptr(), CW, dP.data_ptr(), 128, pp(gw1[2 * H]), 128, SA, CW, 128)
+            dn1 = torch.empty((SA, 64), device=dev)
+            self._gemm(dno.data_ptr(), 1, self.p("actor.noop_o_w").data_ptr(), 1, 1, dn1.data_ptr(), 64, None, SA, 64, 1)
+            self._wgrad(ht.n1.data_ptr(), 64, dno.data_ptr(), 1, self.g("actor.noop_o_w").data_ptr(), 1, SA, 64, 1)
+            self._colsum(dno.data_ptr(), 1, SA, 1, self.g("actor.noop_o_b").data_ptr())
+            _chk(L_.msat_relu_bwd(dn1.data_ptr(), ht.n1.data_ptr(), dn1.numel(), self.stream), "relu_bwd")
+            self._gemm(dn1.data_ptr(), 64, self.p("actor.noop_d_w").data_ptr(), 64, 1, dctx.data_ptr(), CW, None, SA,
+                       CW, 64, 1)
+            self._wgrad(ht.ctx.data_ptr(), CW, dn1.data_ptr(), 64, self.g("actor.noop_d_w").data_ptr(), 64, SA, CW, 64)
+            self._colsum(dn1.data_ptr(), 64, SA, 64, self.g("actor.noop_d_b").data_ptr())
+        else:
+            dh2 = torch.empty((SA * M, 64), device=dev)
+            self._gemm(dlogits.data_ptr(), 2, self.p("actor.out_w").data_ptr(), 2, 1, dh2.data_ptr(), 64, None, SA * M,
+                       64, 2)
+            self._wgrad(ht.h2.data_ptr(), 64, dlogits.data_ptr(), 2, self.g("actor.out_w").data_ptr(), 2, SA * M, 64, 2)
+            self._colsum(dlogits.data_ptr(), 2, SA * M, 2, self.g("actor.out_b").data_ptr())
+            _chk(L_.msat_relu_bwd(dh2.data_ptr(), ht.h2.data_ptr(), dh2.numel(), self.stream), "relu_bwd")
+            dh1 = torch.empty((SA * M, 128), device=dev)
+            self._gemm(dh2.data_ptr(), 64, self.p("actor.d1_w").data_ptr(), 64, 1, dh1.data_ptr(), 128, None, SA * M,
+                       128, 64)
+            self._wgrad(ht.h1.data_ptr(), 128, dh2.data_ptr(), 64, self.g("actor.d1_w").data_ptr(), 64, SA * M, 128, 64)
+            self._colsum(dh2.data_ptr(), 64, SA * M, 64, self.g("actor.d1_b").data_ptr())
+            _chk(L_.msat_relu_bwd(dh1.data_ptr(), ht.h1.data_ptr(), dh1.numel(), self.stream), "relu_bwd")
+            dP = torch.empty((SA, 128), device=dev)
+            _chk(L_.msat_group_sum(dh1.data_ptr(), SA, M, 128, dP.data_ptr(), self.stream), "group_sum")
+            w0, gw0 = self.p("actor.d0_w"), self.g("actor.d0_w")
+            self._gemm(dh1.data_ptr(), 128, w0.data_ptr(), 128, 1, dmy.data_ptr(), 2 * H, None, SA * M, 2 * H, 128)
+            self._wgrad(ht.my.data_ptr(), 2 * H, dh1.data_ptr(), 128, gw0.data_ptr(), 128, SA * M, 2 * H, 128)
+            self._colsum(dh1.data_ptr(), 128, SA * M, 128, self.g("actor.d0_b").data_ptr())
+            dctx.zero_()
+            self._gemm(dP.data_ptr(), 128, pp(w0[2 * H]), 128, 1, pp(dctx, 5 * H), CW, None, SA, self.E, 128)
+            self._wgrad(pp(ht.ctx, 5 * H), CW, dP.data_ptr(), 128, pp(gw0[2 * H]), 128, SA, self.E, 128)
+        did = torch.empty((SA, self.E), device=dev)
+        _chk(L_.msat_actor_pool_bwd(H, *self._gr(b), b.G, S, A, M, self.base, self.rem, self.E, dmy.data_ptr(),
+                                    dctx.data_ptr(), dHp.data_ptr(), dHn.data_ptr(), dHc.data_ptr(), did.data_ptr(),
+                                    self.stream), "actor_pool_bwd")
+        self._colsum(did.data_ptr(), A * self.E, S, A * self.E, self.g("actor.id_emb").data_ptr())
+
+    # ---------------------------------------------------------- top level ----
+    def forward(self, b: GraphBatch, actor: bool = True, critic: bool = True, save: bool = False):
+        Hp, Hn, Hc, tape = self.encode(b, save)
+        ht = HeadTape()
+        logits = self.actor_head(b, Hp, Hn, Hc, ht) if actor else None
+        value = self.critic_head(b, Hp, Hn, Hc, ht) if critic else None
+        state = (Hp, Hn, Hc, tape, ht) if save else None
+        return logits, value, state
+
+    def backward(self, b: GraphBatch, state, dlogits: Optional[torch.Tensor], dvalue: Optional[torch.Tensor]):
+        """Accumulate parameter gradients (self.grads += ...) for upstream grads of logits / value."""
+        Hp, Hn, Hc, tape, ht = state
+        dHp = torch.zeros_like(Hp)
+        dHn = torch.zeros_like(Hn)
+        dHc = torch.zeros_like(Hc)
+        if dvalue is not None:
+            self.critic_head_backward(b, Hp, Hn, Hc, ht, dvalue, dHp, dHn, dHc)
+        if dlogits is not None:
+            self.actor_head_backward(b, ht, dlogits, dHp, dHn, dHc)
+        self.encode_backward(b, tape, Hc, dHp, dHn, dHc)
+
+    def adam_step(self, lr: float, grad_scale: float = 1.0, b1=0.9, b2=0.999, eps=1e-8):
+        self.adam_count += 1
+        _chk(L_.msat_adam(self.params.data_ptr(), self.grads.data_ptr(), self.adam_m.data_ptr(),
+                          self.adam_v.data_ptr(), self.size, float(lr), b1, b2, eps, self.adam_count,
+                          float(grad_scale), self.stream), "adam")

@@ -1,0 +1,207 @@
+"""Graph templates + device batch assembly for the GNN encoder.
+
+The reference runs ONE full-size encoder per agent with a masked dense V x C
+adjacency (``GNN_ActorCritic.apply_actor``, learner:243-276) plus one unmasked
+encoder for the critic (:340-342).  An agent's mask keeps exactly the edges
+between its *visible* vars (own vars + vars of clauses touching them) and its
+*related* clauses (clauses touching an own var), and every var of a related
+clause is visible, so the masked graph's visible/related nodes form a closed
+subgraph: their states are identical to the masked full-size computation, and
+the other nodes never reach the pooled outputs (learner:287-301).  Hence each
+sample is encoded as a ragged batch of small graphs:
+
+  graph 0      critic, all V vars and C clauses
+  graph 1 + i  agent i, vars = own (in order) ++ neighbours (ascending), clauses = related (ascending)
+
+Templates are built once per (problem pool, agent partition) on the host (static
+data preparation, like packing the pool) and uploaded; per micro-batch a HIP
+kernel instantiates them for the sampled (instance, assignment) pairs.  The
+adjacency used here is the network's (``create_static_graph``, literal 0 adds
+nothing), not the env's literal-0 quirk.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _lib
+
+
+def _agent_of(v, base, rem):
+    split = rem * (base + 1)
+    return np.where(v < split, v // (base + 1), rem + (v - split) // max(base, 1))
+
+
+def instance_graphs(clauses: np.ndarray, V: int, A: int):
+    """Graphs of one instance: list of (var_ids, clause_ids) for g = 0..A."""
+    C, K = clauses.shape
+    base, rem = divmod(V, A)
+    vid = np.abs(clauses).astype(np.int64) - 1
+    real = clauses != 0
+    ag = np.where(real, _agent_of(np.maximum(vid, 0), base, rem), -1)
+    graphs = [(np.arange(V), np.arange(C))]
+    for i in range(A):
+        lo = i * base + min(i, rem)
+        n = base + (1 if i < rem else 0)
+        own = np.arange(lo, lo + n)
+        rel = np.nonzero((ag == i).any(axis=1))[0]
+        vis = np.unique(vid[rel][real[rel]])
+        nbr = vis[(vis < lo) | (vis >= lo + n)]
+        graphs.append((np.concatenate([own, nbr]), rel))
+    return graphs
+
+
+@dataclass
+class Templates:
+    """Flattened per-instance templates (host numpy), graph 0 first in every array."""
+
+    vgid: np.ndarray  # (sum vrows,) global var id of each var row
+    cgid: np.ndarray  # (sum crows,) global clause id of each clause row
+    slots: np.ndarray  # (sum crows, 3) instance-relative (var_row << 1 | neg) or -1
+    ptr: np.ndarray  # (sum vrows + N,) per instance: instance-relative CSR pointer (vrows+1 entries)
+    inc: np.ndarray  # (sum nnz,) instance-relative (clause_row << 1 | neg)
+    voff: np.ndarray  # (N+1,) var-row offset of each instance
+    coff: np.ndarray  # (N+1,) clause-row offset
+    eoff: np.ndarray  # (N+1,) incidence offset
+    poff: np.ndarray  # (N+1,) ptr offset (voff + n)
+    gv: np.ndarray  # (N, A+2) graph var-row starts within the instance (cumulative, last = total)
+    gc: np.ndarray  # (N, A+2)
+    ge: np.ndarray  # (N, A+2) incidence starts per graph
+
+
+def build_templates(pool_clauses: np.ndarray, V: int, A: int) -> Templates:
+    N, C, K = pool_clauses.shape
+    vgid, cgid, slots, ptrs, incs = [], [], [], [], []
+    voff, coff, eoff, poff = [0], [0], [0], [0]
+    gv = np.zeros((N, A + 2), np.int64)
+    gc = np.zeros((N, A + 2), np.int64)
+    ge = np.zeros((N, A + 2), np.int64)
+    for n in range(N):
+        cl = pool_clauses[n]
+        vid = np.abs(cl).astype(np.int64) - 1
+        neg = (cl < 0).astype(np.int64)
+        real = cl != 0
+        vr, cr = 0, 0
+        s_list, v_list, c_list = [], [], []
+        for g, (vars_g, cls_g) in enumerate(instance_graphs(cl, V, A)):
+            gv[n, g], gc[n, g] = vr, cr
+            local = np.full(V, -1, np.int64)
+            local[vars_g] = np.arange(len(vars_g)) + vr
+            sv = vid[cls_g]
+            lv = np.where(real[cls_g], local[np.maximum(sv, 0)], -1)
+            assert (lv[real[cls_g]] >= 0).all(), "related clause with an invisible var"
+            s = np.where(lv >= 0, (lv << 1) | neg[cls_g], -1)
+            if K < 3:
+                s = np.concatenate([s, np.full((len(cls_g), 3 - K), -1, np.int64)], 1)
+            s_list.append(s)
+            v_list.append(vars_g)
+            c_list.append(cls_g)
+            vr += len(vars_g)
+            cr += len(cls_g)
+        gv[n, A + 1], gc[n, A + 1] = vr, cr
+        s_all = np.concatenate(s_list)  # (crows, 3)
+        # var-side CSR (transpose of the slots), entries in (clause row, slot) order
+        crow_idx = np.repeat(np.arange(cr), 3)
+        flat = s_all.reshape(-1)
+        keep = flat >= 0
+        vrow = flat[keep] >> 1
+        ent = (crow_idx[keep] << 1) | (flat[keep] & 1)
+        order = np.argsort(vrow, kind="stable")
+        vrow, ent = vrow[order], ent[order]
+        counts = np.bincount(vrow, minlength=vr)
+        ptr = np.concatenate([[0], np.cumsum(counts)])
+        # incidence start of each graph = ptr at its first var row
+        for g in range(A + 2):
+            ge[n, g] = ptr[gv[n, g]]
+        vgid.append(np.concatenate(v_list))
+        cgid.append(np.concatenate(c_list))
+        slots.append(s_all)
+        ptrs.append(ptr)
+        incs.append(ent)
+        voff.append(voff[-1] + vr)
+        coff.append(coff[-1] + cr)
+        eoff.append(eoff[-1] + len(ent))
+        poff.append(poff[-1] + vr + 1)
+    i32 = lambda a: np.asarray(a, np.int32)
+    return Templates(i32(np.concatenate(vgid)), i32(np.concatenate(cgid)), i32(np.concatenate(slots)),
+                     i32(np.concatenate(ptrs)), i32(np.concatenate(incs)), i32(voff), i32(coff), i32(eoff),
+                     i32(poff), i32(gv), i32(gc), i32(ge))
+
+
+class DeviceTemplates:
+    """Templates resident on the device + per-instance totals for batch sizing."""
+
+    def __init__(self, t: Templates, A: int, device):
+        dv = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        self.A, self.G = A, A + 1
+        self.vgid, self.cgid, self.slots = dv(t.vgid), dv(t.cgid), dv(t.slots)
+        self.ptr, self.inc = dv(t.ptr), dv(t.inc)
+        self.voff, self.coff, self.eoff, self.poff = dv(t.voff), dv(t.coff), dv(t.eoff), dv(t.poff)
+        self.gv, self.gc, self.ge = dv(t.gv), dv(t.gc), dv(t.ge)
+        # rows per instance for a full (critic + agents) sample and for a critic-only sample
+        self.full_v = dv(t.gv[:, -1])
+        self.full_c = dv(t.gc[:, -1])
+        self.full_e = dv(t.ge[:, -1])
+        self.crit_v = dv(t.gv[:, 1])
+        self.crit_c = dv(t.gc[:, 1])
+        self.crit_e = dv(t.ge[:, 1])
+        self.max_full_rows = int((t.gv[:, -1] + t.gc[:, -1]).max())
+        self.mean_full_rows = float((t.gv[:, -1] + t.gc[:, -1]).mean())
+
+
+@dataclass
+class GraphBatch:
+    """Device row-level graph batch of S samples (G graphs each)."""
+
+    S: int
+    G: int
+    Nv: int
+    Nc: int
+    nnz: int
+    vfeat: torch.Tensor  # (Nv, 4) [x, deg+/C, deg-/C, 0]
+    cfeat: torch.Tensor  # (Nc, 3) [is_sat, ntrue/3, 1]
+    slots: torch.Tensor  # (Nc, 3)
+    ptr: torch.Tensor  # (Nv + 1,)
+    inc: torch.Tensor  # (nnz,)
+    vbase: torch.Tensor  # (S*G,)
+    nv: torch.Tensor
+    cbase: torch.Tensor
+    nc: torch.Tensor
+
+
+def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor, inst: torch.Tensor,
+             x: torch.Tensor, critic_only: bool = False) -> GraphBatch:
+    """Instantiate the templates for samples (inst (S,), x (S,V) uint8) on the device."""
+    S = int(inst.shape[0])
+    G = 1 if critic_only else tpl.G
+    il = inst.long()
+    nvs = (tpl.crit_v if critic_only else tpl.full_v)[il]
+    ncs = (tpl.crit_c if critic_only else tpl.full_c)[il]
+    nes = (tpl.crit_e if critic_only else tpl.full_e)[il]
+    cat0 = lambda t: torch.cat([torch.zeros(1, dtype=torch.int64, device=t.device), torch.cumsum(t.long(), 0)])
+    vb, cb, eb = cat0(nvs), cat0(ncs), cat0(nes)
+    Nv, Nc, nnz = (int(t) for t in torch.stack([vb[-1], cb[-1], eb[-1]]).tolist())
+    dev = inst.device
+    out = GraphBatch(S, G, Nv, Nc, nnz,
+                     torch.empty((Nv, 4), dtype=torch.float32, device=dev),
+                     torch.empty((Nc, 3), dtype=torch.float32, device=dev),
+                     torch.empty((Nc, 3), dtype=torch.int32, device=dev),
+                     torch.empty((Nv + 1,), dtype=torch.int32, device=dev),
+                     torch.empty((max(nnz, 1),), dtype=torch.int32, device=dev),
+                     torch.empty((S * G,), dtype=torch.int32, device=dev),
+                     torch.empty((S * G,), dtype=torch.int32, device=dev),
+                     torch.empty((S * G,), dtype=torch.int32, device=dev),
+                     torch.empty((S * G,), dtype=torch.int32, device=dev))
+    V = x.shape[1]
+    C = pool_packed.shape[1]
+    sb = torch.stack([vb[:-1], cb[:-1], eb[:-1]], 1).to(torch.int32).contiguous()  # (S, 3)
+    _lib.check(_lib.lib.msat_assemble_graph_batch(
+        S, G, tpl.A, V, C, inst.data_ptr(), x.data_ptr(), svf.data_ptr(), pool_packed.data_ptr(), sb.data_ptr(),
+        tpl.vgid.data_ptr(), tpl.cgid.data_ptr(), tpl.slots.data_ptr(), tpl.ptr.data_ptr(), tpl.inc.data_ptr(),
+        tpl.voff.data_ptr(), tpl.coff.data_ptr(), tpl.eoff.data_ptr(), tpl.poff.data_ptr(), tpl.gv.data_ptr(),
+        tpl.gc.data_ptr(), out.vfeat.data_ptr(), out.cfeat.data_ptr(), out.slots.data_ptr(), out.ptr.data_ptr(),
+        out.inc.data_ptr(), out.vbase.data_ptr(), out.nv.data_ptr(), out.cbase.data_ptr(), out.nc.data_ptr(),
+        Nv, nnz, _lib.stream_ptr(dev)), "msat_assemble_graph_batch")
+    return out

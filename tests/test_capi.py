@@ -11,7 +11,9 @@ from conftest import ROOT
 
 
 def _header_symbols():
-    text = open(os.path.join(ROOT, "include", "marlsat.h")).read()
+    import glob
+
+    text = "".join(open(f).read() for f in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
     return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(msat_[a-z_0-9]+)\s*\(", text, re.M)))
 
 

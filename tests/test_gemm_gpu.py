@@ -1,0 +1,71 @@
+"""GPU: fp32 MFMA GEMMs vs a float64 torch reference (error bound ~1e-6 * sum|a*b|)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_close(out, ref, absprod, rtol=2e-6):
+    err = (out.double() - ref).abs()
+    bound = rtol * absprod + 1e-30
+    assert bool((err <= bound).all()), float((err / bound).max())
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (7, 5, 3), (128, 128, 16), (300, 128, 132), (1000, 384, 256),
+                                   (257, 512, 384), (4096, 64, 656), (33, 130, 19)])
+@pytest.mark.parametrize("transB", [0, 1])
+def test_gemm(M, N, K, transB):
+    from marlsat import _lib
+
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    B = torch.randn((N, K) if transB else (K, N), device="cuda", generator=g)
+    bias = torch.randn(N, device="cuda", generator=g)
+    C = torch.randn(M, N, device="cuda", generator=g)
+    C0 = C.clone()
+    Bop = B.double().t() if transB else B.double()
+    for acc in (0, 1):
+        C.copy_(C0)
+        _lib.check(_lib.lib.msat_gemm(A.data_ptr(), K, B.data_ptr(), B.shape[1], transB, C.data_ptr(), N,
+                                      bias.data_ptr(), M, N, K, acc, _lib.stream_ptr()), "gemm")
+        ref = A.double() @ Bop + bias.double() + (C0.double() if acc else 0)
+        absprod = A.double().abs() @ Bop.abs() + bias.double().abs() + (C0.double().abs() if acc else 0)
+        _ref_close(C, ref, absprod)
+
+
+def test_gemm_strided_column_slices():
+    """Write into / read from column slices of wider buffers (the [m_pos | m_neg] concat pattern)."""
+    from marlsat import _lib
+
+    M, K, N = 500, 128, 128
+    X = torch.randn(M, 2 * K + 4, device="cuda")
+    W = torch.randn(K, N, device="cuda")
+    Y = torch.zeros(M, 3 * N, device="cuda")
+    _lib.check(_lib.lib.msat_gemm(X[:, K:].data_ptr(), 2 * K + 4, W.data_ptr(), N, 0, Y[:, N:].data_ptr(), 3 * N,
+                                  None, M, N, K, 0, _lib.stream_ptr()), "gemm")
+    ref = X[:, K:2 * K].double() @ W.double()
+    _ref_close(Y[:, N:2 * N], ref, X[:, K:2 * K].double().abs() @ W.double().abs())
+    assert float(Y[:, :N].abs().max()) == 0 and float(Y[:, 2 * N:].abs().max()) == 0
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 1, 1), (100, 3, 128), (5000, 256, 384), (70000, 128, 128), (999, 133, 65)])
+def test_gemm_wgrad(M, K, N):
+    from marlsat import _lib
+
+    A = torch.randn(M, K, device="cuda")
+    G = torch.randn(M, N, device="cuda")
+    W = torch.randn(K, N, device="cuda")
+    W0 = W.clone()
+    ws = torch.empty(int(_lib.lib.msat_gemm_wgrad_workspace_bytes(M, K, N)) // 4 + 1, device="cuda")
+    for acc in (0, 1):
+        W.copy_(W0)
+        _lib.check(_lib.lib.msat_gemm_wgrad(A.data_ptr(), K, G.data_ptr(), N, W.data_ptr(), N, M, K, N, acc,
+                                            ws.data_ptr(), _lib.stream_ptr()), "wgrad")
+        ref = A.double().t() @ G.double() + (W0.double() if acc else 0)
+        absprod = A.double().abs().t() @ G.double().abs() + (W0.double().abs() if acc else 0)
+        _ref_close(W, ref, absprod, rtol=4e-6)
+        W1 = W.clone()
+        _lib.check(_lib.lib.msat_gemm_wgrad(A.data_ptr(), K, G.data_ptr(), N, W.data_ptr(), N, M, K, N, 0,
+                                            ws.data_ptr(), _lib.stream_ptr()), "wgrad")
+        if not acc:
+            assert torch.equal(W, W1)  # bitwise reproducible

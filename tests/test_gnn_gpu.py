@@ -1,0 +1,186 @@
+"""GPU parity of the device GNN actor-critic (forward, backward, PPO loss) vs the
+torch-CPU oracle of the reference network (oracle/net.py), float64 on the same
+fp32 parameters.  Tolerances: forward outputs 1e-5 relative (+1e-6 abs); gradients
+1e-4 relative to the gradient tensor's max magnitude (fp32 accumulation over
+L GRU steps and thousands of rows)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import net as onet
+from oracle.sat_env import OracleSATEnv
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # V, C, vpa, H, L, S, action_mode
+    (12, 40, 4, 64, 2, 5, 0),
+    (20, 91, 10, 64, 3, 4, 0),
+    (23, 97, 10, 64, 2, 3, 0),  # padded agent slots
+    (16, 60, 4, 64, 2, 4, 1),
+    (20, 91, 10, 128, 2, 3, 0),
+]
+
+
+def _setup(V, C, vpa, H, L, S, mode, seed=0):
+    from marlsat.learners.gnn import GNNActorCritic
+    from marlsat.learners.graphs import DeviceTemplates, assemble, build_templates
+    from marlsat import SATEnv
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+
+    N = 4
+    pool = generate_problem_pool(V, C, N, size_id=7)
+    env = SATEnv(V, C, max_steps=10, vars_per_agent=vpa)
+    A, M = env.num_agents, env.max_vars_per_agent
+    dpool = env.make_pool(pool)
+    net = GNNActorCritic(H, L, A, M, mode, V, device="cuda", seed=seed)
+    tree64 = onet.init_params(onet.param_shapes(H, L, A, M, mode), seed=seed + 1)
+    tree32 = {k: v.float().numpy() for k, v in tree64.items()}
+    net.load_flax(tree32)
+    tpl = DeviceTemplates(build_templates(pool, V, A), A, "cuda")
+    rng = np.random.default_rng(seed)
+    inst = rng.integers(0, N, S).astype(np.int32)
+    x = rng.integers(0, 2, (S, V)).astype(np.uint8)
+    b = assemble(tpl, dpool.packed, dpool.static_var_features(), torch.from_numpy(inst).cuda(),
+                 torch.from_numpy(x).cuda())
+    # oracle inputs
+    ora = OracleSATEnv(V, C, 10, vars_per_agent=vpa)
+    _, ost = ora.reset(pool[inst], x.astype(np.int32))
+    Ap, An = onet.dense_graph(pool[inst], V)
+    batch = {"svf": torch.from_numpy(ora.static_var_features(pool[inst])).double(),
+             "x": torch.from_numpy(x).double(), "cf": torch.from_numpy(ora.clause_features(ost)).double(),
+             "A_pos": Ap, "A_neg": An}
+    P = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in tree32.items()}
+    av = torch.from_numpy(ora.agent_vars.astype(np.int64))
+    am = torch.from_numpy(ora.action_mask)
+    return net, b, P, batch, av, am, A, M
+
+
+def _close(dev, ref, rtol, atol, what):
+    dev = np.asarray(dev, np.float64)
+    ref = np.asarray(ref, np.float64)
+    fin = np.isfinite(ref)
+    assert np.array_equal(fin, np.isfinite(dev)), what + " (inf pattern)"
+    err = np.abs(dev[fin] - ref[fin])
+    bound = rtol * np.abs(ref[fin]) + atol
+    assert (err <= bound).all(), f"{what}: max err {err.max():.3g}, worst ratio {(err / bound).max():.3g}"
+
+
+@pytest.mark.parametrize("V,C,vpa,H,L,S,mode", CASES)
+def test_forward_backward_match_oracle(V, C, vpa, H, L, S, mode):
+    net, b, P, batch, av, am, A, M = _setup(V, C, vpa, H, L, S, mode)
+    logits, value, state = net.forward(b, save=True)
+    ref_logits = onet.actor_logits(P, L, batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"], av,
+                                   am, mode)
+    ref_value = onet.critic(P, L, batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"])
+    _close(logits.cpu().numpy(), ref_logits.detach().numpy(), 1e-5, 1e-6, "logits")
+    _close(value.cpu().numpy(), ref_value.detach().numpy(), 1e-5, 1e-6, "value")
+    # random cotangents
+    g = torch.Generator().manual_seed(3)
+    wl = torch.randn(ref_logits.shape, generator=g, dtype=torch.float64)
+    wl = torch.where(torch.isfinite(ref_logits), wl, torch.zeros_like(wl))
+    wv = torch.randn(ref_value.shape, generator=g, dtype=torch.float64)
+    obj = (torch.where(torch.isfinite(ref_logits), ref_logits, torch.zeros_like(ref_logits)) * wl).sum() + \
+        (ref_value * wv).sum()
+    obj.backward()
+    net.grads.zero_()
+    net.backward(b, state, wl.float().cuda().contiguous(), wv.float().cuda().contiguous())
+    got = net.to_flax(grads=True)
+    for name, p in P.items():
+        ref = p.grad.numpy() if p.grad is not None else np.zeros(p.shape)
+        scale = max(np.abs(ref).max(), 1e-12)
+        _close(got[name], ref, 0.0, 1e-4 * scale, f"grad {name}")
+
+
+def test_critic_only_batch_matches_full():
+    from marlsat.learners.graphs import DeviceTemplates, assemble, build_templates
+
+    net, b, P, batch, av, am, A, M = _setup(20, 91, 10, 64, 2, 4, 0)
+    _, v_full, _ = net.forward(b)
+    # rebuild the same samples as a critic-only batch
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+    from marlsat import SATEnv
+
+    pool = generate_problem_pool(20, 91, 4, size_id=7)
+    env = SATEnv(20, 91, 10, vars_per_agent=10)
+    dpool = env.make_pool(pool)
+    tpl = DeviceTemplates(build_templates(pool, 20, env.num_agents), env.num_agents, "cuda")
+    rng = np.random.default_rng(0)
+    inst = rng.integers(0, 4, 4).astype(np.int32)
+    x = rng.integers(0, 2, (4, 20)).astype(np.uint8)
+    bc = assemble(tpl, dpool.packed, dpool.static_var_features(), torch.from_numpy(inst).cuda(),
+                  torch.from_numpy(x).cuda(), critic_only=True)
+    _, v_crit, _ = net.forward(bc, actor=False)
+    assert torch.equal(v_full, v_crit)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_ppo_loss_and_grads_match_oracle(mode):
+    from marlsat import _lib
+
+    V, C, vpa, H, L, S = (20, 91, 10, 64, 2, 6) if mode == 0 else (16, 60, 4, 64, 2, 6)
+    net, b, P, batch, av, am, A, M = _setup(V, C, vpa, H, L, S, mode, seed=5)
+    cfg = {"CLIP_EPS": 0.12, "VF_CLIP": 0.5, "ENT_COEF": 0.005, "VF_COEF": 0.5}
+    rng = np.random.default_rng(9)
+    with torch.no_grad():
+        lg = onet.actor_logits(P, L, batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"], av, am, mode)
+        vv = onet.critic(P, L, batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"])
+        probs = torch.softmax(lg, -1)
+        act = torch.distributions.Categorical(probs=probs).sample(generator=None) if False else \
+            torch.multinomial(probs.reshape(-1, probs.shape[-1]), 1, generator=torch.Generator().manual_seed(1)) \
+            .reshape(probs.shape[:-1])
+        lp = torch.log_softmax(lg, -1).gather(-1, act[..., None])[..., 0]
+    old_lp = lp + torch.from_numpy(rng.normal(0, 0.1, lp.shape))  # ratios both inside and outside the clip range
+    if mode == 1:
+        old_lp = torch.where(torch.isfinite(lp), old_lp, torch.zeros_like(old_lp))
+    bt = dict(batch, action=act, log_prob=old_lp, gae=torch.from_numpy(rng.normal(0, 1, S)),
+              value=vv + torch.from_numpy(rng.normal(0, 0.4, S)), targets=vv + torch.from_numpy(rng.normal(0, 1, S)))
+    total, (vl, la, ent), _, _ = onet.ppo_loss(P, L, bt, cfg, av, am, mode)
+    total.backward()
+    logits, value, state = net.forward(b, save=True)
+    dlog = torch.empty_like(logits)
+    dval = torch.empty_like(value)
+    R = S * A
+    rows = torch.empty(2 * R + S, device="cuda")
+    sums = torch.zeros(3, dtype=torch.float64, device="cuda")
+    cu = lambda t, dt=torch.float32: t.to(dt).contiguous().cuda()
+    # keep every device temporary referenced until the kernel has run (a tensor freed before the
+    # launch is enqueued can be handed to the next allocation and overwritten first)
+    d_act, d_olp, d_gae = cu(act, torch.int32), cu(old_lp), cu(bt["gae"])
+    d_vold, d_tgt = cu(bt["value"]), cu(bt["targets"])
+    assert int(d_act.min()) >= 0 and int(d_act.max()) < (M + 1 if mode == 0 else 2)
+    _lib.check(_lib.lib.msat_ppo_loss(
+        logits.data_ptr(), S, A, M, mode, net.base, net.rem, d_act.data_ptr(), d_olp.data_ptr(),
+        d_gae.data_ptr(), value.data_ptr(), d_vold.data_ptr(), d_tgt.data_ptr(),
+        cfg["CLIP_EPS"], cfg["VF_CLIP"], cfg["ENT_COEF"], cfg["VF_COEF"], S, dlog.data_ptr(), dval.data_ptr(),
+        rows.data_ptr(), sums.data_ptr(), _lib.stream_ptr()), "ppo_loss")
+    torch.cuda.synchronize()
+    s = sums.cpu().numpy()
+    n_act = S * A
+    n_ent = S * A if mode == 0 else S * A * M
+    np.testing.assert_allclose(s[0] / S, float(vl), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(s[1] / n_act, float(la), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(s[2] / n_ent, float(ent), rtol=1e-5, atol=1e-7)
+    net.grads.zero_()
+    net.backward(b, state, dlog, dval)
+    got = net.to_flax(grads=True)
+    for name, p in P.items():
+        ref = p.grad.numpy() if p.grad is not None else np.zeros(p.shape)
+        scale = max(np.abs(ref).max(), 1e-12)
+        _close(got[name], ref, 0.0, 2e-4 * scale, f"grad {name}")
+
+
+def test_adam_matches_optax_formula():
+    from marlsat.learners.gnn import GNNActorCritic
+    from oracle.net import adam_update
+
+    net = GNNActorCritic(64, 1, 2, 10, 0, 20, device="cuda")
+    p0 = net.params.clone()
+    g = torch.randn_like(net.params)
+    state = {"count": 0, "m": {"p": torch.zeros(net.size, dtype=torch.float64)},
+             "v": {"p": torch.zeros(net.size, dtype=torch.float64)}}
+    pr = {"p": p0.double().cpu()}
+    for step in range(3):
+        net.grads.copy_(g * (step + 1))
+        net.adam_step(1e-3 * (step + 1))
+        pr, state = adam_update(pr, {"p": (g * (step + 1)).double().cpu()}, state, 1e-3 * (step + 1))
+    np.testing.assert_allclose(net.params.cpu().numpy(), pr["p"].numpy(), rtol=1e-5, atol=1e-6)
