@@ -182,6 +182,12 @@ int msat_gae(int32_t T, int32_t B, const float *reward, int32_t reward_stride,
              float gamma, float gamma_lambda, int32_t normalize, float *advantages,
              float *targets, void *workspace, void *stream);
 
+/* Global-normalisation pieces for multi-GPU GAE (the reference normalises over ALL
+ * T*B advantages, learner:529-532): per-rank moments (fp64 sum, sum of squares;
+ * workspace >= 2*1024 doubles), all-reduced by the caller, then x = (x - mean)/std. */
+int msat_moments(const float *x, size_t n, double *out2, void *workspace, void *stream);
+int msat_standardize(float *x, size_t n, float mean, float stdv, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

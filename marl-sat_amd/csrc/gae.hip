@@ -82,9 +82,70 @@ gae_normalize_kernel(size_t n, int nparts, const double *__restrict__ partial, f
         adv[i] = __fdiv_rn(__fsub_rn(adv[i], mf), sf);
 }
 
+// out[0] += sum x, out[1] += sum x^2 (fp64, per-block partials combined by one block)
+__global__ void __launch_bounds__(kGaeThreads)
+moments_kernel(const float *__restrict__ x, size_t n, double *__restrict__ part) {
+    __shared__ double s1[kGaeThreads / 64], s2[kGaeThreads / 64];
+    double a = 0.0, b = 0.0;
+    for (size_t i = (size_t)blockIdx.x * kGaeThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kGaeThreads) {
+        const double v = x[i];
+        a += v;
+        b += v * v;
+    }
+    a = wave_sum_f64(a);
+    b = wave_sum_f64(b);
+    if ((threadIdx.x & 63) == 0) {
+        s1[threadIdx.x >> 6] = a;
+        s2[threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = s1[0] + s1[1] + s1[2] + s1[3];
+        part[2 * blockIdx.x + 1] = s2[0] + s2[1] + s2[2] + s2[3];
+    }
+}
+
+__global__ void moments_reduce_kernel(const double *__restrict__ part, int nb, double *__restrict__ out) {
+    if (threadIdx.x == 0) {
+        double a = 0.0, b = 0.0;
+        for (int k = 0; k < nb; ++k) {
+            a += part[2 * k];
+            b += part[2 * k + 1];
+        }
+        out[0] = a;
+        out[1] = b;
+    }
+}
+
+__global__ void standardize_kernel(float *__restrict__ x, size_t n, float mean, float stdv) {
+    for (size_t i = (size_t)blockIdx.x * kGaeThreads + threadIdx.x; i < n; i += (size_t)gridDim.x * kGaeThreads)
+        x[i] = __fdiv_rn(__fsub_rn(x[i], mean), stdv);
+}
+
 }  // namespace msat
 
 using namespace msat;
+
+static int stat_blocks(size_t n) { return (int)std::min<size_t>((n + kGaeThreads - 1) / kGaeThreads, 1024); }
+
+extern "C" int msat_moments(const float *x, size_t n, double *out2, void *workspace, void *stream) {
+    MSAT_REQUIRE(x && out2 && workspace, "NULL pointer");
+    const int nb = std::max(1, stat_blocks(n));
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(moments_kernel, dim3(nb), dim3(kGaeThreads), 0, s, x, n, (double *)workspace);
+    int rc = check_launch("moments_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(moments_reduce_kernel, dim3(1), dim3(64), 0, s, (const double *)workspace, nb, out2);
+    return check_launch("moments_reduce_kernel");
+}
+
+extern "C" int msat_standardize(float *x, size_t n, float mean, float stdv, void *stream) {
+    MSAT_REQUIRE(x, "NULL pointer");
+    if (!n) return MSAT_OK;
+    hipLaunchKernelGGL(standardize_kernel, dim3(stat_blocks(n)), dim3(kGaeThreads), 0, (hipStream_t)stream, x, n, mean,
+                       stdv);
+    return check_launch("standardize_kernel");
+}
 
 static int gae_blocks(int B) { return (B + kGaeThreads - 1) / kGaeThreads; }
 

@@ -121,6 +121,8 @@ def _load():
     sig["msat_sample_actions"] = (I, [P, I, I, I, U, U, P, P, P])
     sig["msat_ppo_loss"] = (I, [P, I, I, I, I, I, I, P, P, P, P, P, P, F, F, F, F, I, P, P, P, P, P])
     sig["msat_adam"] = (I, [P, P, P, P, Z, F, F, F, F, I, F, P])
+    sig["msat_moments"] = (I, [P, Z, P, P, P])
+    sig["msat_standardize"] = (I, [P, Z, F, F, P])
     sig["msat_debug_fill"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])  # marlsat_debug.h
     sig["msat_debug_fill_chunked"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])
     for name, (res, args) in sig.items():
@@ -134,6 +136,8 @@ lib = _load()
 
 # Every symbol include/marlsat*.h declares (checked by tests/test_capi.py).
 EXPORTED = (
+    "msat_moments",
+    "msat_standardize",
     "msat_assemble_graph_batch",
     "msat_clause_gather",
     "msat_var_gather",
