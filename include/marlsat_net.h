@@ -64,6 +64,10 @@ int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, int32_t ldi, 
                     float *dGh, int32_t lddh, float *dhprev, int32_t lddp, float *dln_scale,
                     float *dln_bias, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
                     void *stream);
+/* out[N] (+)= column sums of G (M x N) — bias gradients; workspace >= msat_colsum_workspace_floats. */
+size_t msat_colsum_workspace_floats(int32_t M, int32_t N);
+int msat_colsum(const float *G, int32_t ldg, int32_t M, int32_t N, float *out, int32_t accumulate,
+                float *workspace, void *stream);
 int msat_relu(float *x, size_t n, void *stream);
 int msat_relu_bwd(float *dy, const float *y, size_t n, void *stream);
 

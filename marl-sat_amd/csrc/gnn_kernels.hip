@@ -195,14 +195,32 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
     }
 }
 
-// dst[j] (+)= sum_b part[b][j]  (fixed order)
-__global__ void partial_reduce_kernel(const float *__restrict__ part, int nblocks, int width, float *__restrict__ dst,
-                                      int accumulate) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= width) return;
+// dst[j] (+)= sum_b part[b][j]: block per 64 columns, 4 waves stride the partial rows, fixed-order
+// combine (bitwise reproducible).
+__global__ void __launch_bounds__(256)
+partial_reduce_kernel(const float *__restrict__ part, int nblocks, int width, float *__restrict__ dst, int accumulate) {
+    __shared__ float red[4][64];
+    const int j = blockIdx.x * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
     float s = 0.f;
-    for (int b = 0; b < nblocks; ++b) s += part[(size_t)b * width + j];
-    dst[j] = accumulate ? dst[j] + s : s;
+    if (j < width)
+        for (int b = w; b < nblocks; b += 4) s += part[(size_t)b * width + j];
+    red[w][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (w == 0 && j < width) {
+        const float t = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+        dst[j] = accumulate ? dst[j] + t : t;
+    }
+}
+
+// Column sums of G (M x N): block (column chunk of 256, row split) partials, then partial_reduce.
+__global__ void __launch_bounds__(256)
+colsum_partial_kernel(const float *__restrict__ G, int ldg, int M, int N, int rows_per, float *__restrict__ part) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= N) return;
+    const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+    float s = 0.f;
+    for (int r = r0; r < r1; ++r) s += G[(size_t)r * ldg + j];
+    part[(size_t)blockIdx.y * N + j] = s;
 }
 
 // ------------------------------------------------------------ elementwise --
@@ -288,6 +306,27 @@ using namespace msat;
 
 static int grid_rows(long rows) { return (int)std::min<long>((rows + 3) / 4, 8192); }
 
+static int colsum_splits(int M, int N) {
+    const int colblocks = (N + 255) / 256;
+    return std::max(1, std::min((M + 255) / 256, 1024 / colblocks));
+}
+
+extern "C" size_t msat_colsum_workspace_floats(int32_t M, int32_t N) { return (size_t)colsum_splits(M, N) * N; }
+
+extern "C" int msat_colsum(const float *G, int32_t ldg, int32_t M, int32_t N, float *out, int32_t accumulate,
+                           float *workspace, void *stream) {
+    MSAT_REQUIRE(G && out && workspace && N >= 1 && M >= 0 && ldg >= N, "bad colsum args");
+    hipStream_t s = (hipStream_t)stream;
+    const int sp = colsum_splits(M, N);
+    const int rows_per = (M + sp - 1) / sp;
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 255) / 256, sp), dim3(256), 0, s, G, ldg, M, N, rows_per,
+                       workspace);
+    int rc = check_launch("colsum_partial_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, s, workspace, sp, N, out, accumulate);
+    return check_launch("partial_reduce_kernel");
+}
+
 extern "C" int msat_clause_gather(const float *src, int32_t ld_src, const int32_t *slots, float *dst, int32_t ld_dst,
                                   int32_t num_clause_rows, int32_t H, int32_t accumulate, void *stream) {
     MSAT_REQUIRE(src && slots && dst && H % 32 == 0 && ld_src % 4 == 0 && ld_dst % 4 == 0, "bad clause_gather args");
@@ -340,7 +379,7 @@ extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, in
     else hipLaunchKernelGGL(gru_ln_bwd_kernel<4>, g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3((2 * H + 255) / 256), dim3(256), 0, s, partial, nb, 2 * H, dln_scale,
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, s, partial, nb, 2 * H, dln_scale,
                        accumulate_ln);
     return check_launch("partial_reduce_kernel");
 }

@@ -107,6 +107,8 @@ def _load():
     sig["msat_gru_ln_fwd"] = (I, [P, I, P, I, P, I, P, P, P, I, I, I, P])
     sig["msat_gru_ln_bwd_partial_floats"] = (Z, [I, I])
     sig["msat_gru_ln_bwd"] = (I, [P, I, P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, I, I, I, P])
+    sig["msat_colsum_workspace_floats"] = (Z, [I, I])
+    sig["msat_colsum"] = (I, [P, I, I, I, P, I, P, P])
     sig["msat_relu"] = (I, [P, Z, P])
     sig["msat_relu_bwd"] = (I, [P, P, Z, P])
     sig["msat_critic_pool"] = (I, [P, P, P, I, P, P, P, P, I, I, P, P])
@@ -144,6 +146,8 @@ EXPORTED = (
     "msat_gru_ln_fwd",
     "msat_gru_ln_bwd_partial_floats",
     "msat_gru_ln_bwd",
+    "msat_colsum_workspace_floats",
+    "msat_colsum",
     "msat_relu",
     "msat_relu_bwd",
     "msat_critic_pool",

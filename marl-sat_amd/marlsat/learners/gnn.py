@@ -125,17 +125,24 @@ class GNNActorCritic:
     def stream(self):
         return _lib.stream_ptr(self.device)
 
+    flops = 0  # matmul FLOPs issued (2*M*N*K per GEMM), for the MFMA roofline
+
     def _gemm(self, A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc=0):
+        GNNActorCritic.flops += 2 * M * N * K
         _chk(L_.msat_gemm(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, self.stream), "msat_gemm")
 
     def _wgrad(self, A, lda, G, ldg, W, ldw, M, K, N, acc=1):
         if M == 0:
             return
+        GNNActorCritic.flops += 2 * M * N * K
         ws = self.scr.get_ws(int(L_.msat_gemm_wgrad_workspace_bytes(M, K, N)))
         _chk(L_.msat_gemm_wgrad(A, lda, G, ldg, W, ldw, M, K, N, acc, ws.data_ptr(), self.stream), "msat_gemm_wgrad")
 
     def _colsum(self, G, ldg, M, N, out, acc=1):
-        self._wgrad(self.scr.get_ones(M).data_ptr(), 1, G, ldg, out, N, M, 1, N, acc)
+        if M == 0:
+            return
+        ws = self.scr.get_part(int(L_.msat_colsum_workspace_floats(M, N)))
+        _chk(L_.msat_colsum(G, ldg, M, N, out, acc, ws.data_ptr(), self.stream), "msat_colsum")
 
     @staticmethod
     def _ptr(t: torch.Tensor, col: int = 0) -> int:
