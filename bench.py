@@ -11,6 +11,13 @@ Multi-GPU (torchrun, one process per GPU): independent env shards, no
 collective on the data path; barrier + synchronize around the timed region,
 max elapsed over ranks; value = all ranks' env-steps / that time (weak scaling).
 
+MAPPO leg (the metric's "MAPPO updates/sec"): one full train cycle of the device
+learner -- rollout of T steps (actor + critic forward, sampling, fused env step with
+auto-reset), GAE + global advantage normalisation, UPDATE_EPOCHS x T*B/MINIBATCH_SIZE
+PPO minibatches (forward, loss, backward, gradient all-reduce over RCCL when N>1,
+Adam) and the cycle metrics -- timed after one warm-up cycle, reported under
+"mappo" with per-phase times and the fp32-MFMA roofline of the GEMMs issued.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -35,6 +42,7 @@ WORKLOADS = {  # name: V, C, vars_per_agent, envs per GPU, size_id (seed = 1000*
     "uf200-860": (200, 860, 8, 4096, 3),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
 
 
 def step_bytes(V: int, C: int, A: int) -> int:
@@ -108,6 +116,79 @@ def load_pmc_traffic(workload: str):
     return None, None
 
 
+# ------------------------------------------------------------------ MAPPO ----
+def mappo_bench(args, rank, world, dist):
+    """One timed MAPPO train cycle (after one warm-up cycle) on the stated config."""
+    import torch
+
+    from marlsat import SATEnv
+    from marlsat.learners.gnn import GNNActorCritic
+    from marlsat.learners.mappo_gnn_sat_learner import MAPPOLearner
+    from marlsat.random import PRNGKey
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+
+    V, C, vpa, _, size_id = WORKLOADS[args.mappo_workload]
+    B, T, E = args.mappo_envs, args.mappo_T, 4
+    H, L = 128, 16
+    cfg = dict(NUM_ENVS=B, NUM_STEPS=T, UPDATE_EPOCHS=E, MINIBATCH_SIZE=B * T // 4, NUM_UPDATES=1000,
+               LEARNING_RATE=3e-4, ANNEAL_LR=True, LR_START_FACTOR=1.0, LR_END_FLOOR=1e-5, GAMMA=0.99,
+               GAE_LAMBDA=0.95, CLIP_EPS=0.2, ENT_COEF=0.01, VF_COEF=0.5, VF_CLIP=0.2,
+               GNN_HIDDEN_DIM=H, GNN_NUM_MESSAGE_PASSING_STEPS=L, action_mode=0)
+    env = SATEnv(V, C, max_steps=512, vars_per_agent=vpa)
+    pool = env.make_pool(generate_problem_pool(V, C, args.pool, size_id=size_id))
+    net = GNNActorCritic(H, L, env.num_agents, env.max_vars_per_agent, 0, V, device=env.device, seed=0)
+    learner = MAPPOLearner(cfg, env, net, pool, dist=dist if world > 1 else None)
+    rs = learner.init_runner_state(PRNGKey(77 + rank))
+    gen = torch.Generator().manual_seed(99 + rank)
+    rs, _ = learner.train_cycle(rs, 0, gen)  # warm-up: kernels loaded, caches and pools grown
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    GNNActorCritic.flops = 0
+    t0 = time.perf_counter()
+    ev[0].record()
+    rs = learner.rollout(rs)
+    ev[1].record()
+    learner.compute_advantages(rs)
+    ev[2].record()
+    losses, ent = learner.ppo_update(1, gen)
+    ev[3].record()
+    met = learner.metrics(losses, ent)
+    ev[4].record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    phases = [ev[i].elapsed_time(ev[i + 1]) for i in range(4)]
+    flops = float(GNNActorCritic.flops)
+    if dist is not None:
+        t = torch.tensor([elapsed] + phases, dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, phases = float(t[0]), [float(v) for v in t[1:]]
+    n_mb = B * T // cfg["MINIBATCH_SIZE"]
+    gemm_tflops = flops / (elapsed * 1e12)
+    return {
+        "metric": "MAPPO updates/sec",
+        "value": 1.0 / elapsed,
+        "unit": "updates/s",
+        "s_per_update": elapsed,
+        "adam_steps_per_s": E * n_mb / elapsed,
+        "samples_per_s": world * B * T / elapsed,
+        "phase_ms": dict(zip(("rollout", "gae", "ppo_update", "metrics"), phases)),
+        "config": {"workload": args.mappo_workload, "num_vars": V, "num_clauses": C, "num_agents": env.num_agents,
+                   "envs_per_gpu": B, "NUM_STEPS": T, "UPDATE_EPOCHS": E, "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"],
+                   "GNN_HIDDEN_DIM": H, "GNN_NUM_MESSAGE_PASSING_STEPS": L, "micro_batch": learner.micro,
+                   "parallelism": f"dp{world} (env shards; RCCL gradient all-reduce per minibatch)"},
+        "roofline": {"bound": "mfma", "achieved": gemm_tflops, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": gemm_tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                     "note": "2*M*N*K of every fp32 GEMM issued in the cycle / cycle wall time (rank max)"},
+        "dtype": "f32",
+        "solve_rate": met["solve_rate"],
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -118,6 +199,9 @@ def main():
     ap.add_argument("--pool", type=int, default=1024, help="problem instances in the pool")
     ap.add_argument("--obs-dtype", default="int32", choices=["int32", "int8"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline per core (0: skip)")
+    ap.add_argument("--mappo-workload", default="uf50-218", choices=sorted(WORKLOADS))
+    ap.add_argument("--mappo-envs", type=int, default=1024, help="envs per GPU in the MAPPO leg")
+    ap.add_argument("--mappo-T", type=int, default=8, help="NUM_STEPS of the MAPPO leg (0: skip the leg)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,6 +272,9 @@ def main():
     assert torch.equal(C - state.clauses_satisfied_status.int().sum(1), state.num_unsatisfied)
     done_frac = float(out["done"].float().mean())
 
+    del obs, state, out, actions, step, pool
+    mappo = mappo_bench(args, rank, world, dist) if args.mappo_T > 0 else None
+
     if rank == 0:
         per_env = step_bytes(V, C, A)
         if obs_dtype == torch.int8:
@@ -230,6 +317,7 @@ def main():
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
+            "mappo": mappo,
             "done_fraction_last_step": done_frac,
         }
         print(json.dumps(rec), flush=True)

@@ -31,6 +31,7 @@ import torch
 from .. import _lib
 from ..envs.multi_agent_sat_env import ObsDict, ProblemPool, SATEnv, SATState
 from ..random import Key, as_key, split
+from .collectives import allreduce_grads, allreduce_sums, global_moments, world_size
 from .gnn import GNNActorCritic
 from .graphs import DeviceTemplates, GraphBatch, assemble, build_templates
 from .ops import gae as device_gae
@@ -139,7 +140,7 @@ class MAPPOLearner:
         self.cfg = dict(config)
         self.env, self.net, self.pool = env, network, pool
         self.dist = dist
-        self.world = dist.get_world_size() if dist is not None else 1
+        self.world = world_size(dist)
         self.device = env.device
         self.B = int(config["NUM_ENVS"])
         self.T = int(config["NUM_STEPS"])
@@ -219,10 +220,6 @@ class MAPPOLearner:
             out[b0:b1] = v
         return out
 
-    def _allreduce(self, t: torch.Tensor):
-        if self.dist is not None and self.world > 1:
-            self.dist.all_reduce(t)
-
     # ------------------------------------------------------------- rollout ----
     def rollout(self, rs: RunnerState) -> RunnerState:
         tr, env = self.tr, self.env
@@ -250,11 +247,7 @@ class MAPPOLearner:
         n = self.adv.numel()
         _lib.check(L_.msat_moments(self.adv.data_ptr(), n, self.moments.data_ptr(), self.mom_ws.data_ptr(),
                                    _lib.stream_ptr(self.device)), "msat_moments")
-        mom = torch.cat([self.moments, torch.tensor([float(n)], dtype=torch.float64, device=self.device)])
-        self._allreduce(mom)
-        s1, s2, cnt = mom.tolist()
-        mean = s1 / cnt
-        std = math.sqrt(max(s2 / cnt - mean * mean, 0.0)) + 1e-8
+        mean, std = global_moments(self.moments, n, self.dist)
         _lib.check(L_.msat_standardize(self.adv.data_ptr(), n, mean, std, _lib.stream_ptr(self.device)),
                    "msat_standardize")
 
@@ -294,9 +287,9 @@ class MAPPOLearner:
                         rows.data_ptr(), sums.data_ptr(), _lib.stream_ptr(dev)), "msat_ppo_loss")
                     net.backward(gb, state, dlog, dval)
                     del state
-                self._allreduce(net.grads)
+                scale = allreduce_grads(net.grads, self.dist)
                 lr = learning_rate_at(net.adam_count, c)
-                net.adam_step(lr, grad_scale=1.0 / self.world)
+                net.adam_step(lr, grad_scale=scale)
         # per-minibatch means: (value_loss, loss_actor, entropy)
         losses[..., 0] /= MB
         losses[..., 1] /= MB * A
@@ -319,8 +312,8 @@ class MAPPOLearner:
         d = tg - vpred
         ev = torch.stack([tg.sum(), (tg * tg).sum(), d.sum(), (d * d).sum(),
                           torch.tensor(float(N), device=dev, dtype=torch.float64)])
-        self._allreduce(sums)
-        self._allreduce(ev)
+        allreduce_sums(sums, self.dist)
+        allreduce_sums(ev, self.dist)
         s = sums.tolist()
         t1, t2, d1, d2, n = ev.tolist()
         var_t = t2 / n - (t1 / n) ** 2
