@@ -64,6 +64,22 @@ int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, int32_t ldi, 
                     float *dGh, int32_t lddh, float *dhprev, int32_t lddp, float *dln_scale,
                     float *dln_bias, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
                     void *stream);
+/* One kernel per GRU call on the fp32 matrix cores (gru_fused.hip): x = [x0 | x1 | x2]
+ * (segment widths multiples of 4, 16-byte aligned rows; w1/w2 may be 0), Wi (Kx, 3H),
+ * Wh (H, 3H), bi/bh (3H), out = LN(GRU(hprev, x)).  g4 (nullable, ldg >= 4H) receives the
+ * pre-activations [r_pre | z_pre | gin | ghn] for msat_gru_ln_bwd_g4.
+ * Replaces the two gate GEMMs + msat_gru_ln_fwd of update_c / update_v_pos / update_v_neg
+ * + LayerNorm_k (learner:68-80). */
+int msat_gru_ln_fused_fwd(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
+                          const float *x2, int32_t ld2, int32_t w2, const float *hprev, int32_t ldp,
+                          const float *wi, const float *bi, const float *wh, const float *bh,
+                          const float *ln_scale, const float *ln_bias, float *out, int32_t ldo, float *g4,
+                          int32_t ldg, int32_t R, int32_t H, void *stream);
+/* msat_gru_ln_bwd from the fused forward's g4 tape (same outputs; partial as msat_gru_ln_bwd). */
+int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
+                       int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
+                       float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *partial,
+                       int32_t R, int32_t H, int32_t accumulate_ln, void *stream);
 /* out[N] (+)= column sums of G (M x N) — bias gradients; workspace >= msat_colsum_workspace_floats. */
 size_t msat_colsum_workspace_floats(int32_t M, int32_t N);
 int msat_colsum(const float *G, int32_t ldg, int32_t M, int32_t N, float *out, int32_t accumulate,

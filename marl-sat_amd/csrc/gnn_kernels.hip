@@ -113,7 +113,9 @@ gru_ln_fwd_kernel(const float *__restrict__ Gi, int ldi, const float *__restrict
 // dy -> dGi, dGh (3H each), dh (+=), and per-block partial sums of dscale / dbias
 // (part[block][0:H] = sum dy*xhat, part[block][H:2H] = sum dy), reduced later in a
 // fixed order.
-template <int PER>
+// G4 = true: Gi is the fused forward's pre-activation tape [r_pre | z_pre | gin | ghn]
+// (gru_fused.hip) and Gh is unused.
+template <int PER, bool G4>
 __global__ void __launch_bounds__(kRowThreads)
 gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
@@ -125,16 +127,22 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
 #pragma unroll
     for (int u = 0; u < PER; ++u) ps[u] = pb[u] = 0.f;
     for (int r = blockIdx.x * 4 + w; r < R; r += gridDim.x * 4) {
-        const float *gi = Gi + (size_t)r * ldi, *gh = Gh + (size_t)r * ldh, *h = hp + (size_t)r * ldp;
+        const float *gi = Gi + (size_t)r * ldi, *gh = G4 ? gi : Gh + (size_t)r * ldh, *h = hp + (size_t)r * ldp;
         const float *g = dy + (size_t)r * ldy;
         float rg[PER], zg[PER], ng[PER], hn[PER], hv[PER], ghn[PER], dyv[PER];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int j = lane + 64 * u;
-            rg[u] = sigmoidf_(gi[j] + gh[j]);
-            zg[u] = sigmoidf_(gi[H + j] + gh[H + j]);
-            ghn[u] = gh[2 * H + j];
+            if (G4) {
+                rg[u] = sigmoidf_(gi[j]);
+                zg[u] = sigmoidf_(gi[H + j]);
+                ghn[u] = gi[3 * H + j];
+            } else {
+                rg[u] = sigmoidf_(gi[j] + gh[j]);
+                zg[u] = sigmoidf_(gi[H + j] + gh[H + j]);
+                ghn[u] = gh[2 * H + j];
+            }
             ng[u] = tanhf(gi[2 * H + j] + rg[u] * ghn[u]);
             hv[u] = h[j];
             hn[u] = (1.0f - zg[u]) * ng[u] + zg[u] * hv[u];
@@ -374,9 +382,32 @@ extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, in
     hipStream_t s = (hipStream_t)stream;
     const int nb = grid_rows(R);
     const dim3 g(nb), b(kRowThreads);
-    if (H == 64) hipLaunchKernelGGL(gru_ln_bwd_kernel<1>, g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
-    else if (H == 128) hipLaunchKernelGGL(gru_ln_bwd_kernel<2>, g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
-    else hipLaunchKernelGGL(gru_ln_bwd_kernel<4>, g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    int rc = check_launch("gru_ln_bwd_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, s, partial, nb, 2 * H, dln_scale,
+                       accumulate_ln);
+    return check_launch("partial_reduce_kernel");
+}
+
+extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
+                                  int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
+                                  float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *partial,
+                                  int32_t R, int32_t H, int32_t accumulate_ln, void *stream) {
+    MSAT_REQUIRE(dy && g4 && hprev && ln_scale && dGi && dGh && dhprev && dln_scale && dln_bias && partial,
+                 "NULL pointer");
+    MSAT_REQUIRE(H == 64 || H == 128 || H == 256, "gru_ln: H must be 64, 128 or 256 (got %d)", H);
+    MSAT_REQUIRE(ldg >= 4 * H, "gru_ln_bwd_g4: ldg must be >= 4H");
+    MSAT_REQUIRE(dln_bias == dln_scale + H, "dln_bias must follow dln_scale (contiguous [scale|bias] grads)");
+    if (R == 0) return MSAT_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = grid_rows(R);
+    const dim3 g(nb), b(kRowThreads);
+    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, true>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, true>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, true>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(partial_reduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, s, partial, nb, 2 * H, dln_scale,

@@ -1,0 +1,304 @@
+// Fused GRU cell + LayerNorm forward on the gfx950 matrix cores.
+//
+// One kernel per encoder GRU call (learner:68-80: update_c / update_v_pos / update_v_neg
+// followed by a fresh nn.LayerNorm) computes, for a 64-row tile,
+//     [r_pre | z_pre | gin | ghn] = [h | x] @ [[Wh_r Wh_z 0 Wh_n], [Wi_r Wi_z Wi_n 0]] + biases
+// on fp32 MFMA 32x32x2 (exact f32), then the flax GRUCell gate algebra and the
+// LayerNorm (eps 1e-6, E[x^2]-E[x]^2 variance) in the epilogue, writing only h'.
+// It replaces two GEMMs (N = 3H), the gate round trips through HBM and the separate
+// GRU/LN row kernel.
+//
+// Reduction order: k runs over the hidden state first (H rows of Wh, slab-aligned), then
+// over the input segments x = [seg0 | seg1 | seg2] (the rows of Wi).  The third gate
+// tile therefore accumulates ghn in the hidden slabs and gin in the input slabs; the
+// structurally-zero blocks of the stacked weight are never multiplied.
+//
+// Tile: 64 rows x 4H gate columns per workgroup of H/32 waves.  Wave w owns hidden units
+// [32w, 32w+32) of all four gates for all 64 rows (2 x 4 MFMA tiles, 128 accumulators),
+// so the gate algebra is lane-local; the LayerNorm row sums are reduced across the 32
+// lanes of a half-wave and then across waves through LDS in a fixed order.
+// Operand slabs (16 deep) are staged in LDS, register double-buffered.
+//
+// training: `g4` (nullable) receives the pre-activations [r_pre | z_pre | gin | ghn]
+// (R x 4H) that gru_ln_bwd (G4 form) consumes.
+#include "common.h"
+
+namespace msat {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kFR = 64;     // rows per workgroup
+constexpr int kFK = 16;     // slab depth
+constexpr int kFAP = 66;    // A slab row stride (words): conflict-free transposed ds_write_b32
+
+struct GruFwdArgs {
+    const float *seg[3];
+    int seg_ld[3];
+    int seg_w[3];
+    const float *hp;
+    int ldp;
+    const float *wi, *bi, *wh, *bh, *ln_scale, *ln_bias;
+    float *out;
+    int ldo;
+    float *g4;
+    int ldg;
+    int R, Kx;
+};
+
+__device__ __forceinline__ float fsig(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 2)
+gru_ln_fused_fwd_kernel(GruFwdArgs a) {
+    constexpr int H = 32 * NW, T = 64 * NW, BW = 3 * H;
+    constexpr int AN = (kFR * kFK / 4 + T - 1) / T;  // float4 A loads per thread
+    constexpr int BN = (kFK * BW / 4) / T;           // float4 B loads per thread (= 6)
+    static_assert((kFK * BW / 4) % T == 0, "B slab split");
+    __shared__ __attribute__((aligned(16))) float As[2][kFK * kFAP];
+    __shared__ __attribute__((aligned(16))) float Bs[2][kFK * BW];
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int row0 = blockIdx.x * kFR;
+    const int nsh = H / kFK;
+    const int ns = nsh + (a.Kx + kFK - 1) / kFK;
+
+    // A (activations): register-staged, stored k-major (transposed) into LDS.
+    // B (weights, L2-resident): global_load_lds_dwordx4 straight into a lane-linear LDS image
+    // (rows of Wi / Wh are contiguous, ld = 3H), no VGPRs.  Rows past Kx are clamped to the
+    // last valid row; the matching A columns are zero, so they contribute exact zeros.
+    float4 ra[AN];
+    auto loadA = [&](int s) {
+        const bool hid = s < nsh;
+#pragma unroll
+        for (int i = 0; i < AN; ++i) {
+            const int idx = t + i * T;
+            ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (idx < kFR * kFK / 4) {
+                const int r = row0 + (idx >> 2), kq = (idx & 3) * 4;
+                if (r < a.R) {
+                    const float *p = nullptr;
+                    if (hid) {
+                        p = a.hp + (size_t)r * a.ldp + s * kFK + kq;
+                    } else {
+                        int k = (s - nsh) * kFK + kq;
+#pragma unroll
+                        for (int g = 0; g < 3; ++g) {
+                            if (!p && k < a.seg_w[g]) p = a.seg[g] + (size_t)r * a.seg_ld[g] + k;
+                            k -= a.seg_w[g];
+                        }
+                    }
+                    if (p) ra[i] = *reinterpret_cast<const float4 *>(p);
+                }
+            }
+        }
+    };
+    auto issueB = [&](int s, int buf) {
+        const bool hid = s < nsh;
+        const float *W = hid ? a.wh : a.wi;
+        const int kb = hid ? s * kFK : (s - nsh) * kFK;
+        const int klast = (hid ? H : a.Kx) - 1;
+#pragma unroll
+        for (int i = 0; i < BN; ++i) {
+            const int f = i * T + t;  // float4 index in the slab image
+            const int r = f / (BW / 4), c4 = f - r * (BW / 4);
+            const float *src = W + (size_t)min(kb + r, klast) * BW + 4 * c4;
+            float *dst = Bs[buf] + 4 * (i * T + 64 * w);  // wave-uniform base; lane l lands at +16 l bytes
+            __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+        }
+    };
+    auto storeA = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AN; ++i) {
+            const int idx = t + i * T;
+            if (idx < kFR * kFK / 4) {
+                const int r = idx >> 2, kq = (idx & 3) * 4;
+                float *q = As[buf] + kq * kFAP + r;
+                q[0] = ra[i].x;
+                q[kFAP] = ra[i].y;
+                q[2 * kFAP] = ra[i].z;
+                q[3 * kFAP] = ra[i].w;
+            }
+        }
+    };
+
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[i][g] = f32x16{};
+
+    const int li = lane & 31, lk = lane >> 5;
+    auto slab = [&](int buf, bool hid) {
+        const float *A_ = As[buf], *B_ = Bs[buf] + 32 * w + li;
+        if (hid) {
+#pragma unroll
+            for (int kk = 0; kk < kFK; kk += 2) {
+                const int kr = kk + lk;
+                const float a0 = A_[kr * kFAP + li], a1 = A_[kr * kFAP + 32 + li];
+                const float *bp = B_ + kr * BW;
+                const float b0 = bp[0], b1 = bp[H], b2 = bp[2 * H];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+                acc[0][3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b2, acc[0][3], 0, 0, 0);
+                acc[1][3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b2, acc[1][3], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < kFK; kk += 2) {
+                const int kr = kk + lk;
+                const float a0 = A_[kr * kFAP + li], a1 = A_[kr * kFAP + 32 + li];
+                const float *bp = B_ + kr * BW;
+                const float b0 = bp[0], b1 = bp[H], b2 = bp[2 * H];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+                acc[0][2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b2, acc[0][2], 0, 0, 0);
+                acc[1][2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b2, acc[1][2], 0, 0, 0);
+            }
+        }
+    };
+
+    issueB(0, 0);
+    loadA(0);
+    storeA(0);
+    __syncthreads();
+    // two loops (hidden slabs, then input slabs) so each carries one accumulator subset
+    int buf = 0;
+    for (int s = 0; s < nsh; ++s) {
+        issueB(s + 1, buf ^ 1);  // ns > nsh: there is always a next slab here
+        loadA(s + 1);
+        slab(buf, true);
+        storeA(buf ^ 1);
+        __syncthreads();  // drains the LDS-DMA (vmcnt) and the A stores before the next slab
+        buf ^= 1;
+    }
+    for (int s = nsh; s < ns; ++s) {
+        const bool more = s + 1 < ns;
+        if (more) {
+            issueB(s + 1, buf ^ 1);
+            loadA(s + 1);
+        }
+        slab(buf, false);
+        if (more) storeA(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+
+    // ---------------------------------------------------------------- epilogue --
+    const int u = 32 * w + li;
+    const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
+    const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
+    float2 *red = reinterpret_cast<float2 *>(&As[0][0]);  // [NW][64] (As is free after the last sync)
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int lr = rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
+            const int row = row0 + lr;
+            const float rp = acc[rt][0][reg] + br, zp = acc[rt][1][reg] + bz;
+            const float gi = acc[rt][2][reg] + bni, gh = acc[rt][3][reg] + bnh;
+            float hv = 0.0f;
+            if (row < a.R) {
+                hv = a.hp[(size_t)row * a.ldp + u];
+                if (a.g4) {
+                    float *q = a.g4 + (size_t)row * a.ldg + u;
+                    q[0] = rp;
+                    q[H] = zp;
+                    q[2 * H] = gi;
+                    q[3 * H] = gh;
+                }
+            }
+            const float rg = fsig(rp), zg = fsig(zp);
+            const float ng = tanhf(gi + rg * gh);
+            const float hn = (1.0f - zg) * ng + zg * hv;
+            acc[rt][0][reg] = hn;
+            float s1 = hn, s2 = hn * hn;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                s1 += __shfl_xor(s1, o, 64);
+                s2 += __shfl_xor(s2, o, 64);
+            }
+            if (li == 0) red[w * kFR + lr] = make_float2(s1, s2);
+        }
+    __syncthreads();
+    const float sc = a.ln_scale[u], lb = a.ln_bias[u];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int lr = rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
+            const int row = row0 + lr;
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int v = 0; v < NW; ++v) {
+                const float2 p = red[v * kFR + lr];
+                s1 += p.x;
+                s2 += p.y;
+            }
+            const float mean = s1 / (float)H;
+            const float var = fmaxf(s2 / (float)H - mean * mean, 0.0f);
+            const float rs = rsqrtf(var + 1e-6f);
+            if (row < a.R) a.out[(size_t)row * a.ldo + u] = (acc[rt][0][reg] - mean) * (rs * sc) + lb;
+        }
+}
+
+static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace msat
+
+using namespace msat;
+
+extern "C" int msat_gru_ln_fused_fwd(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1,
+                                     int32_t w1, const float *x2, int32_t ld2, int32_t w2, const float *hprev,
+                                     int32_t ldp, const float *wi, const float *bi, const float *wh, const float *bh,
+                                     const float *ln_scale, const float *ln_bias, float *out, int32_t ldo, float *g4,
+                                     int32_t ldg, int32_t R, int32_t H, void *stream) {
+    MSAT_REQUIRE(H == 64 || H == 128 || H == 256, "gru_ln_fused: H must be 64, 128 or 256 (got %d)", H);
+    MSAT_REQUIRE(R >= 0, "gru_ln_fused: R < 0");
+    if (R == 0) return MSAT_OK;  // empty batches may carry NULL row pointers
+    MSAT_REQUIRE(x0 && hprev && wi && bi && wh && bh && ln_scale && ln_bias && out, "NULL pointer");
+    MSAT_REQUIRE(R >= 0 && ldo >= H && ldp >= H && (!g4 || ldg >= 4 * H), "gru_ln_fused: bad dims");
+    const float *seg[3] = {x0, x1, x2};
+    const int lds_[3] = {ld0, ld1, ld2}, ws[3] = {w0, w1, w2};
+    int Kx = 0;
+    for (int g = 0; g < 3; ++g) {
+        MSAT_REQUIRE(ws[g] >= 0 && ws[g] % 4 == 0, "gru_ln_fused: segment %d width %d must be a multiple of 4", g,
+                     ws[g]);
+        if (ws[g] == 0) continue;
+        MSAT_REQUIRE(seg[g] && aligned16(seg[g]) && lds_[g] % 4 == 0 && lds_[g] >= ws[g],
+                     "gru_ln_fused: segment %d must be 16-byte aligned with ld %% 4 == 0", g);
+        Kx += ws[g];
+    }
+    MSAT_REQUIRE(Kx > 0 && w0 > 0, "gru_ln_fused: empty input");
+    MSAT_REQUIRE(aligned16(hprev) && ldp % 4 == 0 && aligned16(wi) && aligned16(wh),
+                 "gru_ln_fused: hprev / weights must be 16-byte aligned");
+    GruFwdArgs a;
+    for (int g = 0; g < 3; ++g) {
+        a.seg[g] = ws[g] ? seg[g] : nullptr;
+        a.seg_ld[g] = lds_[g];
+        a.seg_w[g] = ws[g];
+    }
+    a.hp = hprev;
+    a.ldp = ldp;
+    a.wi = wi;
+    a.bi = bi;
+    a.wh = wh;
+    a.bh = bh;
+    a.ln_scale = ln_scale;
+    a.ln_bias = ln_bias;
+    a.out = out;
+    a.ldo = ldo;
+    a.g4 = g4;
+    a.ldg = ldg;
+    a.R = R;
+    a.Kx = Kx;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid((R + kFR - 1) / kFR);
+    if (H == 64) hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<2>), grid, dim3(128), 0, s, a);
+    else if (H == 128) hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<4>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<8>), grid, dim3(512), 0, s, a);
+    return check_launch("gru_ln_fused_fwd_kernel");
+}

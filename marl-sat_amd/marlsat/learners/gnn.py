@@ -63,13 +63,10 @@ class StepTape:
     Hn: torch.Tensor
     Hc: torch.Tensor
     GIN: torch.Tensor  # (Nc, 2H) gathered clause input
-    GIc: torch.Tensor
-    GHc: torch.Tensor
+    G4c: torch.Tensor  # (Nc, 4H) clause GRU pre-activations [r | z | gin | ghn]
     NV: torch.Tensor  # (Nv, 2H) var-side messages
-    GIp: torch.Tensor
-    GHp: torch.Tensor
-    GIn: torch.Tensor
-    GHn: torch.Tensor
+    G4p: torch.Tensor  # (Nv, 4H) update_v_pos pre-activations
+    G4n: torch.Tensor  # (Nv, 4H) update_v_neg pre-activations
 
 
 @dataclass
@@ -144,6 +141,21 @@ class GNNActorCritic:
         ws = self.scr.get_part(int(L_.msat_colsum_workspace_floats(M, N)))
         _chk(L_.msat_colsum(G, ldg, M, N, out, acc, ws.data_ptr(), self.stream), "msat_colsum")
 
+    def _gru(self, cell: str, segs, hprev: torch.Tensor, ln_row: torch.Tensor, out: torch.Tensor,
+             g4: Optional[torch.Tensor], R: int):
+        """One fused GRU cell + LayerNorm (msat_gru_ln_fused_fwd): segs = [(ptr, ld, width)] of x."""
+        H = self.H
+        segs = list(segs) + [(0, 0, 0)] * (3 - len(segs))
+        kx = sum(w for _, _, w in segs)
+        GNNActorCritic.flops += 2 * R * 3 * H * (H + (kx + 15) // 16 * 16)
+        (p0, l0, w0), (p1, l1, w1), (p2, l2, w2) = segs
+        _chk(L_.msat_gru_ln_fused_fwd(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
+                                      self.p(f"enc.{cell}_wi").data_ptr(), self.p(f"enc.{cell}_bi").data_ptr(),
+                                      self.p(f"enc.{cell}_wh").data_ptr(), self.p(f"enc.{cell}_bh").data_ptr(),
+                                      self._ptr(ln_row), self._ptr(ln_row, H), out.data_ptr(), H,
+                                      g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
+             "msat_gru_ln_fused_fwd")
+
     @staticmethod
     def _ptr(t: torch.Tensor, col: int = 0) -> int:
         return t.data_ptr() + col * t.element_size()
@@ -173,13 +185,9 @@ class GNNActorCritic:
             GIN = e(Nc, 2 * H)
             _chk(L_.msat_clause_gather(MV.data_ptr(), 2 * H, b.slots.data_ptr(), GIN.data_ptr(), 2 * H, Nc, H, 0,
                                        self.stream), "clause_gather")
-            GIc, GHc, Hc1 = e(Nc, 3 * H), e(Nc, 3 * H), e(Nc, H)
-            self._gemm(GIN.data_ptr(), 2 * H, self.p("enc.gru_c_wi").data_ptr(), 3 * H, 0, GIc.data_ptr(), 3 * H,
-                       self.p("enc.gru_c_bi").data_ptr(), Nc, 3 * H, 2 * H)
-            self._gemm(Hc.data_ptr(), H, self.p("enc.gru_c_wh").data_ptr(), 3 * H, 0, GHc.data_ptr(), 3 * H,
-                       self.p("enc.gru_c_bh").data_ptr(), Nc, 3 * H, H)
-            _chk(L_.msat_gru_ln_fwd(GIc.data_ptr(), 3 * H, GHc.data_ptr(), 3 * H, Hc.data_ptr(), H, pp(ln[3 * l]),
-                                    pp(ln[3 * l], H), Hc1.data_ptr(), H, Nc, H, self.stream), "gru_ln_fwd")
+            Hc1 = e(Nc, H)
+            G4c = e(Nc, 4 * H) if save else None
+            self._gru("gru_c", [(GIN.data_ptr(), 2 * H, 2 * H)], Hc, ln[3 * l], Hc1, G4c, Nc)
             TPN = e(Nc, 2 * H)
             self._gemm(Hc1.data_ptr(), H, self.p("enc.phi_v_w").data_ptr(), 2 * H, 0, TPN.data_ptr(), 2 * H,
                        self.p("enc.phi_v_b").data_ptr(), Nc, 2 * H, H)
@@ -188,20 +196,14 @@ class GNNActorCritic:
                                     Nv, H, 0, self.stream), "var_gather")
             outs = []
             for half, cell, Hx, k in ((0, "gru_vp", Hp, 3 * l + 1), (1, "gru_vn", Hn, 3 * l + 2)):
-                GI, GH, Hx1 = e(Nv, 3 * H), e(Nv, 3 * H), e(Nv, H)
-                wi = self.p(f"enc.{cell}_wi")
-                # input [n_v | x | svf] (learner:75,78): two GEMMs into the same gates
-                self._gemm(pp(NV, half * H), 2 * H, wi.data_ptr(), 3 * H, 0, GI.data_ptr(), 3 * H,
-                           self.p(f"enc.{cell}_bi").data_ptr(), Nv, 3 * H, H)
-                self._gemm(b.vfeat.data_ptr(), 4, pp(wi[H]), 3 * H, 0, GI.data_ptr(), 3 * H, None, Nv, 3 * H, 4, acc=1)
-                self._gemm(Hx.data_ptr(), H, self.p(f"enc.{cell}_wh").data_ptr(), 3 * H, 0, GH.data_ptr(), 3 * H,
-                           self.p(f"enc.{cell}_bh").data_ptr(), Nv, 3 * H, H)
-                _chk(L_.msat_gru_ln_fwd(GI.data_ptr(), 3 * H, GH.data_ptr(), 3 * H, Hx.data_ptr(), H, pp(ln[k]),
-                                        pp(ln[k], H), Hx1.data_ptr(), H, Nv, H, self.stream), "gru_ln_fwd")
-                outs.append((GI, GH, Hx1))
+                # input [n_v | x | svf] (learner:75,78)
+                Hx1 = e(Nv, H)
+                G4 = e(Nv, 4 * H) if save else None
+                self._gru(cell, [(pp(NV, half * H), 2 * H, H), (b.vfeat.data_ptr(), 4, 4)], Hx, ln[k], Hx1, G4, Nv)
+                outs.append((G4, Hx1))
             if save:
-                tape.append(StepTape(Hp, Hn, Hc, GIN, GIc, GHc, NV, outs[0][0], outs[0][1], outs[1][0], outs[1][1]))
-            Hp, Hn, Hc = outs[0][2], outs[1][2], Hc1
+                tape.append(StepTape(Hp, Hn, Hc, GIN, G4c, NV, outs[0][0], outs[1][0]))
+            Hp, Hn, Hc = outs[0][1], outs[1][1], Hc1
         return Hp, Hn, Hc, tape
 
     def encode_backward(self, b: GraphBatch, tape: List[StepTape], Hc_final, dHp, dHn, dHc):
@@ -215,15 +217,15 @@ class GNNActorCritic:
             Hc1 = tape[l + 1].Hc if l + 1 < self.L else Hc_final
             dNV = e(Nv, 2 * H)
             dprev = {}
-            for half, cell, Hx, GI, GH, dHx, k in ((0, "gru_vp", t.Hp, t.GIp, t.GHp, dHp, 3 * l + 1),
-                                                  (1, "gru_vn", t.Hn, t.GIn, t.GHn, dHn, 3 * l + 2)):
+            for half, cell, Hx, G4, dHx, k in ((0, "gru_vp", t.Hp, t.G4p, dHp, 3 * l + 1),
+                                              (1, "gru_vn", t.Hn, t.G4n, dHn, 3 * l + 2)):
                 dGI, dGH = e(Nv, 3 * H), e(Nv, 3 * H)
                 dHx0 = torch.zeros((Nv, H), dtype=torch.float32, device=dev)
                 part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nv, H)))
-                _chk(L_.msat_gru_ln_bwd(dHx.data_ptr(), H, GI.data_ptr(), 3 * H, GH.data_ptr(), 3 * H, Hx.data_ptr(), H,
-                                        pp(ln[k]), dGI.data_ptr(), 3 * H, dGH.data_ptr(), 3 * H, dHx0.data_ptr(), H,
-                                        pp(dln[k]), pp(dln[k], H), part.data_ptr(), Nv, H, 1, self.stream),
-                     "gru_ln_bwd")
+                _chk(L_.msat_gru_ln_bwd_g4(dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, pp(ln[k]),
+                                           dGI.data_ptr(), 3 * H, dGH.data_ptr(), 3 * H, dHx0.data_ptr(), H,
+                                           pp(dln[k]), pp(dln[k], H), part.data_ptr(), Nv, H, 1, self.stream),
+                     "gru_ln_bwd_g4")
                 wi, wh = self.p(f"enc.{cell}_wi"), self.p(f"enc.{cell}_wh")
                 gwi, gwh = self.g(f"enc.{cell}_wi"), self.g(f"enc.{cell}_wh")
                 # hidden path
@@ -250,10 +252,10 @@ class GNNActorCritic:
             dGI, dGH = e(Nc, 3 * H), e(Nc, 3 * H)
             dHc0 = torch.zeros((Nc, H), dtype=torch.float32, device=dev)
             part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nc, H)))
-            _chk(L_.msat_gru_ln_bwd(dHc.data_ptr(), H, t.GIc.data_ptr(), 3 * H, t.GHc.data_ptr(), 3 * H,
-                                    t.Hc.data_ptr(), H, pp(ln[3 * l]), dGI.data_ptr(), 3 * H, dGH.data_ptr(), 3 * H,
-                                    dHc0.data_ptr(), H, pp(dln[3 * l]), pp(dln[3 * l], H), part.data_ptr(), Nc, H, 1,
-                                    self.stream), "gru_ln_bwd")
+            _chk(L_.msat_gru_ln_bwd_g4(dHc.data_ptr(), H, t.G4c.data_ptr(), 4 * H, t.Hc.data_ptr(), H, pp(ln[3 * l]),
+                                       dGI.data_ptr(), 3 * H, dGH.data_ptr(), 3 * H, dHc0.data_ptr(), H,
+                                       pp(dln[3 * l]), pp(dln[3 * l], H), part.data_ptr(), Nc, H, 1, self.stream),
+                 "gru_ln_bwd_g4")
             self._gemm(dGH.data_ptr(), 3 * H, self.p("enc.gru_c_wh").data_ptr(), 3 * H, 1, dHc0.data_ptr(), H, None,
                        Nc, H, 3 * H, 1)
             self._wgrad(t.Hc.data_ptr(), H, dGH.data_ptr(), 3 * H, self.g("enc.gru_c_wh").data_ptr(), 3 * H, Nc, H,

@@ -1,0 +1,128 @@
+"""GPU: fused GRU cell + LayerNorm (msat_gru_ln_fused_fwd / msat_gru_ln_bwd_g4) vs a float64
+torch restatement of flax nn.GRUCell + nn.LayerNorm (learner:68-80).
+
+Inputs are segmented exactly as the encoder calls them: the var cells read
+x = [n_v (H, a column slice of a 2H buffer) | x, svf (4)], the clause cell
+x = [m_c+ | m_c-] (2H).  Row counts include 0, ragged tails (not a multiple of the
+64-row tile) and a size large enough to fill the chip.  Tolerances: h' 1e-5 relative
++ 1e-5 absolute (LayerNorm output is O(1)); pre-activation tape 2e-6 of sum|terms|;
+gradients 1e-4 of the tensor's max magnitude."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_gru_ln(x, h, wi, bi, wh, bh, sc, lb, H):
+    gi = x @ wi + bi
+    gh = h @ wh + bh
+    r = torch.sigmoid(gi[:, :H] + gh[:, :H])
+    z = torch.sigmoid(gi[:, H:2 * H] + gh[:, H:2 * H])
+    n = torch.tanh(gi[:, 2 * H:] + r * gh[:, 2 * H:])
+    hn = (1 - z) * n + z * h
+    mean = hn.mean(-1, keepdim=True)
+    var = (hn * hn).mean(-1, keepdim=True) - mean * mean
+    return (hn - mean) * torch.rsqrt(var + 1e-6) * sc + lb, gi, gh
+
+
+def _setup(R, H, kind, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    rnd = lambda *s: torch.randn(*s, device="cuda", generator=g)
+    if kind == "var":
+        NV = rnd(R, 2 * H)
+        vf = rnd(R, 4)
+        segs = [(NV, H, 2 * H, H), (vf, 0, 4, 4)]  # (tensor, col offset, ld, width)
+        x = torch.cat([NV[:, H:], vf], 1)
+        Kx = H + 4
+    else:
+        GIN = rnd(R, 2 * H)
+        segs = [(GIN, 0, 2 * H, 2 * H)]
+        x = GIN
+        Kx = 2 * H
+    h = rnd(R, H)
+    wi = rnd(Kx, 3 * H) / Kx ** 0.5
+    wh = rnd(H, 3 * H) / H ** 0.5
+    bi = rnd(3 * H) * 0.1
+    bh = torch.cat([torch.zeros(2 * H, device="cuda"), rnd(H) * 0.1])
+    sc = 1 + 0.1 * rnd(H)
+    lb = 0.1 * rnd(H)
+    return segs, x, h, wi, bi, wh, bh, sc, lb
+
+
+def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4):
+    from marlsat import _lib
+
+    out = torch.empty(R, H, device="cuda")
+    args = []
+    for t, off, ld, w in segs + [(None, 0, 0, 0)] * (3 - len(segs)):
+        args += [t.data_ptr() + 4 * off if t is not None else 0, ld, w]
+    _lib.check(_lib.lib.msat_gru_ln_fused_fwd(*args, h.data_ptr(), H, wi.data_ptr(), bi.data_ptr(), wh.data_ptr(),
+                                              bh.data_ptr(), sc.data_ptr(), lb.data_ptr(), out.data_ptr(), H,
+                                              g4.data_ptr() if g4 is not None else 0, 4 * H, R, H,
+                                              _lib.stream_ptr()), "gru_ln_fused_fwd")
+    return out
+
+
+@pytest.mark.parametrize("R", [0, 1, 77, 1000, 70000])
+@pytest.mark.parametrize("H", [64, 128, 256])
+@pytest.mark.parametrize("kind", ["var", "clause"])
+def test_fused_forward_matches_reference(R, H, kind):
+    if R == 70000 and H != 128:
+        pytest.skip("large case at the production width only")
+    segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=R + H)
+    g4 = torch.full((R, 4 * H), float("nan"), device="cuda")
+    out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4)
+    out_nt = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, None)  # inference form (no tape)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_nt)
+    if R == 0:
+        return
+    d = lambda t: t.double()
+    ref, gi, gh = _ref_gru_ln(d(x), d(h), d(wi), d(bi), d(wh), d(bh), d(sc), d(lb), H)
+    err = (out.double() - ref).abs()
+    assert bool((err <= 1e-5 * ref.abs() + 1e-5).all()), float(err.max())
+    # tape: [r_pre | z_pre | gin | ghn]
+    tape_ref = torch.cat([gi[:, :H] + gh[:, :H], gi[:, H:2 * H] + gh[:, H:2 * H], gi[:, 2 * H:], gh[:, 2 * H:]], 1)
+    absx = torch.cat([d(x).abs() @ d(wi).abs() + d(bi).abs(), d(h).abs() @ d(wh).abs() + d(bh).abs()], 1)
+    ab = torch.cat([absx[:, :H] + absx[:, 3 * H:4 * H], absx[:, H:2 * H] + absx[:, 4 * H:5 * H],
+                    absx[:, 2 * H:3 * H], absx[:, 5 * H:]], 1)
+    terr = (g4.double() - tape_ref).abs()
+    assert bool((terr <= 2e-6 * ab + 1e-30).all()), float((terr / (ab + 1e-30)).max())
+
+
+@pytest.mark.parametrize("R,H", [(77, 64), (1000, 128), (300, 256)])
+def test_g4_backward_matches_autograd(R, H):
+    from marlsat import _lib
+
+    segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, "var", seed=7 * R + H)
+    g4 = torch.empty(R, 4 * H, device="cuda")
+    _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4)
+    dy = torch.randn(R, H, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
+    dGi = torch.empty(R, 3 * H, device="cuda")
+    dGh = torch.empty(R, 3 * H, device="cuda")
+    dh = torch.zeros(R, H, device="cuda")
+    dln = torch.zeros(2 * H, device="cuda")
+    part = torch.empty(int(_lib.lib.msat_gru_ln_bwd_partial_floats(R, H)), device="cuda")
+    _lib.check(_lib.lib.msat_gru_ln_bwd_g4(dy.data_ptr(), H, g4.data_ptr(), 4 * H, h.data_ptr(), H, sc.data_ptr(),
+                                           dGi.data_ptr(), 3 * H, dGh.data_ptr(), 3 * H, dh.data_ptr(), H,
+                                           dln.data_ptr(), dln.data_ptr() + 4 * H, part.data_ptr(), R, H, 1,
+                                           _lib.stream_ptr()), "gru_ln_bwd_g4")
+    torch.cuda.synchronize()
+    # autograd through the float64 reference w.r.t. gi, gh (pre-activation gate vectors), h, LN params
+    d = lambda t: t.double().detach().requires_grad_(True)
+    xd, hd, scd, lbd = d(x), d(h), d(sc), d(lb)
+    gi = (xd @ wi.double() + bi.double()).detach().requires_grad_(True)
+    gh = (hd @ wh.double() + bh.double()).detach().requires_grad_(True)
+    r = torch.sigmoid(gi[:, :H] + gh[:, :H])
+    z = torch.sigmoid(gi[:, H:2 * H] + gh[:, H:2 * H])
+    n = torch.tanh(gi[:, 2 * H:] + r * gh[:, 2 * H:])
+    hn = (1 - z) * n + z * hd
+    mean = hn.mean(-1, keepdim=True)
+    var = (hn * hn).mean(-1, keepdim=True) - mean * mean
+    y = (hn - mean) * torch.rsqrt(var + 1e-6) * scd + lbd
+    (y * dy.double()).sum().backward()
+    for got, ref, what in ((dGi, gi.grad, "dGi"), (dGh, gh.grad, "dGh"), (dh, hd.grad, "dh"),
+                           (dln[:H], scd.grad, "dscale"), (dln[H:], lbd.grad, "dbias")):
+        scale = float(ref.abs().max())
+        err = float((got.double() - ref).abs().max())
+        assert err <= 1e-4 * scale + 1e-7, (what, err, scale)
