@@ -75,11 +75,13 @@ int msat_gru_ln_fused_fwd(const float *x0, int32_t ld0, int32_t w0, const float 
                           const float *wi, const float *bi, const float *wh, const float *bh,
                           const float *ln_scale, const float *ln_bias, float *out, int32_t ldo, float *g4,
                           int32_t ldg, int32_t R, int32_t H, void *stream);
-/* msat_gru_ln_bwd from the fused forward's g4 tape (same outputs; partial as msat_gru_ln_bwd). */
+/* msat_gru_ln_bwd from the fused forward's g4 tape (same outputs).  dbi (3H) / dbh_n (H), both
+ * or neither, receive (+=) the gate-bias gradients sum_rows dGi and sum_rows dGh[:, 2H:3H]
+ * (b_ir|b_iz|b_in and b_hn) from the same pass.  partial >= msat_gru_ln_bwd_partial_floats. */
 int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
                        int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
-                       float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *partial,
-                       int32_t R, int32_t H, int32_t accumulate_ln, void *stream);
+                       float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *dbi, float *dbh_n,
+                       float *partial, int32_t R, int32_t H, int32_t accumulate_ln, void *stream);
 /* out[N] (+)= column sums of G (M x N) — bias gradients; workspace >= msat_colsum_workspace_floats. */
 size_t msat_colsum_workspace_floats(int32_t M, int32_t N);
 int msat_colsum(const float *G, int32_t ldg, int32_t M, int32_t N, float *out, int32_t accumulate,

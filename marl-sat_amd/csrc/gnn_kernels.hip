@@ -115,17 +115,22 @@ gru_ln_fwd_kernel(const float *__restrict__ Gi, int ldi, const float *__restrict
 // fixed order.
 // G4 = true: Gi is the fused forward's pre-activation tape [r_pre | z_pre | gin | ghn]
 // (gru_fused.hip) and Gh is unused.
-template <int PER, bool G4>
+// NQ = 6: the partials also carry the gate-bias gradients, part[block] =
+// [dscale | dbias | d b_ir | d b_iz | d b_in | d b_hn] (H each), so no column-sum pass
+// over dGi / dGh is needed.
+template <int PER, bool G4, int NQ = 2>
 __global__ void __launch_bounds__(kRowThreads)
 gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
                   const float *__restrict__ scale, float *__restrict__ dGi, int lddi, float *__restrict__ dGh, int lddh,
                   float *__restrict__ dh, int lddh_prev, float *__restrict__ part, int R, int H) {
-    __shared__ float s_part[4][2 * 64 * PER];
+    __shared__ float s_part[4][NQ * 64 * PER];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float ps[PER], pb[PER];
+    float pq[NQ][PER];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) ps[u] = pb[u] = 0.f;
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int u = 0; u < PER; ++u) pq[q][u] = 0.f;
     for (int r = blockIdx.x * 4 + w; r < R; r += gridDim.x * 4) {
         const float *gi = Gi + (size_t)r * ldi, *gh = G4 ? gi : Gh + (size_t)r * ldh, *h = hp + (size_t)r * ldp;
         const float *g = dy + (size_t)r * ldy;
@@ -164,8 +169,8 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
             dxh[u] = dyv[u] * scale[j];
             a1 += dxh[u];
             a2 += dxh[u] * xh[u];
-            ps[u] += dyv[u] * xh[u];
-            pb[u] += dyv[u];
+            pq[0][u] += dyv[u] * xh[u];
+            pq[1][u] += dyv[u];
         }
         a1 = wave_sum_f32(a1) / (float)H;
         a2 = wave_sum_f32(a2) / (float)H;
@@ -187,31 +192,36 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
             dhh[H + j] = daz;
             dhh[2 * H + j] = dan * rg[u];
             dh[(size_t)r * lddh_prev + j] += dhn * zg[u];
+            if constexpr (NQ == 6) {
+                pq[2][u] += dar;
+                pq[3][u] += daz;
+                pq[4][u] += dan;
+                pq[5][u] += dan * rg[u];
+            }
         }
     }
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        s_part[w][lane + 64 * u] = ps[u];
-        s_part[w][64 * PER + lane + 64 * u] = pb[u];
-    }
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int u = 0; u < PER; ++u) s_part[w][q * 64 * PER + lane + 64 * u] = pq[q][u];
     __syncthreads();
-    for (int j = threadIdx.x; j < 2 * 64 * PER; j += kRowThreads) {
-        const float v = s_part[0][j] + s_part[1][j] + s_part[2][j] + s_part[3][j];
-        // part layout per block: [dscale (H) | dbias (H)]
-        const int half = j / (64 * PER), jj = j - half * 64 * PER;
-        if (jj < H) part[(size_t)blockIdx.x * 2 * H + half * H + jj] = v;
+    for (int j = threadIdx.x; j < NQ * 64 * PER; j += kRowThreads) {
+        const float v = (s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]);
+        const int q = j / (64 * PER), jj = j - q * 64 * PER;
+        if (jj < H) part[(size_t)blockIdx.x * NQ * H + q * H + jj] = v;
     }
 }
 
 // dst[j] (+)= sum_b part[b][j]: block per 64 columns, 4 waves stride the partial rows, fixed-order
 // combine (bitwise reproducible).
 __global__ void __launch_bounds__(256)
-partial_reduce_kernel(const float *__restrict__ part, int nblocks, int width, float *__restrict__ dst, int accumulate) {
+partial_reduce_kernel(const float *__restrict__ part, int nblocks, int width, float *__restrict__ dst, int accumulate,
+                      int ld) {
     __shared__ float red[4][64];
     const int j = blockIdx.x * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
     float s = 0.f;
     if (j < width)
-        for (int b = w; b < nblocks; b += 4) s += part[(size_t)b * width + j];
+        for (int b = w; b < nblocks; b += 4) s += part[(size_t)b * ld + j];
     red[w][threadIdx.x & 63] = s;
     __syncthreads();
     if (w == 0 && j < width) {
@@ -313,6 +323,14 @@ assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__rest
 using namespace msat;
 
 static int grid_rows(long rows) { return (int)std::min<long>((rows + 3) / 4, 8192); }
+// GRU/LN backward: at most 1024 blocks (16 waves per CU), so its per-block LN partials stay small
+static int bwd_blocks(long rows) { return (int)std::min<long>((rows + 3) / 4, 1024); }
+constexpr int kPartRows = 16;  // rows per first-stage block when reducing LN partials
+
+// dst (+)= sum over the nrows rows of part (nrows x width): 16-row first-stage sums, then the
+// fixed-order partial_reduce over them (deterministic; ws >= ceil(nrows/16) * width floats).
+static int reduce_partials(const float *part, int nrows, int width, float *dst, int accumulate, float *ws,
+                           hipStream_t s);
 
 static int colsum_splits(int M, int N) {
     const int colblocks = (N + 255) / 256;
@@ -320,6 +338,18 @@ static int colsum_splits(int M, int N) {
 }
 
 extern "C" size_t msat_colsum_workspace_floats(int32_t M, int32_t N) { return (size_t)colsum_splits(M, N) * N; }
+
+static int reduce_partials(const float *part, int nrows, int width, float *dst, int accumulate, float *ws,
+                           hipStream_t s) {
+    const int sp = (nrows + kPartRows - 1) / kPartRows;
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((width + 255) / 256, sp), dim3(256), 0, s, part, width, nrows, width,
+                       kPartRows, ws);
+    int rc = check_launch("colsum_partial_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((width + 63) / 64), dim3(256), 0, s, ws, sp, width, dst, accumulate,
+                       width);
+    return check_launch("partial_reduce_kernel");
+}
 
 extern "C" int msat_colsum(const float *G, int32_t ldg, int32_t M, int32_t N, float *out, int32_t accumulate,
                            float *workspace, void *stream) {
@@ -331,7 +361,8 @@ extern "C" int msat_colsum(const float *G, int32_t ldg, int32_t M, int32_t N, fl
                        workspace);
     int rc = check_launch("colsum_partial_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, s, workspace, sp, N, out, accumulate);
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, s, workspace, sp, N, out, accumulate,
+                       N);
     return check_launch("partial_reduce_kernel");
 }
 
@@ -367,7 +398,10 @@ extern "C" int msat_gru_ln_fwd(const float *Gi, int32_t ldi, const float *Gh, in
     return check_launch("gru_ln_fwd_kernel");
 }
 
-extern "C" size_t msat_gru_ln_bwd_partial_floats(int32_t R, int32_t H) { return (size_t)grid_rows(R) * 2 * H; }
+extern "C" size_t msat_gru_ln_bwd_partial_floats(int32_t R, int32_t H) {
+    const size_t nb = bwd_blocks(R);
+    return nb * 6 * H + (nb + kPartRows - 1) / kPartRows * 6 * H;  // block partials + reduction workspace
+}
 
 extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, int32_t ldi, const float *Gh, int32_t ldh,
                                const float *hprev, int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi,
@@ -380,38 +414,60 @@ extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, in
     MSAT_REQUIRE(dln_bias == dln_scale + H, "dln_bias must follow dln_scale (contiguous [scale|bias] grads)");
     if (R == 0) return MSAT_OK;
     hipStream_t s = (hipStream_t)stream;
-    const int nb = grid_rows(R);
+    const int nb = bwd_blocks(R);
     const dim3 g(nb), b(kRowThreads);
     if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
     else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
     else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, s, partial, nb, 2 * H, dln_scale,
-                       accumulate_ln);
-    return check_launch("partial_reduce_kernel");
+    return reduce_partials(partial, nb, 2 * H, dln_scale, accumulate_ln, partial + (size_t)nb * 2 * H, s);
 }
 
 extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
                                   int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
-                                  float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *partial,
-                                  int32_t R, int32_t H, int32_t accumulate_ln, void *stream) {
-    MSAT_REQUIRE(dy && g4 && hprev && ln_scale && dGi && dGh && dhprev && dln_scale && dln_bias && partial,
-                 "NULL pointer");
+                                  float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *dbi,
+                                  float *dbh_n, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
+                                  void *stream) {
     MSAT_REQUIRE(H == 64 || H == 128 || H == 256, "gru_ln: H must be 64, 128 or 256 (got %d)", H);
     MSAT_REQUIRE(ldg >= 4 * H, "gru_ln_bwd_g4: ldg must be >= 4H");
     MSAT_REQUIRE(dln_bias == dln_scale + H, "dln_bias must follow dln_scale (contiguous [scale|bias] grads)");
+    MSAT_REQUIRE((dbi == nullptr) == (dbh_n == nullptr), "gru_ln_bwd_g4: dbi and dbh_n go together");
     if (R == 0) return MSAT_OK;
+    MSAT_REQUIRE(dy && g4 && hprev && ln_scale && dGi && dGh && dhprev && dln_scale && partial, "NULL pointer");
     hipStream_t s = (hipStream_t)stream;
-    const int nb = grid_rows(R);
+    const int nb = bwd_blocks(R);
     const dim3 g(nb), b(kRowThreads);
-    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, true>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
-    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, true>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
-    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, true>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    const bool bias = dbi != nullptr;
+    const int NQ = bias ? 6 : 2;
+#define MSAT_BWD(PER)                                                                                              \
+    if (bias)                                                                                                      \
+        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, 6>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,    \
+                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);                           \
+    else                                                                                                           \
+        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, 2>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,    \
+                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    if (H == 64) { MSAT_BWD(1) }
+    else if (H == 128) { MSAT_BWD(2) }
+    else { MSAT_BWD(4) }
+#undef MSAT_BWD
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, s, partial, nb, 2 * H, dln_scale,
-                       accumulate_ln);
+    // stage 1: 16-row sums of the block partials; stage 2: fixed-order reduce of each column segment
+    float *ws = partial + (size_t)nb * NQ * H;
+    const int sp = (nb + kPartRows - 1) / kPartRows, width = NQ * H;
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((width + 255) / 256, sp), dim3(256), 0, s, partial, width, nb, width,
+                       kPartRows, ws);
+    rc = check_launch("colsum_partial_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, s, ws, sp, 2 * H, dln_scale,
+                       accumulate_ln, width);
+    if (bias) {
+        hipLaunchKernelGGL(partial_reduce_kernel, dim3((3 * H + 63) / 64), dim3(256), 0, s, ws + 2 * H, sp, 3 * H, dbi,
+                           1, width);
+        hipLaunchKernelGGL(partial_reduce_kernel, dim3((H + 63) / 64), dim3(256), 0, s, ws + 5 * H, sp, H, dbh_n, 1,
+                           width);
+    }
     return check_launch("partial_reduce_kernel");
 }
 

@@ -224,20 +224,19 @@ class GNNActorCritic:
                 part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nv, H)))
                 _chk(L_.msat_gru_ln_bwd_g4(dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, pp(ln[k]),
                                            dGI.data_ptr(), 3 * H, dGH.data_ptr(), 3 * H, dHx0.data_ptr(), H,
-                                           pp(dln[k]), pp(dln[k], H), part.data_ptr(), Nv, H, 1, self.stream),
-                     "gru_ln_bwd_g4")
+                                           pp(dln[k]), pp(dln[k], H), self.g(f"enc.{cell}_bi").data_ptr(),
+                                           pp(self.g(f"enc.{cell}_bh"), 2 * H), part.data_ptr(), Nv, H, 1,
+                                           self.stream), "gru_ln_bwd_g4")
                 wi, wh = self.p(f"enc.{cell}_wi"), self.p(f"enc.{cell}_wh")
                 gwi, gwh = self.g(f"enc.{cell}_wi"), self.g(f"enc.{cell}_wh")
                 # hidden path
                 self._gemm(dGH.data_ptr(), 3 * H, wh.data_ptr(), 3 * H, 1, dHx0.data_ptr(), H, None, Nv, H, 3 * H, 1)
                 self._wgrad(Hx.data_ptr(), H, dGH.data_ptr(), 3 * H, gwh.data_ptr(), 3 * H, Nv, H, 3 * H)
-                self._colsum(pp(dGH, 2 * H), 3 * H, Nv, H, pp(self.g(f"enc.{cell}_bh"), 2 * H))
                 # input path [n_v | x | svf]
                 self._gemm(dGI.data_ptr(), 3 * H, wi.data_ptr(), 3 * H, 1, pp(dNV, half * H), 2 * H, None, Nv, H,
                            3 * H, 0)
                 self._wgrad(pp(t.NV, half * H), 2 * H, dGI.data_ptr(), 3 * H, gwi.data_ptr(), 3 * H, Nv, H, 3 * H)
                 self._wgrad(b.vfeat.data_ptr(), 4, dGI.data_ptr(), 3 * H, pp(gwi[H]), 3 * H, Nv, 4, 3 * H)
-                self._colsum(dGI.data_ptr(), 3 * H, Nv, 3 * H, self.g(f"enc.{cell}_bi").data_ptr())
                 dprev[half] = dHx0
             # var gather backward = clause gather of dNV
             dTPN = e(Nc, 2 * H)
@@ -254,19 +253,18 @@ class GNNActorCritic:
             part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nc, H)))
             _chk(L_.msat_gru_ln_bwd_g4(dHc.data_ptr(), H, t.G4c.data_ptr(), 4 * H, t.Hc.data_ptr(), H, pp(ln[3 * l]),
                                        dGI.data_ptr(), 3 * H, dGH.data_ptr(), 3 * H, dHc0.data_ptr(), H,
-                                       pp(dln[3 * l]), pp(dln[3 * l], H), part.data_ptr(), Nc, H, 1, self.stream),
+                                       pp(dln[3 * l]), pp(dln[3 * l], H), self.g("enc.gru_c_bi").data_ptr(),
+                                       pp(self.g("enc.gru_c_bh"), 2 * H), part.data_ptr(), Nc, H, 1, self.stream),
                  "gru_ln_bwd_g4")
             self._gemm(dGH.data_ptr(), 3 * H, self.p("enc.gru_c_wh").data_ptr(), 3 * H, 1, dHc0.data_ptr(), H, None,
                        Nc, H, 3 * H, 1)
             self._wgrad(t.Hc.data_ptr(), H, dGH.data_ptr(), 3 * H, self.g("enc.gru_c_wh").data_ptr(), 3 * H, Nc, H,
                         3 * H)
-            self._colsum(pp(dGH, 2 * H), 3 * H, Nc, H, pp(self.g("enc.gru_c_bh"), 2 * H))
             dGIN = e(Nc, 2 * H)
             self._gemm(dGI.data_ptr(), 3 * H, self.p("enc.gru_c_wi").data_ptr(), 3 * H, 1, dGIN.data_ptr(), 2 * H,
                        None, Nc, 2 * H, 3 * H, 0)
             self._wgrad(t.GIN.data_ptr(), 2 * H, dGI.data_ptr(), 3 * H, self.g("enc.gru_c_wi").data_ptr(), 3 * H, Nc,
                         2 * H, 3 * H)
-            self._colsum(dGI.data_ptr(), 3 * H, Nc, 3 * H, self.g("enc.gru_c_bi").data_ptr())
             # clause gather backward = var gather of dGIN
             dMV = e(Nv, 2 * H)
             _chk(L_.msat_var_gather(dGIN.data_ptr(), 2 * H, b.ptr.data_ptr(), b.inc.data_ptr(), dMV.data_ptr(),

@@ -17,6 +17,7 @@ from marlsat.utils.generate_cnf_dataset import generate_problem_pool
 wl = sys.argv[1] if len(sys.argv) > 1 else "uf200"
 S_roll = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 S_train = int(sys.argv[3]) if len(sys.argv) > 3 else 32
+phases = sys.argv[4].split(",") if len(sys.argv) > 4 else ["rollout", "train"]
 V, C, vpa, sid = {"uf20": (20, 91, 10, 0), "uf50": (50, 218, 10, 1), "uf100": (100, 430, 10, 2),
                   "uf200": (200, 860, 8, 3)}[wl]
 H, L = 128, 16
@@ -41,8 +42,9 @@ def timed(fn, reps=3):
     return min(ts), GNNActorCritic.flops
 
 res = {"workload": wl, "H": H, "L": L, "A": env.num_agents}
-t, fl = timed(lambda: lr.policy(st, PRNGKey(1)))
-res["rollout_forward"] = {"samples": S_roll, "s": t, "samples_per_s": S_roll / t, "tflops": fl / t / 1e12,
+if "rollout" in phases:
+  t, fl = timed(lambda: lr.policy(st, PRNGKey(1)))
+  res["rollout_forward"] = {"samples": S_roll, "s": t, "samples_per_s": S_roll / t, "tflops": fl / t / 1e12,
                           "frac_fp32_mfma_peak": fl / t / 157.3e12}
 pidx = st.problem_idx[:S_train].contiguous(); x = st.variable_assignments[:S_train].contiguous()
 def train_step():
@@ -52,7 +54,8 @@ def train_step():
     dl = torch.where(torch.isfinite(logits), dl, torch.zeros_like(dl))
     dv = torch.randn_like(value) * 1e-3
     net.backward(gb, state, dl.contiguous(), dv.contiguous())
-t, fl = timed(train_step, reps=2)
-res["train_fwd_bwd"] = {"samples": S_train, "s": t, "samples_per_s": S_train / t, "tflops": fl / t / 1e12,
+if "train" in phases:
+  t, fl = timed(train_step, reps=2)
+  res["train_fwd_bwd"] = {"samples": S_train, "s": t, "samples_per_s": S_train / t, "tflops": fl / t / 1e12,
                         "frac_fp32_mfma_peak": fl / t / 157.3e12, "rows_per_sample": lr.tpl.mean_full_rows}
 print(json.dumps(res, indent=1))
