@@ -189,64 +189,56 @@ def mappo_bench(args, rank, world, dist):
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", default="uf200-860", choices=sorted(WORKLOADS))
-    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the workload's)")
-    ap.add_argument("--pool", type=int, default=1024, help="problem instances in the pool")
-    ap.add_argument("--obs-dtype", default="int32", choices=["int32", "int8"])
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline per core (0: skip)")
-    ap.add_argument("--mappo-workload", default="uf50-218", choices=sorted(WORKLOADS))
-    ap.add_argument("--mappo-envs", type=int, default=1024, help="envs per GPU in the MAPPO leg")
-    ap.add_argument("--mappo-T", type=int, default=8, help="NUM_STEPS of the MAPPO leg (0: skip the leg)")
-    args = ap.parse_args()
+MIXED = ("uf50-218", "uf100-430", "uf200-860")  # BASELINE config 5 size classes (1024 envs per GPU of 8192)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    V, C, vpa, B_default, size_id = WORKLOADS[args.workload]
-    B = args.envs or B_default
 
-    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
-
-    pool_np = generate_problem_pool(V, C, args.pool, size_id=size_id)
-
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
-        cpu = cpu_baseline(V, C, vpa, pool_np[: min(256, args.pool)], budget_s=args.cpu_budget)
-
+def env_leg(args, rank, world, dist):
+    """Time K fused env steps (+ auto-reset) over the local shard; returns the measurement dict."""
     import torch
 
-    torch.cuda.set_device(local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
     from marlsat import SATEnv
+    from marlsat.envs.mixed import MixedSATEnv
     from marlsat.random import Key
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
 
+    mixed = args.workload == "mixed"
+    names = MIXED if mixed else (args.workload,)
+    if mixed:
+        total = args.envs or 1024
+        sizes = [total // 3 + (1 if i < total % 3 else 0) for i in range(3)]
+    else:
+        sizes = [args.envs or WORKLOADS[args.workload][3]]
     obs_dtype = torch.int32 if args.obs_dtype == "int32" else torch.int8
-    env = SATEnv(V, C, max_steps=512, vars_per_agent=vpa, obs_dtype=obs_dtype)
-    A, M = env.num_agents, env.max_vars_per_agent
-    pool = env.make_pool(pool_np)
     seed = 0x5EED0000 + rank
-    obs, state = env.reset_from_pool(pool, B, Key(seed, 0))
-    out = env._step_out(B)
+    classes, pools, pools_np = [], [], []
+    for name in names:
+        V, C, vpa, _, size_id = WORKLOADS[name]
+        pools_np.append(generate_problem_pool(V, C, args.pool, size_id=size_id))
+        env = SATEnv(V, C, max_steps=512, vars_per_agent=vpa, obs_dtype=obs_dtype)
+        classes.append(env)
+        pools.append(env.make_pool(pools_np[-1]))
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     ring = 64
-    actions = torch.randint(0, M + 1, (ring, B, A), generator=gen, device="cuda", dtype=torch.int32)
-    step = env.stepper(state, obs, out, autoreset=True, seed=seed)
+    acts = [torch.randint(0, e.max_vars_per_agent + 1, (ring, b, e.num_agents), generator=gen, device="cuda",
+                          dtype=torch.int32) for e, b in zip(classes, sizes)]
+    if mixed:
+        menv = MixedSATEnv(classes)
+        obs, states = menv.reset(pools, sizes, Key(seed, 0))
+        outs = menv.alloc_outs(states)
+        gstep = menv.stepper(states, obs, outs, autoreset=True, seed=seed)
+        step = lambda i, c: gstep([a[i % ring] for a in acts], c)
+        kernel = "env_group_kernel<2,int>"
+    else:
+        o, st = classes[0].reset_from_pool(pools[0], sizes[0], Key(seed, 0))
+        obs, states, outs = [o], [st], [classes[0]._step_out(sizes[0])]
+        sstep = classes[0].stepper(st, o, outs[0], autoreset=True, seed=seed)
+        step = lambda i, c: sstep(acts[0][i % ring], c)
+        kernel = "env_kernel<2,int>"
     counter = 1
     for i in range(args.warmup):
-        step(actions[i % ring], counter)
+        step(i, counter)
         counter += 1
     torch.cuda.synchronize()
-
     K = args.steps
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     if dist is not None:
@@ -255,7 +247,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(K):
         ev[i][0].record()
-        step(actions[i % ring], counter)
+        step(i, counter)
         ev[i][1].record()
         counter += 1
     torch.cuda.synchronize()
@@ -267,25 +259,95 @@ def main():
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-
     # sanity: the state stays consistent (cheap device checks, after timing)
-    assert torch.equal(C - state.clauses_satisfied_status.int().sum(1), state.num_unsatisfied)
-    done_frac = float(out["done"].float().mean())
+    for e, st in zip(classes, states):
+        assert torch.equal(e.num_clauses - st.clauses_satisfied_status.int().sum(1), st.num_unsatisfied)
+    done_frac = float(torch.cat([o["done"].float() for o in outs]).mean())
+    per_class = []
+    launch_bytes = 0
+    for name, e, b in zip(names, classes, sizes):
+        pe = step_bytes(e.num_vars, e.num_clauses, e.num_agents)
+        if obs_dtype == torch.int8:
+            pe -= 3 * e.num_agents * (2 * e.num_vars + e.num_clauses)
+        launch_bytes += pe * b
+        per_class.append({"workload": name, "num_vars": e.num_vars, "num_clauses": e.num_clauses,
+                          "num_agents": e.num_agents, "vars_per_agent": WORKLOADS[name][2], "envs_per_gpu": b,
+                          "algorithmic_bytes_per_env_step": pe})
+    return {"names": names, "sizes": sizes, "elapsed": elapsed, "kern_ms": kern_ms, "K": K, "kernel": kernel,
+            "launch_bytes": launch_bytes, "per_class": per_class, "done_frac": done_frac}
 
-    del obs, state, out, actions, step, pool
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="uf200-860", choices=sorted(WORKLOADS) + ["mixed"],
+                    help="'mixed' = BASELINE config 5: uf50/uf100/uf200 classes in one ragged launch")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the workload's; mixed: 1024)")
+    ap.add_argument("--pool", type=int, default=1024, help="problem instances in the pool")
+    ap.add_argument("--obs-dtype", default="int32", choices=["int32", "int8"])
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline per core (0: skip)")
+    ap.add_argument("--mappo-workload", default="uf50-218", choices=sorted(WORKLOADS))
+    ap.add_argument("--mappo-envs", type=int, default=1024, help="envs per GPU in the MAPPO leg")
+    ap.add_argument("--mappo-T", type=int, default=8, help="NUM_STEPS of the MAPPO leg (0: skip the leg)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+
+        names = MIXED if args.workload == "mixed" else (args.workload,)
+        rates = []
+        for name in names:  # forked before any GPU initialisation
+            V, C, vpa, _, size_id = WORKLOADS[name]
+            pnp = generate_problem_pool(V, C, min(256, args.pool), size_id=size_id)
+            rates.append(cpu_baseline(V, C, vpa, pnp, budget_s=args.cpu_budget / len(names)))
+        cpu = rates[0]
+        if len(rates) > 1:  # time to step one env of each class in the workload's proportions
+            tot = args.envs or 1024
+            sz = [tot // 3 + (1 if i < tot % 3 else 0) for i in range(3)]
+            cpu = dict(rates[0], value=sum(sz) / sum(b / r["value"] for b, r in zip(sz, rates)),
+                       sample=" | ".join(r["sample"] for r in rates))
+
+    import torch
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    r = env_leg(args, rank, world, dist)
     mappo = mappo_bench(args, rank, world, dist) if args.mappo_T > 0 else None
 
     if rank == 0:
-        per_env = step_bytes(V, C, A)
-        if obs_dtype == torch.int8:
-            per_env -= 3 * A * (2 * V + C)
-        launch_bytes = per_env * B
-        achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_pmc_traffic(f"{args.workload}/B{B}/{args.obs_dtype}")
-        value = B * K * world / elapsed
+        B, K, elapsed, kern_ms = sum(r["sizes"]), r["K"], r["elapsed"], r["kern_ms"]
+        achieved = r["launch_bytes"] / (kern_ms * 1e-3) / 1e9
+        wl_key = args.workload if args.workload != "mixed" else "mixed"
+        traffic, traffic_src = load_pmc_traffic(f"{wl_key}/B{B}/{args.obs_dtype}")
+        sids = ",".join(str(WORKLOADS[n][4]) for n in r["names"])
+        cfg = {
+            "workload": f"{args.workload} SATEnv.step_env + rollout auto-reset (fused "
+                        f"{'msat_env_step_grouped, ragged size classes' if args.workload == 'mixed' else 'msat_env_step'})",
+            "envs_per_gpu": B, "global_envs": B * world, "max_steps": 512, "obs_dtype": args.obs_dtype,
+            "parallelism": f"dp{world} (independent env shards, no data-path collective)",
+        }
+        if len(r["per_class"]) == 1:
+            pc = r["per_class"][0]
+            cfg.update({k: pc[k] for k in ("num_vars", "num_clauses", "num_agents", "vars_per_agent")})
+            per_env = pc["algorithmic_bytes_per_env_step"]
+        else:
+            cfg["classes"] = r["per_class"]
+            per_env = r["launch_bytes"] / B
         rec = {
             "metric": METRIC,
-            "value": value,
+            "value": B * K * world / elapsed,
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
@@ -296,13 +358,8 @@ def main():
             "vs_baseline": None,
             "dtype": args.obs_dtype,
             "data": "synthetic (planted-solution random 3-SAT from the reference generator algorithm, "
-                    f"seed=1000*{size_id}+i, pool {args.pool}; random valid mode-0 actions)",
-            "config": {
-                "workload": f"{args.workload} SATEnv.step_env + rollout auto-reset (fused msat_env_step)",
-                "num_vars": V, "num_clauses": C, "num_agents": A, "vars_per_agent": vpa,
-                "envs_per_gpu": B, "global_envs": B * world, "max_steps": 512, "obs_dtype": args.obs_dtype,
-                "parallelism": f"dp{world} (independent env shards, no data-path collective)",
-            },
+                    f"seed=1000*size_id+i (size_id {sids}), pool {args.pool}; random valid mode-0 actions)",
+            "config": cfg,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -310,15 +367,15 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "env_kernel<2,int>",
+                "kernel": r["kernel"],
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_env_step": per_env,
-                "algorithmic_bytes_per_launch": launch_bytes,
+                "algorithmic_bytes_per_launch": r["launch_bytes"],
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
             "mappo": mappo,
-            "done_fraction_last_step": done_frac,
+            "done_fraction_last_step": r["done_frac"],
         }
         print(json.dumps(rec), flush=True)
     if dist is not None:

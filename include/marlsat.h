@@ -146,6 +146,21 @@ int msat_env_step(const msat_env_desc *desc, const msat_pool *pool,
                   const uint8_t *new_assign, uint64_t seed, uint64_t rng_counter,
                   const msat_step_out *out, void *obs, void *stream);
 
+/* Ragged batches (BASELINE config 5: mixed uf50/uf100/uf200): up to MSAT_MAX_GROUPS size
+ * classes, each a homogeneous batch with its own desc / pool / state / obs / actions / outs,
+ * advanced by ONE kernel launch (no padding to the largest instance; the reference cannot
+ * mix sizes at all, runner:118 jnp.stack).  Resets draw from the counter RNG only, class g
+ * keyed by seed ^ (g * 0x9E3779B97F4A7C15) -- bit-identical to msat_env_reset / msat_env_step
+ * of that class alone with that seed.  All classes share obs_dtype. */
+#define MSAT_MAX_GROUPS 8
+int msat_env_reset_grouped(int32_t num_groups, const msat_env_desc *descs, const msat_pool *pools,
+                           const msat_env_state *states, uint64_t seed, uint64_t rng_counter,
+                           void *const *obs, void *stream);
+int msat_env_step_grouped(int32_t num_groups, const msat_env_desc *descs, const msat_pool *pools,
+                          const msat_env_state *states, const int32_t *const *actions, int32_t autoreset,
+                          uint64_t seed, uint64_t rng_counter, const msat_step_out *outs, void *const *obs,
+                          void *stream);
+
 /* SATEnv.get_obs (env:345-398) of the current state, without changing it. */
 int msat_env_obs(const msat_env_desc *desc, const msat_pool *pool,
                  const msat_env_state *state, void *obs, void *stream);

@@ -24,6 +24,8 @@
 //   rollout auto-reset      src/learners/mappo_gnn_sat_learner.py:422-464
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace msat {
@@ -264,18 +266,20 @@ __device__ __forceinline__ void write_obs(const EnvParams &p, const EnvLds &l, O
 }
 
 // ---------------------------------------------------------------- kernel ----
+// XCD-major env order: blocks b and b+8 share an XCD (round-robin dispatch, speed only),
+// so consecutive envs -- adjacent obs blocks in HBM -- are written through one XCD's L2.
+__device__ __forceinline__ int xcd_major(int blk, int n, bool off) {
+    return (!off && (n & 7) == 0) ? (blk & 7) * (n >> 3) + (blk >> 3) : blk;
+}
+
+// One environment (index b of its batch) advanced / reset / observed by one workgroup.
 template <int MODE, typename ObsT>
-__global__ void __launch_bounds__(kThreads)
-env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__restrict__ actions,
-           const uint8_t *__restrict__ reset_mask, const int32_t *__restrict__ new_pidx,
-           const uint8_t *__restrict__ new_assign, uint64_t seed, uint64_t ctr, msat_step_out out,
-           ObsT *__restrict__ obs) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+__device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &pool, const msat_env_state &st,
+                                        const int32_t *__restrict__ actions, const uint8_t *__restrict__ reset_mask,
+                                        const int32_t *__restrict__ new_pidx, const uint8_t *__restrict__ new_assign,
+                                        uint64_t seed, uint64_t ctr, const msat_step_out &out, ObsT *__restrict__ obs,
+                                        int b, uint32_t *smem) {
     const EnvLds l = carve(smem, p);
-    int b = blockIdx.x;
-    // XCD-major env order: blocks b and b+8 share an XCD (round-robin dispatch, speed only),
-    // so consecutive envs -- adjacent obs blocks in HBM -- are written through one XCD's L2.
-    if (!(p.ablate & 4) && (p.B & 7) == 0) b = (blockIdx.x & 7) * (p.B >> 3) + (blockIdx.x >> 3);
     const int tid = threadIdx.x;
     if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
 
@@ -443,6 +447,52 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
         const int n = (p.A * p.D) / VEC;
         for (int q = tid; q < n; q += kThreads) ObsVec<ObsT>::store(o + q * VEC, 0u, 0u);
     }
+}
+
+template <int MODE, typename ObsT>
+__global__ void __launch_bounds__(kThreads)
+env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__restrict__ actions,
+           const uint8_t *__restrict__ reset_mask, const int32_t *__restrict__ new_pidx,
+           const uint8_t *__restrict__ new_assign, uint64_t seed, uint64_t ctr, msat_step_out out,
+           ObsT *__restrict__ obs) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int b = xcd_major(blockIdx.x, p.B, p.ablate & 4);
+    env_run<MODE, ObsT>(p, pool, st, actions, reset_mask, new_pidx, new_assign, seed, ctr, out, obs, b, smem);
+}
+
+// Ragged batches (BASELINE config 5): several size classes, each its own (V, C, A) batch with its own
+// pool / state / obs, advanced by ONE launch.  Blocks map to (class, env) in class order after the
+// XCD-major permutation of the whole grid.  Class g draws its resets from seed ^ group_seed(g), so it
+// replays exactly as a single-class launch with that seed (group_seed(0) = 0).
+struct EnvGroup {
+    EnvParams p;
+    msat_pool pool;
+    msat_env_state st;
+    const int32_t *actions;
+    msat_step_out out;
+    void *obs;
+    int begin;  // first block of the class
+};
+
+struct EnvGroups {
+    int G, total, ablate;
+    EnvGroup g[MSAT_MAX_GROUPS];
+};
+
+__host__ __device__ __forceinline__ uint64_t group_seed(int g) { return (uint64_t)g * 0x9E3779B97F4A7C15ull; }
+
+template <int MODE, typename ObsT>
+__global__ void __launch_bounds__(kThreads)
+env_group_kernel(EnvGroups gs, uint64_t seed, uint64_t ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int gb = xcd_major(blockIdx.x, gs.total, gs.ablate & 4);
+    int g = 0;
+#pragma unroll
+    for (int k = 1; k < MSAT_MAX_GROUPS; ++k)
+        if (k < gs.G && gb >= gs.g[k].begin) g = k;
+    const EnvGroup &e = gs.g[g];
+    env_run<MODE, ObsT>(e.p, e.pool, e.st, e.actions, nullptr, nullptr, nullptr, seed ^ group_seed(g), ctr, e.out,
+                        reinterpret_cast<ObsT *>(e.obs), gb - e.begin, smem);
 }
 
 // ---------------------------------------------------------------- cold path --
@@ -656,9 +706,68 @@ static int launch_env(const EnvParams &p, const msat_env_desc *d, const msat_poo
     return check_launch("env_kernel");
 }
 
+template <int MODE>
+static int launch_groups(int G, const msat_env_desc *descs, const msat_pool *pools, const msat_env_state *states,
+                         const int32_t *const *actions, uint64_t seed, uint64_t ctr, const msat_step_out *outs,
+                         void *const *obs, hipStream_t s) {
+    MSAT_REQUIRE(G >= 1 && G <= MSAT_MAX_GROUPS, "num_groups %d out of [1,%d]", G, MSAT_MAX_GROUPS);
+    MSAT_REQUIRE(descs && pools && states && obs, "NULL group arrays");
+    MSAT_REQUIRE(MODE == kModeReset || (actions && outs), "NULL actions / outs");
+    EnvGroups gs{};
+    gs.G = G;
+    size_t lds = 0;
+    int total = 0;
+    for (int g = 0; g < G; ++g) {
+        EnvGroup &e = gs.g[g];
+        int rc = make_params(&descs[g], &e.p);
+        if (rc) return rc;
+        if ((rc = check_state(&states[g])) || (rc = check_pool(&pools[g]))) return rc;
+        MSAT_REQUIRE(descs[g].obs_dtype == descs[0].obs_dtype, "groups must share obs_dtype");
+        MSAT_REQUIRE(obs[g], "NULL obs for group %d", g);
+        e.pool = pools[g];
+        e.st = states[g];
+        e.actions = MODE == kModeReset ? nullptr : actions[g];
+        if (MODE != kModeReset) {
+            MSAT_REQUIRE(e.actions && outs[g].reward && outs[g].done && outs[g].solved, "NULL step I/O, group %d", g);
+            e.out = outs[g];
+        }
+        e.obs = obs[g];
+        e.begin = total;
+        total += e.p.B;
+        lds = std::max(lds, env_lds_words(e.p) * 4);
+        gs.ablate = e.p.ablate;
+    }
+    MSAT_REQUIRE(lds <= 160 * 1024, "env needs %zu B of LDS (> 160 KiB)", lds);
+    gs.total = total;
+    if (total == 0) return MSAT_OK;
+    if (descs[0].obs_dtype == MSAT_OBS_I32)
+        hipLaunchKernelGGL((env_group_kernel<MODE, int32_t>), dim3(total), dim3(kThreads), lds, s, gs, seed, ctr);
+    else
+        hipLaunchKernelGGL((env_group_kernel<MODE, int8_t>), dim3(total), dim3(kThreads), lds, s, gs, seed, ctr);
+    return check_launch("env_group_kernel");
+}
+
 }  // namespace msat
 
 using namespace msat;
+
+extern "C" int msat_env_reset_grouped(int32_t num_groups, const msat_env_desc *descs, const msat_pool *pools,
+                                      const msat_env_state *states, uint64_t seed, uint64_t rng_counter,
+                                      void *const *obs, void *stream) {
+    return launch_groups<kModeReset>(num_groups, descs, pools, states, nullptr, seed, rng_counter, nullptr, obs,
+                                     (hipStream_t)stream);
+}
+
+extern "C" int msat_env_step_grouped(int32_t num_groups, const msat_env_desc *descs, const msat_pool *pools,
+                                     const msat_env_state *states, const int32_t *const *actions, int32_t autoreset,
+                                     uint64_t seed, uint64_t rng_counter, const msat_step_out *outs, void *const *obs,
+                                     void *stream) {
+    if (autoreset)
+        return launch_groups<kModeStepAutoReset>(num_groups, descs, pools, states, actions, seed, rng_counter, outs,
+                                                 obs, (hipStream_t)stream);
+    return launch_groups<kModeStep>(num_groups, descs, pools, states, actions, seed, rng_counter, outs, obs,
+                                    (hipStream_t)stream);
+}
 
 extern "C" int msat_pool_pack(const int32_t *lits, int32_t num_problems, int32_t num_clauses,
                               int32_t clause_width, int32_t num_vars, uint16_t *pool,

@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MARLSAT_LIB", os.path.join(_HERE, "lib", "libmarlsat.so"))
 
 OBS_I32, OBS_I8 = 0, 1
+MAX_GROUPS = 8  # MSAT_MAX_GROUPS
 REWARD_SPARSE, REWARD_PBRS = 0, 1
 
 
@@ -84,6 +85,13 @@ def _load():
             c_int32,
             [POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, c_int32, P, P, c_uint64, c_uint64,
              POINTER(StepOutC), P, P],
+        ),
+        "msat_env_reset_grouped": (
+            c_int32, [c_int32, POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), c_uint64, c_uint64, P, P]
+        ),
+        "msat_env_step_grouped": (
+            c_int32, [c_int32, POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, c_int32, c_uint64, c_uint64,
+                      POINTER(StepOutC), P, P]
         ),
         "msat_env_obs": (c_int32, [POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, P]),
         "msat_env_masks": (c_int32, [POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, P, P, P]),
@@ -177,6 +185,8 @@ EXPORTED = (
     "msat_pool_agent_tables",
     "msat_env_reset",
     "msat_env_step",
+    "msat_env_reset_grouped",
+    "msat_env_step_grouped",
     "msat_env_obs",
     "msat_env_masks",
     "msat_clause_features",

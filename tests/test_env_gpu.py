@@ -265,3 +265,44 @@ def test_full_size_uf200_x4096_properties_and_sampled_parity():
         np.testing.assert_array_equal(_np(obs)[sample], oobs)
         np.testing.assert_array_equal(_np(out["done"])[sample].astype(bool), d)
         np.testing.assert_array_equal(_np(st.variable_assignments)[sample], ost.variable_assignments)
+
+
+@pytest.mark.parametrize("obs_dtype", [torch.int32, torch.int8])
+def test_grouped_mixed_batch_equals_per_class(obs_dtype):
+    """Ragged batch (config 5 shape: several size classes in ONE launch) == each class stepped
+    alone with its class seed, bit for bit: state, obs and step outputs, through RNG resets."""
+    from marlsat.envs.mixed import MixedSATEnv, group_seed
+    from marlsat.random import Key
+
+    specs = [(20, 91, 10, 37), (50, 218, 10, 64), (23, 97, 10, 19), (200, 860, 8, 8)]  # V, C, vpa, B
+    classes, solo, pools = [], [], []
+    for i, (V, C, vpa, B) in enumerate(specs):
+        env, _ = _mk(V, C, vpa, max_steps=3, obs_dtype=obs_dtype)
+        env2, _ = _mk(V, C, vpa, max_steps=3, obs_dtype=obs_dtype)
+        classes.append(env)
+        solo.append(env2)
+        pools.append(_pool(V, C, 5, seed0=100 * i))
+    mixed = MixedSATEnv(classes)
+    key = Key(0xABCDEF, 3)
+    mpools = [c.make_pool(p) for c, p in zip(classes, pools)]
+    obs, states = mixed.reset(mpools, [s[3] for s in specs], key)
+    ref = []
+    for g, (env2, p, s) in enumerate(zip(solo, pools, specs)):
+        o, st = env2.reset_from_pool(env2.make_pool(p), s[3], Key(key.seed ^ group_seed(g), key.counter))
+        ref.append((o, st))
+    outs = mixed.alloc_outs(states)
+    step = mixed.stepper(states, obs, outs, autoreset=True, seed=0x5151)
+    rng = np.random.default_rng(0)
+    for t in range(6):  # max_steps 3: every env auto-resets at least once
+        acts = [torch.from_numpy(_random_actions(rng, c, s[3])).cuda() for c, s in zip(classes, specs)]
+        step(acts, 10 + t)
+        for g, (env2, (o, st)) in enumerate(zip(solo, ref)):
+            o2, out2 = env2.step_raw(st, acts[g], autoreset=True, key=Key(0x5151 ^ group_seed(g), 10 + t), obs=o)
+            ctx = f"class {g} step {t}"
+            assert torch.equal(obs[g], o2), ctx
+            for k in ("reward", "done", "solved", "num_unsatisfied", "episode_step"):
+                assert torch.equal(outs[g][k], out2[k]), (ctx, k)
+            for f in ("variable_assignments", "clauses_satisfied_status", "num_unsatisfied", "step", "done",
+                      "problem_idx"):
+                assert torch.equal(getattr(states[g], f), getattr(st, f)), (ctx, f)
+    assert any(bool(o["done"].any()) for o in outs)
