@@ -191,8 +191,9 @@ class MAPPOLearner:
     def _batch(self, pidx: torch.Tensor, x: torch.Tensor, critic_only: bool = False) -> GraphBatch:
         return assemble(self.tpl, self.pool.packed, self.svf, pidx.contiguous(), x.contiguous(), critic_only)
 
-    def policy(self, st: SATState, key: Key, greedy: bool = False):
-        """Actor + critic on the current states (learner:391-403): actions, log_probs, values."""
+    def policy(self, st: SATState, key: Key, greedy: bool = False, critic: bool = True):
+        """Actor (+ critic) on the current states (learner:391-403): actions, log_probs, values.
+        greedy: argmax actions (evaluate_policy, runner:38-46); critic=False skips the value head."""
         B = st.num_envs
         A, M = self.A, self.M
         act = torch.empty((B, A) if self.mode == 0 else (B, A, M), dtype=torch.int32, device=self.device)
@@ -202,8 +203,9 @@ class MAPPOLearner:
         for c, b0 in enumerate(range(0, B, self.chunk)):
             b1 = min(B, b0 + self.chunk)
             gb = self._batch(st.problem_idx[b0:b1], st.variable_assignments[b0:b1])
-            logits, value, _ = self.net.forward(gb)
-            val[b0:b1] = value
+            logits, value, _ = self.net.forward(gb, critic=critic)
+            if critic:
+                val[b0:b1] = value
             rows = logits.numel() // W
             _lib.check(L_.msat_sample_actions(logits.data_ptr(), rows, W, 1 if greedy else 0, key.seed,
                                               (key.counter << 16) + c, act[b0:b1].data_ptr(), logp[b0:b1].data_ptr(),

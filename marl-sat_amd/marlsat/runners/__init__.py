@@ -1,0 +1,1 @@
+"""Training / evaluation drivers (src/runners of the reference)."""

@@ -1,0 +1,112 @@
+"""Host-side pieces around the hot path (no GPU): DIMACS input (data_parser.py), the
+80/20 split, size-class grouping, the flax-msgpack checkpoint codec, config overrides
+and the test_solutions.txt line format."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+def test_parse_cnf_matches_reference_parser_fixture(tmp_path):
+    """tests/golden/parse_cnf.json holds a DIMACS text and the clause lists the reference's own
+    parser (src/test/verify_solutions.py parse_cnf_file) returned for it."""
+    from marlsat.utils.data_parser import parse_cnf
+
+    g = json.load(open(os.path.join(GOLDEN, "parse_cnf.json")))
+    p = tmp_path / "a.cnf"
+    p.write_text(g["text"])
+    V, C, clauses = parse_cnf(str(p))
+    assert clauses == g["clauses"]
+    head = [l for l in g["text"].splitlines() if l.startswith("p")][0].split()
+    assert (V, C) == (int(head[2]), int(head[3]))
+
+
+def test_parse_cnf_satlib_trailer_and_blank_lines(tmp_path):
+    from marlsat.utils.data_parser import parse_cnf
+
+    p = tmp_path / "uf3.cnf"
+    p.write_text("c SATLIB style\nc second comment\np cnf 3 2\n 1 -2 3 0\n\n-1 2 -3 0\n%\n0\n\n")
+    assert parse_cnf(str(p)) == (3, 2, [[1, -2, 3], [-1, 2, -3]])
+
+
+def test_generator_files_roundtrip_and_loader(tmp_path):
+    from marlsat.utils.data_parser import group_problems, load_cnf_problems, write_cnf
+    from marlsat.utils.generate_cnf_dataset import generate_cnf_dataset_sat, generate_sat_clauses
+
+    generate_cnf_dataset_sat(5, 20, 91, str(tmp_path), seed=7)
+    write_cnf(str(tmp_path / "z50.cnf"), 50, generate_sat_clauses(50, 218, seed=3).tolist(), comment="x")
+    probs = load_cnf_problems(str(tmp_path))
+    assert [p["name"] for p in probs] == sorted(os.listdir(tmp_path))
+    groups = group_problems(probs)
+    assert list(groups) == [(20, 91), (50, 218)]
+    assert groups[(20, 91)]["clauses"].shape == (5, 91, 3)
+    np.testing.assert_array_equal(groups[(50, 218)]["clauses"][0], generate_sat_clauses(50, 218, seed=3))
+
+
+def test_split_is_the_reference_split():
+    from marlsat.utils.data_parser import split_train_eval
+
+    idx = np.arange(37)
+    np.random.RandomState(42).shuffle(idx)
+    tr, ev = split_train_eval(37, 42)
+    np.testing.assert_array_equal(tr, idx[:29])
+    np.testing.assert_array_equal(ev, idx[29:])
+
+
+def test_checkpoint_codec_layout_and_roundtrip(tmp_path):
+    """flax serialization rules: arrays -> ExtType(1, packb((shape, dtype name, C bytes))),
+    numpy scalars -> ExtType(3, ...), nested dicts stay maps."""
+    import msgpack
+
+    from marlsat.utils import checkpoints as ck
+
+    a = np.arange(6, dtype=np.float32).reshape(2, 3)
+    tree = {"step": np.asarray(3, np.int32), "params": {"enc": {"kernel": a}},
+            "opt_state": {"0": {"count": np.asarray(3, np.int32)}, "1": {}}}
+    raw = ck.to_bytes(tree)
+    # decode with plain msgpack: the array leaf is ext type 1 holding (shape, "float32", bytes)
+    plain = msgpack.unpackb(raw, raw=False)
+    ext = plain["params"]["enc"]["kernel"]
+    assert isinstance(ext, msgpack.ExtType) and ext.code == 1
+    shape, name, buf = msgpack.unpackb(ext.data, raw=False)
+    assert shape == [2, 3] and name == "float32" and buf == a.tobytes()
+    back = ck.from_bytes(raw)
+    np.testing.assert_array_equal(back["params"]["enc"]["kernel"], a)
+    assert back["opt_state"]["1"] == {} and int(back["step"]) == 3
+    path = ck.save_checkpoint(str(tmp_path / "ckpt"), tree, 0, "latest_model_")
+    assert os.path.basename(path) == "latest_model_0"
+    got = ck.restore_checkpoint(str(tmp_path / "ckpt"), "latest_model_", None)
+    np.testing.assert_array_equal(got["params"]["enc"]["kernel"], a)
+    assert ck.restore_checkpoint(str(tmp_path / "missing")) is None
+
+
+def test_flax_tree_nesting_matches_param_layout():
+    from marlsat.learners import params as P
+    from marlsat.utils import checkpoints as ck
+
+    flat = P.to_flax(P.init_flat(64, 2, 3, 4, 0, seed=1), 64, 2, 3, 4, 0)
+    tree = ck.nest(flat)
+    assert set(tree) >= {"encoder", "critic_dense_0", "actor_flip_head_dense", "agent_id_embedding"}
+    assert tree["encoder"]["update_c"]["ir"]["kernel"].shape == (128, 64)
+    assert "LayerNorm_5" in tree["encoder"]
+    back = P.from_flax(ck.flatten(tree), 64, 2, 3, 4, 0)
+    np.testing.assert_array_equal(back, P.init_flat(64, 2, 3, 4, 0, seed=1))
+
+
+def test_config_overrides_and_solution_line(tmp_path):
+    from marlsat.runners.mappo_runner import flat_config, load_config, solution_line
+
+    cfg = load_config(os.path.join(os.path.dirname(__file__), "..", "configs", "MAPPO_CONFIG.yaml"),
+                      ["training.NUM_UPDATES=3", "loading.inject_bc_model_path=models/bc", "SEED=7"])
+    assert cfg["training"]["NUM_UPDATES"] == 3 and cfg["SEED"] == 7
+    assert cfg["loading"]["inject_bc_model_path"] == "models/bc"
+    fc = flat_config(cfg)
+    assert fc["NUM_VARS"] == 35 and fc["GNN_HIDDEN_DIM"] == 128 and fc["MINIBATCH_SIZE"] == 256
+    line = solution_line("uf20-01.cnf", True, 17, np.array([1, 0, 1], np.uint8))
+    m = re.search(r"Problem: ([\w.-]+), Solved: True, .* Solution: ([01]+)", line.strip())  # verify_solutions.py:107
+    assert m.groups() == ("uf20-01.cnf", "101")
+    assert solution_line("b.cnf", False, 0, None) == "Problem: b.cnf, Solved: False\n"
