@@ -13,6 +13,7 @@
 // tile, writes fp32 partial slabs and reduces them in a fixed order
 // (bitwise reproducible, no float atomics).
 #include <algorithm>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -206,15 +207,28 @@ __global__ void wgrad_reduce_kernel(const float *__restrict__ part, int splits, 
     *w = accumulate ? *w + s : s;
 }
 
+// at most 512 workgroups (2 per CU), >= ~1024 rows per split
 static int wgrad_splits(int M, int K, int N) {
     const int tiles = ((K + kTM - 1) / kTM) * ((N + kTN - 1) / kTN);
-    int splits = std::max(1, std::min(512 / std::max(tiles, 1), (M + 1023) / 1024));
-    return splits;
+    return std::max(1, std::min(512 / std::max(tiles, 1), (M + 1023) / 1024));
 }
 
 }  // namespace msat
 
 using namespace msat;
+
+// LDS-DMA fast path (gemm2.hip); MARLSAT_GEMM=1 forces the register-staged kernels (A/B tests).
+bool msat_gemm2_ok(const float *A, int lda, const float *B, int ldb, int transB, int N, int K);
+int msat_gemm2_launch(const float *A, int lda, const float *B, int ldb, int transB, float *C, int ldc,
+                      const float *bias, int M, int N, int K, int accumulate, hipStream_t s);
+bool msat_wgrad2_ok(const float *A, int lda, const float *G, int ldg, int K, int N);
+int msat_wgrad2_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
+                       int rows_per_split, hipStream_t s);
+
+static bool legacy_gemm() {
+    const char *e = getenv("MARLSAT_GEMM");
+    return e && e[0] == '1';
+}
 
 extern "C" int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ldb, int32_t transB, float *C,
                          int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, int32_t accumulate,
@@ -223,6 +237,11 @@ extern "C" int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ld
     MSAT_REQUIRE(M >= 0 && N >= 1 && K >= 0, "bad dims M=%d N=%d K=%d", M, N, K);
     MSAT_REQUIRE(lda >= K && ldc >= N && ldb >= (transB ? K : N), "leading dims too small");
     if (M == 0) return MSAT_OK;
+    if (!legacy_gemm() && msat_gemm2_ok(A, lda, B, ldb, transB, N, K)) {
+        const char *e = getenv("MARLSAT_GEMM");
+        const int acc = (e && e[0] == '2') ? 2 : accumulate;  // 2: store-less diagnostic
+        return msat_gemm2_launch(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, (hipStream_t)stream);
+    }
     dim3 grid((M + kTM - 1) / kTM, (N + kTN - 1) / kTN);
     hipLaunchKernelGGL(gemm_kernel, grid, dim3(kGT), 0, (hipStream_t)stream, A, lda, B, ldb, transB, C, ldc, bias, M,
                        N, K, accumulate);
@@ -240,10 +259,17 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
     hipStream_t s = (hipStream_t)stream;
     const int splits = wgrad_splits(M, K, N);
     const int rows = (M + splits - 1) / splits;
-    const int rows16 = ((rows + kKS - 1) / kKS) * kKS;
-    dim3 grid((K + kTM - 1) / kTM, (N + kTN - 1) / kTN, splits);
-    hipLaunchKernelGGL(gemm_wgrad_kernel, grid, dim3(kGT), 0, s, A, lda, G, ldg, (float *)workspace, M, K, N, rows16);
-    int rc = check_launch("gemm_wgrad_kernel");
+    int rc;
+    if (!legacy_gemm() && msat_wgrad2_ok(A, lda, G, ldg, K, N)) {
+        const int rows32 = ((rows + 31) / 32) * 32;
+        rc = msat_wgrad2_launch(A, lda, G, ldg, (float *)workspace, M, K, N, splits, rows32, s);
+    } else {
+        const int rows16 = ((rows + kKS - 1) / kKS) * kKS;
+        dim3 grid((K + kTM - 1) / kTM, (N + kTN - 1) / kTN, splits);
+        hipLaunchKernelGGL(gemm_wgrad_kernel, grid, dim3(kGT), 0, s, A, lda, G, ldg, (float *)workspace, M, K, N,
+                           rows16);
+        rc = check_launch("gemm_wgrad_kernel");
+    }
     if (rc) return rc;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((K * N + 255) / 256), dim3(256), 0, s, (const float *)workspace,
                        splits, K, N, W, ldw, accumulate);

@@ -69,3 +69,47 @@ def test_gemm_wgrad(M, K, N):
                                             ws.data_ptr(), _lib.stream_ptr()), "wgrad")
         if not acc:
             assert torch.equal(W, W1)  # bitwise reproducible
+
+
+@pytest.mark.parametrize("path", ["1", "0"])  # register-staged kernels / LDS-DMA fast path
+@pytest.mark.parametrize("M,N,K,transB", [(1, 4, 32, 0), (130, 132, 64, 0), (1000, 384, 256, 0), (257, 128, 384, 1),
+                                          (700, 260, 128, 1), (129, 256, 96, 0), (3, 128, 32, 1)])
+def test_gemm_fast_path_shapes(M, N, K, transB, path, monkeypatch):
+    """K % 32 == 0 shapes take the LDS-DMA kernel (tails in M and N: clamped reads, masked stores)."""
+    from marlsat import _lib
+
+    monkeypatch.setenv("MARLSAT_GEMM", path)
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    B = torch.randn((N, K) if transB else (K, N), device="cuda", generator=g)
+    bias = torch.randn(N, device="cuda", generator=g)
+    C0 = torch.randn(M, N, device="cuda", generator=g)
+    Bop = B.double().t() if transB else B.double()
+    for acc in (0, 1):
+        C = C0.clone()
+        _lib.check(_lib.lib.msat_gemm(A.data_ptr(), K, B.data_ptr(), B.shape[1], transB, C.data_ptr(), N,
+                                      bias.data_ptr(), M, N, K, acc, _lib.stream_ptr()), "gemm")
+        ref = A.double() @ Bop + bias.double() + (C0.double() if acc else 0)
+        absprod = A.double().abs() @ Bop.abs() + bias.double().abs() + (C0.double().abs() if acc else 0)
+        _ref_close(C, ref, absprod)
+
+
+@pytest.mark.parametrize("path", ["1", "0"])
+@pytest.mark.parametrize("M,K,N", [(1, 4, 4), (33, 128, 384), (5000, 132, 384), (70001, 128, 128), (100, 256, 8)])
+def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
+    """Row tails (M % 32 != 0, splits of uneven length) go through the zero-filled register slab."""
+    from marlsat import _lib
+
+    monkeypatch.setenv("MARLSAT_GEMM", path)
+    g = torch.Generator(device="cuda").manual_seed(M + K + N)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    G = torch.randn(M, N, device="cuda", generator=g)
+    W0 = torch.randn(K, N, device="cuda", generator=g)
+    ws = torch.empty(int(_lib.lib.msat_gemm_wgrad_workspace_bytes(M, K, N)) // 4 + 1, device="cuda")
+    for acc in (0, 1):
+        W = W0.clone()
+        _lib.check(_lib.lib.msat_gemm_wgrad(A.data_ptr(), K, G.data_ptr(), N, W.data_ptr(), N, M, K, N, acc,
+                                            ws.data_ptr(), _lib.stream_ptr()), "wgrad")
+        ref = A.double().t() @ G.double() + (W0.double() if acc else 0)
+        absprod = A.double().abs().t() @ G.double().abs() + (W0.double().abs() if acc else 0)
+        _ref_close(W, ref, absprod)
