@@ -195,6 +195,36 @@ gemm_wgrad_kernel(const float *__restrict__ A, int lda, const float *__restrict_
         }
 }
 
+// float4 form (N % 4 == 0, 16-byte aligned W rows): 8 independent loads in flight per thread
+__global__ void wgrad_reduce4_kernel(const float4 *__restrict__ part, int splits, int K, int N4, float4 *__restrict__ W,
+                                     int ldw4, int accumulate) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t KN4 = (size_t)K * N4;
+    if (t >= (int)KN4) return;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    int i = 0;
+    for (; i + 8 <= splits; i += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(i + u) * KN4 + t];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+        }
+    }
+    for (; i < splits; ++i) {
+        const float4 v = part[(size_t)i * KN4 + t];
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    const int k = t / N4, n4 = t - k * N4;
+    float4 *w = W + (size_t)k * ldw4 + n4;
+    if (accumulate) {
+        const float4 o = *w;
+        a.x = o.x + a.x; a.y = o.y + a.y; a.z = o.z + a.z; a.w = o.w + a.w;
+    }
+    *w = a;
+}
+
 // W[k][n] (+)= sum_s part[s][k][n]  (fixed split order -> reproducible)
 __global__ void wgrad_reduce_kernel(const float *__restrict__ part, int splits, int K, int N, float *__restrict__ W,
                                     int ldw, int accumulate) {
@@ -271,6 +301,13 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
         rc = check_launch("gemm_wgrad_kernel");
     }
     if (rc) return rc;
+    if (N % 4 == 0 && ldw % 4 == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(workspace) & 15) == 0) {
+        const int n4 = N / 4;
+        hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((K * n4 + 255) / 256), dim3(256), 0, s,
+                           (const float4 *)workspace, splits, K, n4, (float4 *)W, ldw / 4, accumulate);
+        return check_launch("wgrad_reduce4_kernel");
+    }
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((K * N + 255) / 256), dim3(256), 0, s, (const float *)workspace,
                        splits, K, N, W, ldw, accumulate);
     return check_launch("wgrad_reduce_kernel");

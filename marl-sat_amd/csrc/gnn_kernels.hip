@@ -241,6 +241,62 @@ colsum_partial_kernel(const float *__restrict__ G, int ldg, int M, int N, int ro
     part[(size_t)blockIdx.y * N + j] = s;
 }
 
+// float4 forms of the two reduction stages (16 column-float4 lanes x 16 row lanes per block,
+// rows strided over the row lanes, combined through LDS in a fixed order -> deterministic).
+// part[split][:] = column sums of G rows [split*rows_per, +rows_per).
+__global__ void __launch_bounds__(256)
+colsum4_kernel(const float4 *__restrict__ G, int ldg4, int M, int N4, int rows_per, float4 *__restrict__ part) {
+    __shared__ float4 red[16][16];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + tx;
+    const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < N4)
+        for (int r = r0 + ty; r < r1; r += 16) {
+            const float4 v = G[(size_t)r * ldg4 + c];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+    red[ty][tx] = a;
+    __syncthreads();
+    if (ty == 0 && c < N4) {
+        float4 t = red[0][tx];
+        for (int k = 1; k < 16; ++k) {
+            const float4 v = red[k][tx];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        part[(size_t)blockIdx.y * N4 + c] = t;
+    }
+}
+
+// dst[c] (+)= sum over the nrows rows of part (row stride ld4 float4s).
+__global__ void __launch_bounds__(256)
+partial_reduce4_kernel(const float4 *__restrict__ part, int nrows, int N4, int ld4, float4 *__restrict__ dst,
+                       int accumulate) {
+    __shared__ float4 red[16][16];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + tx;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < N4)
+        for (int r = ty; r < nrows; r += 16) {
+            const float4 v = part[(size_t)r * ld4 + c];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+    red[ty][tx] = a;
+    __syncthreads();
+    if (ty == 0 && c < N4) {
+        float4 t = red[0][tx];
+        for (int k = 1; k < 16; ++k) {
+            const float4 v = red[k][tx];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        if (accumulate) {
+            const float4 o = dst[c];
+            t.x = o.x + t.x; t.y = o.y + t.y; t.z = o.z + t.z; t.w = o.w + t.w;
+        }
+        dst[c] = t;
+    }
+}
+
 // ------------------------------------------------------------ elementwise --
 __global__ void relu_fwd_kernel(float *__restrict__ x, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -327,43 +383,54 @@ static int grid_rows(long rows) { return (int)std::min<long>((rows + 3) / 4, 819
 static int bwd_blocks(long rows) { return (int)std::min<long>((rows + 3) / 4, 1024); }
 constexpr int kPartRows = 16;  // rows per first-stage block when reducing LN partials
 
-// dst (+)= sum over the nrows rows of part (nrows x width): 16-row first-stage sums, then the
-// fixed-order partial_reduce over them (deterministic; ws >= ceil(nrows/16) * width floats).
-static int reduce_partials(const float *part, int nrows, int width, float *dst, int accumulate, float *ws,
-                           hipStream_t s);
 
+static bool a16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// float4 column-sum plan: ~1024 blocks, >= 64 rows per split
+static int colsum4_splits(int M, int N) {
+    const int cb = std::max(1, (N / 4 + 15) / 16);
+    return std::max(1, std::min((M + 63) / 64, std::max(1, 1024 / cb)));
+}
 static int colsum_splits(int M, int N) {
     const int colblocks = (N + 255) / 256;
     return std::max(1, std::min((M + 255) / 256, 1024 / colblocks));
 }
 
-extern "C" size_t msat_colsum_workspace_floats(int32_t M, int32_t N) { return (size_t)colsum_splits(M, N) * N; }
+extern "C" size_t msat_colsum_workspace_floats(int32_t M, int32_t N) {
+    return (size_t)std::max(colsum_splits(M, N), colsum4_splits(M, N)) * N;
+}
+
+// out (+)= column sums of G (M x N) in two fixed-order stages; float4 form when every row and
+// the output are 16-byte addressable.  ws >= msat_colsum_workspace_floats(M, N).
+static int colsum_det(const float *G, int ldg, int M, int N, float *out, int accumulate, float *ws, hipStream_t s) {
+    if (N % 4 == 0 && ldg % 4 == 0 && a16(G) && a16(out) && a16(ws)) {
+        const int sp = colsum4_splits(M, N), rows_per = (M + sp - 1) / sp, N4 = N / 4;
+        hipLaunchKernelGGL(colsum4_kernel, dim3((N4 + 15) / 16, sp), dim3(256), 0, s,
+                           reinterpret_cast<const float4 *>(G), ldg / 4, M, N4, rows_per, reinterpret_cast<float4 *>(ws));
+        int rc = check_launch("colsum4_kernel");
+        if (rc) return rc;
+        hipLaunchKernelGGL(partial_reduce4_kernel, dim3((N4 + 15) / 16), dim3(256), 0, s,
+                           reinterpret_cast<const float4 *>(ws), sp, N4, N4, reinterpret_cast<float4 *>(out), accumulate);
+        return check_launch("partial_reduce4_kernel");
+    }
+    const int sp = colsum_splits(M, N);
+    const int rows_per = (M + sp - 1) / sp;
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 255) / 256, sp), dim3(256), 0, s, G, ldg, M, N, rows_per, ws);
+    int rc = check_launch("colsum_partial_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, s, ws, sp, N, out, accumulate, N);
+    return check_launch("partial_reduce_kernel");
+}
 
 static int reduce_partials(const float *part, int nrows, int width, float *dst, int accumulate, float *ws,
                            hipStream_t s) {
-    const int sp = (nrows + kPartRows - 1) / kPartRows;
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3((width + 255) / 256, sp), dim3(256), 0, s, part, width, nrows, width,
-                       kPartRows, ws);
-    int rc = check_launch("colsum_partial_kernel");
-    if (rc) return rc;
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3((width + 63) / 64), dim3(256), 0, s, ws, sp, width, dst, accumulate,
-                       width);
-    return check_launch("partial_reduce_kernel");
+    return colsum_det(part, width, nrows, width, dst, accumulate, ws, s);
 }
 
 extern "C" int msat_colsum(const float *G, int32_t ldg, int32_t M, int32_t N, float *out, int32_t accumulate,
                            float *workspace, void *stream) {
-    MSAT_REQUIRE(G && out && workspace && N >= 1 && M >= 0 && ldg >= N, "bad colsum args");
-    hipStream_t s = (hipStream_t)stream;
-    const int sp = colsum_splits(M, N);
-    const int rows_per = (M + sp - 1) / sp;
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 255) / 256, sp), dim3(256), 0, s, G, ldg, M, N, rows_per,
-                       workspace);
-    int rc = check_launch("colsum_partial_kernel");
-    if (rc) return rc;
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, s, workspace, sp, N, out, accumulate,
-                       N);
-    return check_launch("partial_reduce_kernel");
+    MSAT_REQUIRE((G || M == 0) && out && workspace && N >= 1 && M >= 0 && ldg >= N, "bad colsum args");
+    return colsum_det(G, ldg, M, N, out, accumulate, workspace, (hipStream_t)stream);
 }
 
 extern "C" int msat_clause_gather(const float *src, int32_t ld_src, const int32_t *slots, float *dst, int32_t ld_dst,
@@ -453,22 +520,25 @@ extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4,
 #undef MSAT_BWD
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
-    // stage 1: 16-row sums of the block partials; stage 2: fixed-order reduce of each column segment
+    // stage 1: 16-row float4 sums of the block partials; stage 2: fixed-order reduce of each column segment
     float *ws = partial + (size_t)nb * NQ * H;
-    const int sp = (nb + kPartRows - 1) / kPartRows, width = NQ * H;
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3((width + 255) / 256, sp), dim3(256), 0, s, partial, width, nb, width,
-                       kPartRows, ws);
-    rc = check_launch("colsum_partial_kernel");
+    const int sp = (nb + kPartRows - 1) / kPartRows, width = NQ * H, W4 = width / 4;
+    MSAT_REQUIRE(a16(partial) && a16(dln_scale) && (!bias || (a16(dbi) && a16(dbh_n))),
+                 "gru_ln_bwd_g4: partial / gradient outputs must be 16-byte aligned");
+    hipLaunchKernelGGL(colsum4_kernel, dim3((W4 + 15) / 16, sp), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(partial), W4, nb, W4, kPartRows, reinterpret_cast<float4 *>(ws));
+    rc = check_launch("colsum4_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, s, ws, sp, 2 * H, dln_scale,
-                       accumulate_ln, width);
+    const float4 *ws4 = reinterpret_cast<const float4 *>(ws);
+    hipLaunchKernelGGL(partial_reduce4_kernel, dim3((2 * H / 4 + 15) / 16), dim3(256), 0, s, ws4, sp, 2 * H / 4, W4,
+                       reinterpret_cast<float4 *>(dln_scale), accumulate_ln);
     if (bias) {
-        hipLaunchKernelGGL(partial_reduce_kernel, dim3((3 * H + 63) / 64), dim3(256), 0, s, ws + 2 * H, sp, 3 * H, dbi,
-                           1, width);
-        hipLaunchKernelGGL(partial_reduce_kernel, dim3((H + 63) / 64), dim3(256), 0, s, ws + 5 * H, sp, H, dbh_n, 1,
-                           width);
+        hipLaunchKernelGGL(partial_reduce4_kernel, dim3((3 * H / 4 + 15) / 16), dim3(256), 0, s, ws4 + 2 * H / 4, sp,
+                           3 * H / 4, W4, reinterpret_cast<float4 *>(dbi), 1);
+        hipLaunchKernelGGL(partial_reduce4_kernel, dim3((H / 4 + 15) / 16), dim3(256), 0, s, ws4 + 5 * H / 4, sp, H / 4,
+                           W4, reinterpret_cast<float4 *>(dbh_n), 1);
     }
-    return check_launch("partial_reduce_kernel");
+    return check_launch("partial_reduce4_kernel");
 }
 
 extern "C" int msat_assemble_graph_batch(

@@ -113,3 +113,32 @@ def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
         ref = A.double().t() @ G.double() + (W0.double() if acc else 0)
         absprod = A.double().abs().t() @ G.double().abs() + (W0.double().abs() if acc else 0)
         _ref_close(W, ref, absprod)
+
+
+@pytest.mark.parametrize("M,N,ld,off", [(1, 4, 4, 0), (221000, 128, 256, 128), (5000, 384, 384, 0), (777, 7, 9, 1),
+                                        (0, 8, 8, 0), (100, 130, 132, 2)])
+def test_colsum_deterministic(M, N, ld, off):
+    """msat_colsum (bias gradients): float4 path when rows / output are 16-byte addressable, scalar
+    path otherwise; fixed reduction order -> identical results on repeat."""
+    from marlsat import _lib
+
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    buf = torch.randn(max(M, 1) * ld + off + 8, device="cuda", generator=g)
+    G = buf[off:off + M * ld].view(M, ld) if M else buf[:0].view(0, ld)
+    oo = off % 4  # output offset: 0 keeps it 16-byte aligned
+    out0 = torch.randn(N + 8, device="cuda", generator=g)
+    ws = torch.empty(int(_lib.lib.msat_colsum_workspace_floats(M, N)) + 4, device="cuda")
+    res = []
+    for _ in range(2):
+        out = out0.clone()
+        _lib.check(_lib.lib.msat_colsum(G.data_ptr(), ld, M, N, out.data_ptr() + 4 * oo, 1, ws.data_ptr(),
+                                        _lib.stream_ptr()), "colsum")
+        res.append(out)
+    assert torch.equal(res[0], res[1])
+    ref = out0.double().clone()
+    if M:
+        ref[oo:oo + N] += G[:, :N].double().sum(0)
+    err = (res[0].double() - ref).abs()
+    bound = 2e-6 * (G[:, :N].double().abs().sum(0) if M else torch.zeros(N, dtype=torch.float64, device="cuda"))
+    assert bool((err[oo:oo + N] <= bound + 1e-6).all())
+    assert torch.equal(res[0][:oo], out0[:oo]) and torch.equal(res[0][oo + N:], out0[oo + N:])
