@@ -21,6 +21,8 @@
 //
 // training: `g4` (nullable) receives the pre-activations [r_pre | z_pre | gin | ghn]
 // (R x 4H) that gru_ln_bwd (G4 form) consumes.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace msat {
@@ -47,10 +49,12 @@ struct GruFwdArgs {
 
 __device__ __forceinline__ float fsig(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
-template <int NW>
-__global__ void __launch_bounds__(64 * NW, 2)
+// NW = H / 32 unit groups; RS = waves per unit group (row split of the 64-row tile): wave w
+// owns units [32 (w % NW), +32) of all four gates for rows [(w / NW) * 64 / RS, +64 / RS).
+template <int NW, int RS>
+__global__ void __launch_bounds__(64 * NW * RS, 2)
 gru_ln_fused_fwd_kernel(GruFwdArgs a) {
-    constexpr int H = 32 * NW, T = 64 * NW, BW = 3 * H;
+    constexpr int H = 32 * NW, T = 64 * NW * RS, BW = 3 * H, RT = 2 / RS;
     constexpr int AN = (kFR * kFK / 4 + T - 1) / T;  // float4 A loads per thread
     constexpr int BN = (kFK * BW / 4) / T;           // float4 B loads per thread (= 6)
     static_assert((kFK * BW / 4) % T == 0, "B slab split");
@@ -58,6 +62,7 @@ gru_ln_fused_fwd_kernel(GruFwdArgs a) {
     __shared__ __attribute__((aligned(16))) float Bs[2][kFK * BW];
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wu = w % NW, wrow = (w / NW) * (kFR / RS);
     const int row0 = blockIdx.x * kFR;
     const int nsh = H / kFK;
     const int ns = nsh + (a.Kx + kFK - 1) / kFK;
@@ -121,42 +126,28 @@ gru_ln_fused_fwd_kernel(GruFwdArgs a) {
         }
     };
 
-    f32x16 acc[2][4];
+    f32x16 acc[RT][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[i][g] = f32x16{};
 
     const int li = lane & 31, lk = lane >> 5;
+    // hid: third gate tile accumulates ghn (hidden slabs) or gin (input slabs)
     auto slab = [&](int buf, bool hid) {
-        const float *A_ = As[buf], *B_ = Bs[buf] + 32 * w + li;
-        if (hid) {
+        const float *A_ = As[buf] + wrow + li, *B_ = Bs[buf] + 32 * wu + li;
 #pragma unroll
-            for (int kk = 0; kk < kFK; kk += 2) {
-                const int kr = kk + lk;
-                const float a0 = A_[kr * kFAP + li], a1 = A_[kr * kFAP + 32 + li];
-                const float *bp = B_ + kr * BW;
-                const float b0 = bp[0], b1 = bp[H], b2 = bp[2 * H];
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-                acc[0][3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b2, acc[0][3], 0, 0, 0);
-                acc[1][3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b2, acc[1][3], 0, 0, 0);
-            }
-        } else {
+        for (int kk = 0; kk < kFK; kk += 2) {
+            const int kr = kk + lk;
+            const float *bp = B_ + kr * BW;
+            const float b0 = bp[0], b1 = bp[H], b2 = bp[2 * H];
 #pragma unroll
-            for (int kk = 0; kk < kFK; kk += 2) {
-                const int kr = kk + lk;
-                const float a0 = A_[kr * kFAP + li], a1 = A_[kr * kFAP + 32 + li];
-                const float *bp = B_ + kr * BW;
-                const float b0 = bp[0], b1 = bp[H], b2 = bp[2 * H];
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-                acc[0][2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b2, acc[0][2], 0, 0, 0);
-                acc[1][2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b2, acc[1][2], 0, 0, 0);
+            for (int rt = 0; rt < RT; ++rt) {
+                const float av = A_[kr * kFAP + 32 * rt];
+                acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b0, acc[rt][0], 0, 0, 0);
+                acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b1, acc[rt][1], 0, 0, 0);
+                if (hid) acc[rt][3] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b2, acc[rt][3], 0, 0, 0);
+                else acc[rt][2] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b2, acc[rt][2], 0, 0, 0);
             }
         }
     };
@@ -188,15 +179,15 @@ gru_ln_fused_fwd_kernel(GruFwdArgs a) {
     }
 
     // ---------------------------------------------------------------- epilogue --
-    const int u = 32 * w + li;
+    const int u = 32 * wu + li;
     const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
     const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
     float2 *red = reinterpret_cast<float2 *>(&As[0][0]);  // [NW][64] (As is free after the last sync)
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-            const int lr = rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
+            const int lr = wrow + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
             const int row = row0 + lr;
             const float rp = acc[rt][0][reg] + br, zp = acc[rt][1][reg] + bz;
             const float gi = acc[rt][2][reg] + bni, gh = acc[rt][3][reg] + bnh;
@@ -221,15 +212,15 @@ gru_ln_fused_fwd_kernel(GruFwdArgs a) {
                 s1 += __shfl_xor(s1, o, 64);
                 s2 += __shfl_xor(s2, o, 64);
             }
-            if (li == 0) red[w * kFR + lr] = make_float2(s1, s2);
+            if (li == 0) red[wu * kFR + lr] = make_float2(s1, s2);
         }
     __syncthreads();
     const float sc = a.ln_scale[u], lb = a.ln_bias[u];
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-            const int lr = rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
+            const int lr = wrow + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
             const int row = row0 + lr;
             float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -297,8 +288,16 @@ extern "C" int msat_gru_ln_fused_fwd(const float *x0, int32_t ld0, int32_t w0, c
     a.Kx = Kx;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((R + kFR - 1) / kFR);
-    if (H == 64) hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<2>), grid, dim3(128), 0, s, a);
-    else if (H == 128) hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<4>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<8>), grid, dim3(512), 0, s, a);
+    const char *e = getenv("MARLSAT_GRU_RS");  // row split (1 or 2 waves per unit group), A/B measurements
+    const int rs = (e && atoi(e) == 1) ? 1 : 2;
+    if (H == 64) {
+        if (rs == 2) hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<2, 2>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<2, 1>), grid, dim3(128), 0, s, a);
+    } else if (H == 128) {
+        if (rs == 2) hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<4, 2>), grid, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<4, 1>), grid, dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<8, 1>), grid, dim3(512), 0, s, a);
+    }
     return check_launch("gru_ln_fused_fwd_kernel");
 }

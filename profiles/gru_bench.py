@@ -1,0 +1,41 @@
+"""Fused GRU + LayerNorm forward microbenchmark (rollout = no tape, training = with the G4 tape):
+row split RS=1 (2 waves/SIMD, 128 accumulators per lane) vs RS=2 (4 waves/SIMD, 64)."""
+import json, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "marl-sat_amd")]
+import torch
+from marlsat import _lib
+
+H = 128
+for kind, R, segs_w in (("var", 887000, (H, 4)), ("clause", 857000, (2 * H,))):
+    g = torch.Generator(device="cuda").manual_seed(0)
+    X = [torch.randn(R, w if w != H else 2 * H, device="cuda", generator=g) for w in segs_w]
+    h = torch.randn(R, H, device="cuda", generator=g)
+    Kx = sum(segs_w)
+    wi = torch.randn(Kx, 3 * H, device="cuda", generator=g) / Kx ** 0.5
+    wh = torch.randn(H, 3 * H, device="cuda", generator=g) / H ** 0.5
+    bi, bh = torch.zeros(3 * H, device="cuda"), torch.zeros(3 * H, device="cuda")
+    sc, lb = torch.ones(H, device="cuda"), torch.zeros(H, device="cuda")
+    out = torch.empty(R, H, device="cuda")
+    g4 = torch.empty(R, 4 * H, device="cuda")
+    args = []
+    for x, w in zip(X, segs_w):
+        args += [x.data_ptr(), x.shape[1], w]
+    args += [0, 0, 0] * (3 - len(segs_w))
+    for tape in (False, True):
+        for rs in ("1", "2"):
+            os.environ["MARLSAT_GRU_RS"] = rs
+            f = lambda: _lib.lib.msat_gru_ln_fused_fwd(*args, h.data_ptr(), H, wi.data_ptr(), bi.data_ptr(),
+                                                       wh.data_ptr(), bh.data_ptr(), sc.data_ptr(), lb.data_ptr(),
+                                                       out.data_ptr(), H, g4.data_ptr() if tape else 0, 4 * H, R, H,
+                                                       _lib.stream_ptr())
+            f(); torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(10):
+                f()
+            b.record(); torch.cuda.synchronize()
+            us = a.elapsed_time(b) / 10 * 1e3
+            fl = 2 * R * 3 * H * (H + (Kx + 15) // 16 * 16)
+            print(json.dumps({"cell": kind, "R": R, "tape": tape, "RS": rs, "us": round(us, 1),
+                              "tflops": round(fl / us / 1e6, 1)}))
