@@ -140,7 +140,9 @@ def mappo_bench(args, rank, world, dist):
     learner = MAPPOLearner(cfg, env, net, pool, dist=dist if world > 1 else None)
     rs = learner.init_runner_state(PRNGKey(77 + rank))
     gen = torch.Generator().manual_seed(99 + rank)
-    rs, _ = learner.train_cycle(rs, 0, gen)  # warm-up: kernels loaded, caches and pools grown
+    learner.cfg["UPDATE_EPOCHS"] = 1  # warm-up cycle (every kernel and buffer shape), one epoch
+    rs, _ = learner.train_cycle(rs, 0, gen)
+    learner.cfg["UPDATE_EPOCHS"] = E
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
     if dist is not None:
@@ -290,7 +292,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline per core (0: skip)")
     ap.add_argument("--mappo-workload", default="uf50-218", choices=sorted(WORKLOADS))
     ap.add_argument("--mappo-envs", type=int, default=1024, help="envs per GPU in the MAPPO leg")
-    ap.add_argument("--mappo-T", type=int, default=8, help="NUM_STEPS of the MAPPO leg (0: skip the leg)")
+    ap.add_argument("--mappo-T", type=int, default=32, help="NUM_STEPS of the MAPPO leg (0: skip the leg)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

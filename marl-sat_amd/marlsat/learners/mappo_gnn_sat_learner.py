@@ -153,10 +153,11 @@ class MAPPOLearner:
                                    env.num_agents, self.device)
         H, L = network.H, network.L
         rows = self.tpl.mean_full_rows
-        # saved activations per sample (encode tape, fp32): var rows ~16H, clause rows ~9H per step
-        per_sample_train = 4.0 * L * rows * 16 * H + 4.0 * rows * 24 * H
+        # saved activations per sample (encode tape, fp32, per message step): var rows Hp, Hn, NV, two
+        # G4 tapes = 12H, clause rows Hc, GIN, G4 = 7H (bounded by 12H), plus ~24H of transients
+        per_sample_train = 4.0 * L * rows * 12 * H + 4.0 * rows * 24 * H
         per_sample_infer = 4.0 * rows * 24 * H
-        budget = micro_bytes if micro_bytes is not None else float(config.get("MICROBATCH_BYTES", 48e9))
+        budget = micro_bytes if micro_bytes is not None else float(config.get("MICROBATCH_BYTES", 100e9))
         self.micro = max(1, min(self.MB, int(budget // per_sample_train)))
         self.chunk = max(1, min(self.B, int(budget // per_sample_infer)))
         self.A, self.M = env.num_agents, env.max_vars_per_agent
