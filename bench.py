@@ -318,12 +318,20 @@ def main():
 
     import torch
 
-    torch.cuda.set_device(local_rank)
+    # MARLSAT_DIST_BACKEND=gloo + MARLSAT_SHARE_GPU=1: rehearsal of the N>1 path with several ranks on
+    # one GPU (RCCL refuses two ranks per device); the driver's runs use RCCL, one GPU per rank.
+    share = os.environ.get("MARLSAT_SHARE_GPU") == "1"
+    dev_idx = local_rank % torch.cuda.device_count() if share else local_rank
+    torch.cuda.set_device(dev_idx)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        backend = os.environ.get("MARLSAT_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(backend)
 
     r = env_leg(args, rank, world, dist)
     mappo = mappo_bench(args, rank, world, dist) if args.mappo_T > 0 else None
