@@ -60,6 +60,9 @@ extern "C" {
 /* reward modes */
 #define MSAT_REWARD_SPARSE 0 /* active reference reward: 1.0 on solve else 0 (env:183-198) */
 #define MSAT_REWARD_PBRS 1   /* commented reference variant (env:201-223)                  */
+#define MSAT_REWARD_SINGLE_DELTA 2 /* single-agent SatEnv (src/envs/sat_env.py:77-118): f32     */
+                                   /* ((u_prev - u_new) * 10 + r_sat * solved) - 0.005, u =      */
+                                   /* unsat/C; done = solved || step >= max_steps (pre-increment) */
 
 /* Static description of one batch of environments (all envs share V, C, K, A). */
 typedef struct msat_env_desc {
@@ -160,6 +163,22 @@ int msat_env_step_grouped(int32_t num_groups, const msat_env_desc *descs, const 
                           const msat_env_state *states, const int32_t *const *actions, int32_t autoreset,
                           uint64_t seed, uint64_t rng_counter, const msat_step_out *outs, void *const *obs,
                           void *stream);
+
+/* obs may be NULL in msat_env_reset / msat_env_step: state-only update, no observation write
+ * (the single-agent SatEnv observes the GNN input instead, src/envs/sat_env.py:120-166). */
+
+/* Behavioural-cloning joint labels: compute_joint_labels_parallel_greedy
+ * (src/runners/behavioral_cloning.py:54-100) for B envs (desc->num_envs) given explicit
+ * problem_idx (B,) into the packed pool lits and assignments (B,V) u8: per agent, the first
+ * local var index whose single flip lowers the unsatisfied-clause count the most, if that
+ * delta < tau, else the no-op index M.  labels (B,A) int32; deltas (B,V) int32 (nullable) =
+ * unsat(x with v flipped) - unsat(x). */
+int msat_bc_greedy_labels(const msat_env_desc *desc, const uint16_t *lits, const int32_t *problem_idx,
+                          const uint8_t *assign, float tau, int32_t *labels, int32_t *deltas, void *stream);
+
+/* Single-agent SatEnv clause features [is_sat, is_unsat, 1] (B,C,3) (src/envs/sat_env.py:143-160). */
+int msat_clause_sat_features(const msat_env_desc *desc, const msat_env_state *state,
+                             float *clause_features, void *stream);
 
 /* SATEnv.get_obs (env:345-398) of the current state, without changing it. */
 int msat_env_obs(const msat_env_desc *desc, const msat_pool *pool,

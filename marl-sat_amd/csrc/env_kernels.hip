@@ -329,7 +329,13 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
                 const int n = agent_size(p, i);
                 if (a >= n) continue;  // no-op index (and every action of a var-less agent)
                 int s = a;
-                if (s < 0) s = max(s + p.M, 0);  // jnp index normalisation + clamp
+                if (s < 0) {
+                    s += p.M;  // jnp negative-index normalisation
+                    if (s < 0) {
+                        if (p.reward_mode == MSAT_REWARD_SINGLE_DELTA) continue;  // x.at[a] scatter drops it
+                        s = 0;                                                   // agent_vars gather clamps
+                    }
+                }
                 if (s < n) {
                     const int v = agent_lo(p, i) + s;
                     atomicXor(&l.x[v >> 5], 1u << (v & 31));
@@ -354,9 +360,17 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         if (MODE != kModeObs && tid == 0) {
             const int u_new = l.red[0];
             const bool solved = (u_new == 0);
-            const bool done = solved || (step0 + 1 >= p.max_steps);
+            // single-agent SatEnv (sat_env.py:106) tests the pre-increment step
+            const bool done = solved || (p.reward_mode == MSAT_REWARD_SINGLE_DELTA ? step0 >= p.max_steps
+                                                                                   : step0 + 1 >= p.max_steps);
             float r;
-            if (p.reward_mode == MSAT_REWARD_PBRS) {
+            if (p.reward_mode == MSAT_REWARD_SINGLE_DELTA) {
+                // sat_env.py:86-101, f32 in the reference's order: ((u_prev - u_new) * 10 + bonus) + (-0.005)
+                const float up = __fdiv_rn((float)u_old, (float)p.C), un = __fdiv_rn((float)u_new, (float)p.C);
+                r = __fmul_rn(__fsub_rn(up, un), 10.0f);
+                r = __fadd_rn(r, solved ? p.r_sat : 0.0f);
+                r = __fadd_rn(r, -0.005f);
+            } else if (p.reward_mode == MSAT_REWARD_PBRS) {
                 const float pot_new = (float)(-u_new), pot_old = (float)(-u_old);
                 const float r_pbrs = __fsub_rn(__fmul_rn(p.gamma, pot_new), pot_old);
                 const float r_cl = __fmul_rn((float)l.red[1], p.r_clause);
@@ -415,7 +429,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
     }
     if (MODE != kModeObs)
         for (int v = tid; v < p.V; v += kThreads) xg[v] = (uint8_t)bit(l.x, v);
-    if ((p.ablate & 3) == 2) return;
+    if ((p.ablate & 3) == 2 || obs == nullptr) return;  // NULL obs: state-only step (single-agent SatEnv)
     // ---- stage the instance's agent tables (built once per pool instance) --
     {
         const uint32_t *rel_g = pool.rel + (size_t)pidx * p.A * p.WC;
@@ -637,6 +651,85 @@ static_var_features_kernel(const uint16_t *__restrict__ pool, int V, int C, floa
     }
 }
 
+// ------------------------------------------------------- BC joint labels ----
+// behavioral_cloning.py:54-100 (compute_joint_labels_parallel_greedy) for a batch: per env,
+// delta[v] = unsat(x with v flipped) - unsat(x) for every var (one pass over the clauses: a clause
+// changes status under the flip of v iff re-evaluating it with v flipped differs; duplicate vars in
+// a clause are counted once, literal 0 stays false), then per agent the first local index with the
+// smallest delta among strictly improving flips; label = that index if best < tau, else M (no-op).
+__global__ void __launch_bounds__(kThreads)
+bc_labels_kernel(EnvParams p, const uint16_t *__restrict__ lits, const int32_t *__restrict__ pidx,
+                 const uint8_t *__restrict__ assign, float tau, int32_t *__restrict__ labels,
+                 int32_t *__restrict__ deltas) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *xb = smem;                               // [WV] assignment bits
+    int *dl = reinterpret_cast<int *>(smem + p.WV);    // [V]
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const uint8_t *xg = assign + (size_t)b * p.V;
+    for (int t = tid; t < p.WV; t += kThreads) {
+        uint32_t w = 0;
+        for (int k = 0; k < 32; ++k) {
+            const int v = 32 * t + k;
+            if (v < p.V && (xg[v] & 1u)) w |= 1u << k;
+        }
+        xb[t] = w;
+    }
+    for (int v = tid; v < p.V; v += kThreads) dl[v] = 0;
+    __syncthreads();
+    const uint64_t *prow = reinterpret_cast<const uint64_t *>(lits) + (size_t)pidx[b] * p.C;
+    for (int c = tid; c < p.C; c += kThreads) {
+        const uint64_t w = prow[c];
+        int var[MSAT_LIT_SLOTS];
+        bool val[MSAT_LIT_SLOTS];
+        bool old = false;
+#pragma unroll
+        for (int j = 0; j < MSAT_LIT_SLOTS; ++j) {
+            const uint32_t code = (uint32_t)(w >> (16 * j)) & 0xFFFFu;
+            var[j] = code >= MSAT_LIT_ABSENT ? -1 : (int)(code >> 1);  // NULL / ABSENT: no variable, false
+            val[j] = var[j] >= 0 && ((((xb[var[j] >> 5] >> (var[j] & 31)) & 1u) ^ (code & 1u)) != 0u);
+            old = old || val[j];
+        }
+#pragma unroll
+        for (int j = 0; j < MSAT_LIT_SLOTS; ++j) {
+            const int v = var[j];
+            if (v < 0) continue;
+            bool dup = false;
+#pragma unroll
+            for (int k = 0; k < j; ++k) dup = dup || (var[k] == v);
+            if (dup) continue;
+            bool nw = false;
+#pragma unroll
+            for (int k = 0; k < MSAT_LIT_SLOTS; ++k) nw = nw || (var[k] >= 0 && (val[k] != (var[k] == v)));
+            if (nw != old) atomicAdd(&dl[v], old ? 1 : -1);
+        }
+    }
+    __syncthreads();
+    if (deltas)
+        for (int v = tid; v < p.V; v += kThreads) deltas[(size_t)b * p.V + v] = dl[v];
+    for (int i = tid; i < p.A; i += kThreads) {
+        int best = 0, bi = p.M;
+        const int lo = agent_lo(p, i), n = agent_size(p, i);
+        for (int j = 0; j < n; ++j) {
+            const int d = dl[lo + j];
+            if (d < best) {
+                best = d;
+                bi = j;
+            }
+        }
+        labels[(size_t)b * p.A + i] = ((float)best < tau) ? bi : p.M;
+    }
+}
+
+// single-agent SatEnv clause features [is_sat, is_unsat, 1] (sat_env.py:143-160)
+__global__ void clause_sat_features_kernel(int BC, const uint8_t *__restrict__ sat, float *__restrict__ f) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= BC) return;
+    const float s = (float)sat[t];
+    f[3 * (size_t)t + 0] = s;
+    f[3 * (size_t)t + 1] = 1.0f - s;
+    f[3 * (size_t)t + 2] = 1.0f;
+}
+
 // ------------------------------------------------------------- host glue ----
 
 static int make_params(const msat_env_desc *d, EnvParams *p) {
@@ -647,7 +740,7 @@ static int make_params(const msat_env_desc *d, EnvParams *p) {
     MSAT_REQUIRE(d->clause_width >= 1 && d->clause_width <= 3, "clause_width %d out of [1,3]", d->clause_width);
     MSAT_REQUIRE(d->num_agents >= 1 && d->num_agents <= 1000, "num_agents %d out of [1,1000]", d->num_agents);
     MSAT_REQUIRE(d->action_mode == 0 || d->action_mode == 1, "action_mode %d", d->action_mode);
-    MSAT_REQUIRE(d->reward_mode == 0 || d->reward_mode == 1, "reward_mode %d", d->reward_mode);
+    MSAT_REQUIRE(d->reward_mode >= 0 && d->reward_mode <= 2, "reward_mode %d", d->reward_mode);
     MSAT_REQUIRE(d->obs_dtype == MSAT_OBS_I32 || d->obs_dtype == MSAT_OBS_I8, "obs_dtype %d", d->obs_dtype);
     MSAT_REQUIRE(d->num_problems >= 1, "num_problems %d < 1", d->num_problems);
     p->B = d->num_envs;
@@ -802,7 +895,6 @@ extern "C" int msat_env_reset(const msat_env_desc *desc, const msat_pool *pool,
     int rc = make_params(desc, &p);
     if (rc) return rc;
     if ((rc = check_state(state)) || (rc = check_pool(pool))) return rc;
-    MSAT_REQUIRE(obs, "NULL obs");
     return launch_env<kModeReset>(p, desc, pool, state, nullptr, reset_mask, new_problem_idx, new_assign,
                                   seed, rng_counter, nullptr, obs, (hipStream_t)stream);
 }
@@ -815,7 +907,7 @@ extern "C" int msat_env_step(const msat_env_desc *desc, const msat_pool *pool,
     int rc = make_params(desc, &p);
     if (rc) return rc;
     if ((rc = check_state(state)) || (rc = check_pool(pool))) return rc;
-    MSAT_REQUIRE(obs && actions, "NULL obs/actions");
+    MSAT_REQUIRE(actions, "NULL actions");
     MSAT_REQUIRE(out && out->reward && out->done && out->solved, "NULL step outputs");
     if (autoreset)
         return launch_env<kModeStepAutoReset>(p, desc, pool, state, actions, nullptr, new_problem_idx,
@@ -861,6 +953,34 @@ extern "C" int msat_clause_features(const msat_env_desc *desc, const msat_env_st
     hipLaunchKernelGGL(clause_features_kernel, dim3((BC + 255) / 256), dim3(256), 0, (hipStream_t)stream, BC,
                        state->clause_sat, state->clause_ntrue, clause_features);
     return check_launch("clause_features_kernel");
+}
+
+extern "C" int msat_bc_greedy_labels(const msat_env_desc *desc, const uint16_t *lits, const int32_t *problem_idx,
+                                     const uint8_t *assign, float tau, int32_t *labels, int32_t *deltas,
+                                     void *stream) {
+    EnvParams p;
+    int rc = make_params(desc, &p);
+    if (rc) return rc;
+    if (p.B == 0) return MSAT_OK;
+    MSAT_REQUIRE(lits && problem_idx && assign && labels, "NULL pointer");
+    const size_t lds = ((size_t)p.WV + p.V) * 4;
+    MSAT_REQUIRE(lds <= 160 * 1024, "bc labels need %zu B of LDS", lds);
+    hipLaunchKernelGGL(bc_labels_kernel, dim3(p.B), dim3(kThreads), lds, (hipStream_t)stream, p, lits, problem_idx,
+                       assign, tau, labels, deltas);
+    return check_launch("bc_labels_kernel");
+}
+
+extern "C" int msat_clause_sat_features(const msat_env_desc *desc, const msat_env_state *state,
+                                        float *clause_features, void *stream) {
+    EnvParams p;
+    int rc = make_params(desc, &p);
+    if (rc) return rc;
+    MSAT_REQUIRE(state && state->clause_sat && clause_features, "NULL pointer");
+    const int BC = p.B * p.C;
+    if (BC == 0) return MSAT_OK;
+    hipLaunchKernelGGL(clause_sat_features_kernel, dim3((BC + 255) / 256), dim3(256), 0, (hipStream_t)stream, BC,
+                       state->clause_sat, clause_features);
+    return check_launch("clause_sat_features_kernel");
 }
 
 extern "C" int msat_static_var_features(const uint16_t *pool, int32_t num_problems, int32_t num_vars,

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("MARLSAT_LIB", os.path.join(_HERE, "lib", "libmarlsat.
 
 OBS_I32, OBS_I8 = 0, 1
 MAX_GROUPS = 8  # MSAT_MAX_GROUPS
-REWARD_SPARSE, REWARD_PBRS = 0, 1
+REWARD_SPARSE, REWARD_PBRS, REWARD_SINGLE_DELTA = 0, 1, 2
 
 
 class EnvDesc(ctypes.Structure):
@@ -96,6 +96,8 @@ def _load():
         "msat_env_obs": (c_int32, [POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, P]),
         "msat_env_masks": (c_int32, [POINTER(EnvDesc), POINTER(PoolC), POINTER(EnvStateC), P, P, P, P]),
         "msat_clause_features": (c_int32, [POINTER(EnvDesc), POINTER(EnvStateC), P, P]),
+        "msat_clause_sat_features": (c_int32, [POINTER(EnvDesc), POINTER(EnvStateC), P, P]),
+        "msat_bc_greedy_labels": (c_int32, [POINTER(EnvDesc), P, P, P, c_float, P, P, P]),
         "msat_static_var_features": (c_int32, [P, c_int32, c_int32, c_int32, P, P]),
         "msat_gae_workspace_bytes": (c_size_t, [c_int32, c_int32]),
         "msat_gae": (
@@ -186,6 +188,8 @@ EXPORTED = (
     "msat_env_reset",
     "msat_env_step",
     "msat_env_reset_grouped",
+    "msat_clause_sat_features",
+    "msat_bc_greedy_labels",
     "msat_env_step_grouped",
     "msat_env_obs",
     "msat_env_masks",

@@ -296,12 +296,14 @@ class SATEnv:
 
     # ------------------------------------------------------------ reset ----
     def reset_from_pool(self, pool: ProblemPool, num_envs: int, key=None, *, problem_idx=None, assignments=None,
-                        state: Optional[SATState] = None, reset_mask=None, obs: Optional[torch.Tensor] = None):
-        """Reset (all or masked) envs onto pool rows; returns (obs (B,A,D), state). In place when state given."""
+                        state: Optional[SATState] = None, reset_mask=None, obs: Optional[torch.Tensor] = None,
+                        with_obs: bool = True):
+        """Reset (all or masked) envs onto pool rows; returns (obs (B,A,D), state). In place when state given.
+        with_obs=False: state only (obs is None, nothing written)."""
         k = as_key(key)
         if state is None:
             state = self.alloc_state(num_envs, pool)
-        if obs is None:
+        if obs is None and with_obs:
             obs = self.alloc_obs(num_envs)
         pidx = None
         if problem_idx is not None:
@@ -319,7 +321,7 @@ class SATEnv:
         if reset_mask is not None:
             m = torch.as_tensor(reset_mask, device=self.device).to(torch.uint8).contiguous()
         _lib.check(_lib.lib.msat_env_reset(self._desc(num_envs, pool), pool.c(self), state._c(), _lib.ptr(m),
-                                           _lib.ptr(pidx), _lib.ptr(x), k.seed, k.counter, obs.data_ptr(),
+                                           _lib.ptr(pidx), _lib.ptr(x), k.seed, k.counter, _lib.ptr(obs),
                                            _lib.stream_ptr(self.device)),
                    "msat_env_reset")
         state._masks = None
@@ -345,11 +347,13 @@ class SATEnv:
         }
 
     def step_raw(self, state: SATState, actions: torch.Tensor, *, autoreset: bool = False, key=None,
-                 problem_idx=None, assignments=None, obs: Optional[torch.Tensor] = None, out=None):
-        """In-place batched step on device tensors; returns (obs, out-dict). The hot-loop entry point."""
+                 problem_idx=None, assignments=None, obs: Optional[torch.Tensor] = None, out=None,
+                 with_obs: bool = True):
+        """In-place batched step on device tensors; returns (obs, out-dict). The hot-loop entry point.
+        with_obs=False: no observation write (obs is None)."""
         B = state.num_envs
         a = self._actions_tensor(actions, B)
-        if obs is None:
+        if obs is None and with_obs:
             obs = self.alloc_obs(B)
         if out is None:
             out = self._step_out(B)
@@ -360,7 +364,7 @@ class SATEnv:
                            out["num_unsatisfied"].data_ptr(), out["episode_step"].data_ptr())
         _lib.check(_lib.lib.msat_env_step(self._desc(B, state.pool), state.pool.c(self), state._c(),
                                           a.data_ptr(), 1 if autoreset else 0, _lib.ptr(pidx), _lib.ptr(x), k.seed,
-                                          k.counter, so, obs.data_ptr(), _lib.stream_ptr(self.device)),
+                                          k.counter, so, _lib.ptr(obs), _lib.stream_ptr(self.device)),
                    "msat_env_step")
         state._masks = None
         return obs, out
