@@ -133,7 +133,8 @@ def mappo_bench(args, rank, world, dist):
     cfg = dict(NUM_ENVS=B, NUM_STEPS=T, UPDATE_EPOCHS=E, MINIBATCH_SIZE=B * T // 4, NUM_UPDATES=1000,
                LEARNING_RATE=3e-4, ANNEAL_LR=True, LR_START_FACTOR=1.0, LR_END_FLOOR=1e-5, GAMMA=0.99,
                GAE_LAMBDA=0.95, CLIP_EPS=0.2, ENT_COEF=0.01, VF_COEF=0.5, VF_CLIP=0.2,
-               GNN_HIDDEN_DIM=H, GNN_NUM_MESSAGE_PASSING_STEPS=L, action_mode=0)
+               GNN_HIDDEN_DIM=H, GNN_NUM_MESSAGE_PASSING_STEPS=L, action_mode=0,
+               MICROBATCH_BYTES=args.mappo_micro_gb * 1e9)
     env = SATEnv(V, C, max_steps=512, vars_per_agent=vpa)
     pool = env.make_pool(generate_problem_pool(V, C, args.pool, size_id=size_id))
     net = GNNActorCritic(H, L, env.num_agents, env.max_vars_per_agent, 0, V, device=env.device, seed=0)
@@ -188,6 +189,7 @@ def mappo_bench(args, rank, world, dist):
                      "note": "2*M*N*K of every fp32 GEMM issued in the cycle / cycle wall time (rank max)"},
         "dtype": "f32",
         "solve_rate": met["solve_rate"],
+        "peak_hbm_gb": torch.cuda.max_memory_allocated() / 1e9,
     }
 
 
@@ -293,6 +295,7 @@ def main():
     ap.add_argument("--mappo-workload", default="uf50-218", choices=sorted(WORKLOADS))
     ap.add_argument("--mappo-envs", type=int, default=1024, help="envs per GPU in the MAPPO leg")
     ap.add_argument("--mappo-T", type=int, default=32, help="NUM_STEPS of the MAPPO leg (0: skip the leg)")
+    ap.add_argument("--mappo-micro-gb", type=float, default=160.0, help="activation budget per PPO micro-batch")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
