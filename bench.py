@@ -117,6 +117,56 @@ def load_pmc_traffic(workload: str):
 
 
 # ------------------------------------------------------------------ MAPPO ----
+def mappo_cpu_baseline(workload: str, budget_s: float = 10.0, batch: int = 8):
+    """PPO minibatch forward + backward of the reference network restated in torch (oracle/net.py:
+    dense masked per-agent encoders, as the reference computes them), float32, all host cores
+    (<= 16), on the MAPPO leg's instance size: samples/s over ~budget_s."""
+    import numpy as np
+    import torch
+
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+    from oracle import net as onet
+    from oracle.sat_env import OracleSATEnv
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, int(os.environ.get("MARLSAT_CPU_BASELINE_CORES", 16))))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    try:
+        V, C, vpa, _, size_id = WORKLOADS[workload]
+        pool = generate_problem_pool(V, C, batch, size_id=size_id)
+        ora = OracleSATEnv(V, C, 512, vars_per_agent=vpa)
+        A, M = ora.num_agents, ora.max_vars_per_agent
+        rng = np.random.default_rng(0)
+        x = rng.integers(0, 2, (batch, V)).astype(np.int32)
+        _, st = ora.reset(pool, x)
+        Ap, An = onet.dense_graph(pool, V)
+        f32 = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32)
+        mb = {"svf": f32(ora.static_var_features(pool)), "x": f32(x), "cf": f32(ora.clause_features(st)),
+              "A_pos": Ap.float(), "A_neg": An.float(), "action": torch.from_numpy(rng.integers(0, M + 1, (batch, A))),
+              "log_prob": f32(rng.normal(-1.5, 0.3, (batch, A))), "value": f32(rng.normal(0, 0.5, batch)),
+              "targets": f32(rng.normal(0, 1, batch)), "gae": f32(rng.normal(0, 1, batch))}
+        P = onet.init_params(onet.param_shapes(128, 16, A, M, 0), seed=0, dtype=torch.float32)
+        av, am = torch.from_numpy(ora.agent_vars.astype(np.int64)), torch.from_numpy(ora.action_mask)
+        cfg = {"CLIP_EPS": 0.2, "VF_CLIP": 0.2, "ENT_COEF": 0.01, "VF_COEF": 0.5}
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            Pk = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+            total, _, _, _ = onet.ppo_loss(Pk, 16, mb, cfg, av, am, 0)
+            total.backward()
+            n += batch
+        wall = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": n / wall, "unit": "PPO samples/s (minibatch forward + backward)", "cores": cores,
+            "kind": "port",
+            "sample": f"oracle/net.py ppo_loss + autograd (reference GNN_ActorCritic restated: dense masked per-agent "
+                      f"encoders), float32, {workload}, H=128, L=16, minibatches of {batch}, {n} samples in {wall:.1f} s"}
+
+
 def mappo_bench(args, rank, world, dist):
     """One timed MAPPO train cycle (after one warm-up cycle) on the stated config."""
     import torch
@@ -179,6 +229,7 @@ def mappo_bench(args, rank, world, dist):
         "s_per_update": elapsed,
         "adam_steps_per_s": E * n_mb / elapsed,
         "samples_per_s": world * B * T / elapsed,
+        "ppo_samples_per_s": world * E * B * T / (phases[2] * 1e-3),
         "phase_ms": dict(zip(("rollout", "gae", "ppo_update", "metrics"), phases)),
         "config": {"workload": args.mappo_workload, "num_vars": V, "num_clauses": C, "num_agents": env.num_agents,
                    "envs_per_gpu": B, "NUM_STEPS": T, "UPDATE_EPOCHS": E, "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"],
@@ -338,6 +389,8 @@ def main():
 
     r = env_leg(args, rank, world, dist)
     mappo = mappo_bench(args, rank, world, dist) if args.mappo_T > 0 else None
+    if mappo is not None and rank == 0 and world == 1 and args.cpu_budget > 0:
+        mappo["cpu_baseline"] = mappo_cpu_baseline(args.mappo_workload, budget_s=min(10.0, args.cpu_budget))
 
     if rank == 0:
         B, K, elapsed, kern_ms = sum(r["sizes"]), r["K"], r["elapsed"], r["kern_ms"]
