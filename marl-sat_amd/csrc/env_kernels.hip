@@ -814,6 +814,8 @@ static int launch_groups(int G, const msat_env_desc *descs, const msat_pool *poo
         EnvGroup &e = gs.g[g];
         int rc = make_params(&descs[g], &e.p);
         if (rc) return rc;
+        e.begin = total;
+        if (e.p.B == 0) continue;  // empty class: no blocks (its pointers may be NULL)
         if ((rc = check_state(&states[g])) || (rc = check_pool(&pools[g]))) return rc;
         MSAT_REQUIRE(descs[g].obs_dtype == descs[0].obs_dtype, "groups must share obs_dtype");
         MSAT_REQUIRE(obs[g], "NULL obs for group %d", g);
@@ -825,7 +827,6 @@ static int launch_groups(int G, const msat_env_desc *descs, const msat_pool *poo
             e.out = outs[g];
         }
         e.obs = obs[g];
-        e.begin = total;
         total += e.p.B;
         lds = std::max(lds, env_lds_words(e.p) * 4);
         gs.ablate = e.p.ablate;
@@ -894,6 +895,7 @@ extern "C" int msat_env_reset(const msat_env_desc *desc, const msat_pool *pool,
     EnvParams p;
     int rc = make_params(desc, &p);
     if (rc) return rc;
+    if (p.B == 0) return MSAT_OK;
     if ((rc = check_state(state)) || (rc = check_pool(pool))) return rc;
     return launch_env<kModeReset>(p, desc, pool, state, nullptr, reset_mask, new_problem_idx, new_assign,
                                   seed, rng_counter, nullptr, obs, (hipStream_t)stream);
@@ -906,6 +908,7 @@ extern "C" int msat_env_step(const msat_env_desc *desc, const msat_pool *pool,
     EnvParams p;
     int rc = make_params(desc, &p);
     if (rc) return rc;
+    if (p.B == 0) return MSAT_OK;
     if ((rc = check_state(state)) || (rc = check_pool(pool))) return rc;
     MSAT_REQUIRE(actions, "NULL actions");
     MSAT_REQUIRE(out && out->reward && out->done && out->solved, "NULL step outputs");
@@ -921,6 +924,7 @@ extern "C" int msat_env_obs(const msat_env_desc *desc, const msat_pool *pool, co
     EnvParams p;
     int rc = make_params(desc, &p);
     if (rc) return rc;
+    if (p.B == 0) return MSAT_OK;
     if ((rc = check_state(state)) || (rc = check_pool(pool))) return rc;
     MSAT_REQUIRE(obs, "NULL obs");
     return launch_env<kModeObs>(p, desc, pool, state, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, obs,

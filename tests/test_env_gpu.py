@@ -306,3 +306,55 @@ def test_grouped_mixed_batch_equals_per_class(obs_dtype):
                       "problem_idx"):
                 assert torch.equal(getattr(states[g], f), getattr(st, f)), (ctx, f)
     assert any(bool(o["done"].any()) for o in outs)
+
+
+def test_smallest_env_v1_c1():
+    """V=1, C=1, one agent: every code path with single-word bit images."""
+    env, ora = _mk(1, 1, 1, max_steps=2)
+    pool = np.array([[[1, 0, -1]], [[-1, -1, 1]], [[1, 1, 1]]], dtype=np.int32)  # literal 0, x or -x, duplicates
+    B = 6
+    pidx = np.array([0, 1, 2, 0, 1, 2], np.int32)
+    x = np.array([[0], [1], [0], [1], [0], [1]], np.uint8)
+    obs, st = env.reset_from_pool(env.make_pool(pool), B, problem_idx=pidx, assignments=x)
+    oobs, ost = ora.reset(pool[pidx], x.astype(np.int32))
+    np.testing.assert_array_equal(_np(obs), oobs)
+    _check_state(env, st, ost)
+    for t in range(3):
+        a = np.array([[0], [1], [0], [1], [-1], [5]], np.int32)
+        npidx = np.array([2, 2, 1, 1, 0, 0], np.int32)
+        nx = np.array([[1], [0], [1], [0], [1], [0]], np.uint8)
+        obs, out = env.step_raw(st, torch.from_numpy(a).cuda(), autoreset=True, problem_idx=npidx, assignments=nx)
+        oobs, ost, r, d, _ = ora.step_autoreset(ost, a, pool[npidx], nx.astype(np.int32))
+        np.testing.assert_array_equal(_np(obs), oobs, err_msg=f"t={t}")
+        _check_state(env, st, ost, f"t={t}")
+        np.testing.assert_array_equal(_np(out["reward"]), r)
+
+
+def test_grouped_eight_classes_with_empty_ones():
+    """MSAT_MAX_GROUPS classes, two of them empty (middle and last): the block -> class map skips them."""
+    from marlsat.envs.mixed import MixedSATEnv, group_seed
+    from marlsat.random import Key
+
+    specs = [(20, 91, 10, 5), (12, 40, 4, 0), (23, 97, 10, 9), (30, 120, 7, 3), (16, 60, 5, 1), (50, 218, 10, 4),
+             (8, 30, 3, 2), (40, 170, 9, 0)]
+    classes, solo, pools = [], [], []
+    for i, (V, C, vpa, B) in enumerate(specs):
+        classes.append(_mk(V, C, vpa, max_steps=2)[0])
+        solo.append(_mk(V, C, vpa, max_steps=2)[0])
+        pools.append(_pool(V, C, 3, seed0=50 * i))
+    mixed = MixedSATEnv(classes)
+    key = Key(77, 1)
+    obs, states = mixed.reset([c.make_pool(p) for c, p in zip(classes, pools)], [s[3] for s in specs], key)
+    outs = mixed.alloc_outs(states)
+    step = mixed.stepper(states, obs, outs, autoreset=True, seed=99)
+    ref = [e.reset_from_pool(e.make_pool(p), s[3], Key(77 ^ group_seed(g), 1)) for g, (e, p, s)
+           in enumerate(zip(solo, pools, specs))]
+    rng = np.random.default_rng(1)
+    for t in range(3):
+        acts = [torch.from_numpy(_random_actions(rng, c, s[3])).cuda() for c, s in zip(classes, specs)]
+        step(acts, 5 + t)
+        for g, (e, (o, st)) in enumerate(zip(solo, ref)):
+            o2, out2 = e.step_raw(st, acts[g], autoreset=True, key=Key(99 ^ group_seed(g), 5 + t), obs=o)
+            assert torch.equal(obs[g], o2), (g, t)
+            assert torch.equal(states[g].variable_assignments, st.variable_assignments), (g, t)
+            assert torch.equal(outs[g]["reward"], out2["reward"]), (g, t)
