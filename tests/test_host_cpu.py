@@ -110,3 +110,29 @@ def test_config_overrides_and_solution_line(tmp_path):
     m = re.search(r"Problem: ([\w.-]+), Solved: True, .* Solution: ([01]+)", line.strip())  # verify_solutions.py:107
     assert m.groups() == ("uf20-01.cnf", "101")
     assert solution_line("b.cnf", False, 0, None) == "Problem: b.cnf, Solved: False\n"
+
+
+@pytest.mark.parametrize("cfg", [
+    {"ANNEAL_LR": True, "NUM_UPDATES": 300, "LEARNING_RATE": 1e-4, "LR_START_FACTOR": 1.0, "LR_END_FLOOR": 2e-5},
+    {"ANNEAL_LR": True, "NUM_UPDATES": 7, "LEARNING_RATE": 3e-3, "LR_START_FACTOR": 0.5, "LR_END_FLOOR": 1e-5},
+    {"ANNEAL_LR": False, "LEARNING_RATE": 5e-4, "NUM_UPDATES": 10},
+])
+def test_learning_rate_schedule_matches_oracle(cfg):
+    from marlsat.learners.mappo_gnn_sat_learner import learning_rate_at
+    from oracle import mappo as om
+
+    for count in list(range(0, 20)) + [cfg["NUM_UPDATES"] - 1, cfg["NUM_UPDATES"], 10 * cfg["NUM_UPDATES"]]:
+        assert learning_rate_at(count, cfg) == pytest.approx(om.learning_rate(count, cfg), rel=1e-12, abs=0)
+
+
+@pytest.mark.parametrize("cfg", [
+    {"ANNEAL_ENT": True, "NUM_UPDATES": 300, "ENT_COEF": 0.01, "ENT_COEF_END": 0.001, "ANNEAL_ENT_FRAC": 0.333},
+    {"ANNEAL_ENT": True, "NUM_UPDATES": 12, "ENT_COEF": 0.05},
+    {"ANNEAL_ENT": False, "NUM_UPDATES": 12, "ENT_COEF": 0.005},
+])
+def test_entropy_schedule_matches_oracle(cfg):
+    from marlsat.learners.mappo_gnn_sat_learner import ent_coef_at
+    from oracle import mappo as om
+
+    for u in range(0, cfg["NUM_UPDATES"] + 3):
+        assert ent_coef_at(u, cfg) == pytest.approx(om.ent_coef(u, cfg), rel=1e-12, abs=1e-15)

@@ -114,4 +114,20 @@ def test_train_cycle_matches_oracle_replay(mode):
         diff = np.linalg.norm(final[kk] - ref)
         assert diff <= 0.05 * upd + 1e-7, (kk, diff, upd)
         assert np.abs(final[kk] - ref).max() <= 2.0 * lr_sum + 1e-6, kk
-    assert 0.0 <= metrics["solve_rate"] <= 1.0 and np.isfinite(metrics["explained_variance"])
+    # cycle metrics (learner:661-719) from the recorded transitions + the oracle critic on the final params
+    done = tr["done"].astype(bool)
+    solved = tr["solved"].astype(bool) & done
+    n_done, n_solved = done.sum(), solved.sum()
+    exp = {"mean_episodic_return": tr["reward"].astype(np.float64).sum(0).mean(),
+           "solve_rate": n_solved / max(n_done, 1.0),
+           "avg_unsatisfied_clauses": (tr["num_unsatisfied"] * done).sum() / max(n_done, 1.0),
+           "avg_steps_to_solve": (tr["episode_step"] * solved).sum() / max(n_solved, 1.0)}
+    for k, v in exp.items():
+        np.testing.assert_allclose(metrics[k], v, rtol=1e-12, atol=1e-12, err_msg=k)
+    Pf = {k: torch.tensor(v, dtype=torch.float64) for k, v in final.items()}
+    with torch.no_grad():
+        vnew = onet.critic(Pf, 2, bt["svf"], bt["x"], bt["cf"], bt["A_pos"], bt["A_neg"]).numpy()
+    tg = learner.targets.cpu().numpy().reshape(-1).astype(np.float64)
+    ev = 1.0 - np.var(tg - vnew) / max(np.var(tg), 1e-8)
+    np.testing.assert_allclose(metrics["explained_variance"], ev, rtol=1e-4, atol=1e-5)
+    assert metrics["current_ent_coef"] == cfg["ENT_COEF"]
