@@ -132,7 +132,7 @@ __device__ __forceinline__ void mfma_slab(const float *Ai, const float *Bi, int 
 
 // C[M,N] (+)= A[M,K] @ op(B) + bias; A k-major; B o-major (B[K][N]) or k-major (B[N][K]).
 template <int D, bool BK>
-__global__ void __launch_bounds__(kG2T)
+__global__ void __launch_bounds__(kG2T, D == 16 ? 4 : 2)
 gemm2_kernel(const float *__restrict__ A, int lda, const float *__restrict__ B, int ldb, float *__restrict__ C,
              int ldc, const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
     constexpr int IMG = kG2M * D;
@@ -224,7 +224,7 @@ gemm2_kernel(const float *__restrict__ A, int lda, const float *__restrict__ B, 
 
 // partial[s][k][n] = sum_{m in split s} A[m][k] G[m][n]: both operands o-major over the rows m.
 template <int D>
-__global__ void __launch_bounds__(kG2T)
+__global__ void __launch_bounds__(kG2T, D == 16 ? 4 : 2)
 wgrad2_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G, int ldg, float *__restrict__ part,
               int M, int K, int N, int rows_per_split, int ntn, int tiles) {
     constexpr int IMG = kG2M * D;
