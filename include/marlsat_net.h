@@ -24,7 +24,8 @@ int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ldb, int32_t 
               int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, int32_t accumulate,
               void *stream);
 
-/* W[K,N] (+)= A[M,K]^T @ G[M,N]: split over M, partial slabs reduced in a fixed order. */
+/* W[K,N] (+)= A[M,K]^T @ G[M,N]: split over M, partial slabs reduced in a fixed order.
+ * K <= 8 (feature / degree columns) streams G once instead of running 128-row MFMA tiles. */
 size_t msat_gemm_wgrad_workspace_bytes(int32_t M, int32_t K, int32_t N);
 int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
                     int32_t M, int32_t K, int32_t N, int32_t accumulate, void *workspace, void *stream);
@@ -32,14 +33,17 @@ int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int32_t ldg, fl
 /* ---- graph batch assembly (learner:148-195 features + the agents' local graphs) ----
  * Block per sample: instantiate the per-instance templates (marlsat/learners/graphs.py) at the
  * sample's row bases (sample_bases (S,3) = var row, clause row, incidence starts) and compute the
- * node features from the sample's assignment x (S,V): vfeat (Nv,4) = [x, deg+/C, deg-/C, 0],
- * cfeat (Nc,3) = [is_sat, ntrue/3, 1].  G = 1 (critic graph only) or A+1. */
+ * node features from the sample's assignment x (S,V): vfeat (Nv,8) = [x, deg+/C, deg-/C, 0, n+, n-, 0, 0]
+ * (static var features, then the var row's positive / negative incidence counts in its graph),
+ * cfeat (Nc,3) = [is_sat, ntrue/3, 1], cdeg (Nc,4, nullable) = [n+, n-, 0, 0] positive / negative
+ * literal slots of the clause row.  The counts carry the phi biases through the gather-first
+ * message passing (sum_{edges} (h W + b) = (sum h) W + n b).  G = 1 (critic graph only) or A+1. */
 int msat_assemble_graph_batch(
     int32_t S, int32_t G, int32_t A, int32_t V, int32_t C, const int32_t *inst, const uint8_t *x, const float *svf,
     const uint16_t *pool, const int32_t *sample_bases, const int32_t *t_vgid, const int32_t *t_cgid,
     const int32_t *t_slots, const int32_t *t_ptr, const int32_t *t_inc, const int32_t *voff, const int32_t *coff,
     const int32_t *eoff, const int32_t *poff, const int32_t *gv, const int32_t *gc, float *vfeat, float *cfeat,
-    int32_t *slots, int32_t *ptr, int32_t *inc, int32_t *g_vbase, int32_t *g_nv, int32_t *g_cbase, int32_t *g_nc,
+    float *cdeg, int32_t *slots, int32_t *ptr, int32_t *inc, int32_t *g_vbase, int32_t *g_nv, int32_t *g_cbase, int32_t *g_nc,
     int32_t Nv, int32_t nnz, void *stream);
 
 /* ---- message passing: signed literal gathers (the encoder's A^T M and A M, learner:66-74) ----
@@ -51,6 +55,18 @@ int msat_clause_gather(const float *src, int32_t ld_src, const int32_t *slots, f
                        int32_t num_clause_rows, int32_t H, int32_t accumulate, void *stream);
 int msat_var_gather(const float *src, int32_t ld_src, const int32_t *ptr, const int32_t *inc, float *dst,
                     int32_t ld_dst, int32_t num_var_rows, int32_t H, int32_t accumulate, void *stream);
+/* General forms (16-byte aligned rows, H % 32 == 0):
+ * clause_gather2: positive slots read src_pos rows, negative slots src_neg rows (H wide each);
+ *   merged = 0: dst[c] (+)= [sum_pos src_pos[v] | sum_neg src_neg[v]] (2H wide);
+ *   merged = 1: dst[c] (+)= sum_pos src_pos[v] + sum_neg src_neg[v] (H wide; the transpose of
+ *   var_gather2 with src_pos == src_neg).
+ * var_gather2: dst_pos[v] (+)= sum_pos src_pos[c], dst_neg[v] (+)= sum_neg src_neg[c]. */
+int msat_clause_gather2(const float *src_pos, const float *src_neg, int32_t ld_src, const int32_t *slots, float *dst,
+                        int32_t ld_dst, int32_t num_clause_rows, int32_t H, int32_t merged, int32_t accumulate,
+                        void *stream);
+int msat_var_gather2(const float *src_pos, const float *src_neg, int32_t ld_src, const int32_t *ptr,
+                     const int32_t *inc, float *dst_pos, float *dst_neg, int32_t ld_dst, int32_t num_var_rows,
+                     int32_t H, int32_t accumulate, void *stream);
 
 /* ---- fused flax GRUCell + LayerNorm (learner:69-80) ----
  * Gi = x Wi + bi, Gh = h Wh + [0,0,b_hn] (gates [r|z|n]); out = LN(GRU(h, x)).

@@ -237,6 +237,94 @@ __global__ void wgrad_reduce_kernel(const float *__restrict__ part, int splits, 
     *w = accumulate ? *w + s : s;
 }
 
+// Skinny weight gradient (K <= 8: input features, degree columns): a 128-row MFMA tile
+// would multiply 32x more zeros than data, so this is a streaming reduction over G instead.
+// Block (colblock, split): 16 column float4s x 16 row lanes; each thread keeps K float4
+// accumulators over its rows (fixed order), the 16 row lanes combine through LDS in a fixed
+// order, and part[split][k][n] is reduced by skinny_reduce4_kernel (fixed split order).
+constexpr int kSkinnyK = 8;
+
+__global__ void __launch_bounds__(256)
+wgrad_skinny_kernel(const float *__restrict__ A, int lda, const float4 *__restrict__ G, int ldg4, int M, int K, int N4,
+                    int rows_per, float4 *__restrict__ part) {
+    __shared__ float4 red[16][16];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + tx;
+    const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+    float4 acc[kSkinnyK];
+#pragma unroll
+    for (int k = 0; k < kSkinnyK; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < N4)
+        for (int r = r0 + ty; r < r1; r += 16) {
+            const float4 g = G[(size_t)r * ldg4 + c];
+            const float *a = A + (size_t)r * lda;
+#pragma unroll
+            for (int k = 0; k < kSkinnyK; ++k)
+                if (k < K) {
+                    const float av = a[k];
+                    acc[k].x += av * g.x; acc[k].y += av * g.y; acc[k].z += av * g.z; acc[k].w += av * g.w;
+                }
+        }
+#pragma unroll
+    for (int k = 0; k < kSkinnyK; ++k) {
+        if (k >= K) break;
+        red[ty][tx] = acc[k];
+        __syncthreads();
+        if (ty == 0 && c < N4) {
+            float4 t = red[0][tx];
+            for (int j = 1; j < 16; ++j) {
+                const float4 v = red[j][tx];
+                t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+            }
+            part[((size_t)blockIdx.y * K + k) * N4 + c] = t;
+        }
+        __syncthreads();
+    }
+}
+
+// W[k][n] (+)= sum_s part[s][k][n]: 16 output float4s x 16 split lanes per block, fixed order.
+__global__ void __launch_bounds__(256)
+skinny_reduce4_kernel(const float4 *__restrict__ part, int splits, int KN4, int N4, float4 *__restrict__ W, int ldw4,
+                      int accumulate) {
+    __shared__ float4 red[16][16];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + tx;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < KN4)
+        for (int s = ty; s < splits; s += 16) {
+            const float4 v = part[(size_t)s * KN4 + c];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+    red[ty][tx] = a;
+    __syncthreads();
+    if (ty == 0 && c < KN4) {
+        float4 t = red[0][tx];
+        for (int j = 1; j < 16; ++j) {
+            const float4 v = red[j][tx];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        const int k = c / N4, n4 = c - k * N4;
+        float4 *w = W + (size_t)k * ldw4 + n4;
+        if (accumulate) {
+            const float4 o = *w;
+            t.x = o.x + t.x; t.y = o.y + t.y; t.z = o.z + t.z; t.w = o.w + t.w;
+        }
+        *w = t;
+    }
+}
+
+static int skinny_splits(int M, int N) {
+    const int cb = std::max(1, (N / 4 + 15) / 16);
+    return std::max(1, std::min((M + 63) / 64, std::max(1, 1024 / cb)));
+}
+
+static bool skinny_ok(const float *G, int ldg, const float *W, int ldw, int K, int N) {
+    const char *e = getenv("MARLSAT_WGRAD_SKINNY");  // 0: MFMA tiles for every K (A/B measurements)
+    if (e && e[0] == '0') return false;
+    return K <= kSkinnyK && N % 4 == 0 && ldg % 4 == 0 && ldw % 4 == 0 &&
+           (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0;
+}
+
 // at most 512 workgroups (2 per CU), >= ~1024 rows per split
 static int wgrad_splits(int M, int K, int N) {
     const int tiles = ((K + kTM - 1) / kTM) * ((N + kTN - 1) / kTN);
@@ -279,7 +367,8 @@ extern "C" int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ld
 }
 
 extern "C" size_t msat_gemm_wgrad_workspace_bytes(int32_t M, int32_t K, int32_t N) {
-    return (size_t)wgrad_splits(M, K, N) * K * N * sizeof(float);
+    const size_t sp = std::max(wgrad_splits(M, K, N), K <= kSkinnyK ? skinny_splits(M, N) : 0);
+    return sp * K * N * sizeof(float);
 }
 
 extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
@@ -287,6 +376,17 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
     MSAT_REQUIRE(A && G && W && workspace, "NULL operand");
     MSAT_REQUIRE(M >= 0 && K >= 1 && N >= 1 && lda >= K && ldg >= N && ldw >= N, "bad dims");
     hipStream_t s = (hipStream_t)stream;
+    if (!legacy_gemm() && skinny_ok(G, ldg, W, ldw, K, N) && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0) {
+        const int sp = skinny_splits(M, N), rows_per = (M + sp - 1) / sp, N4 = N / 4;
+        float4 *ws4 = reinterpret_cast<float4 *>(workspace);
+        hipLaunchKernelGGL(wgrad_skinny_kernel, dim3((N4 + 15) / 16, sp), dim3(256), 0, s, A, lda,
+                           reinterpret_cast<const float4 *>(G), ldg / 4, M, K, N4, rows_per, ws4);
+        const int rc = check_launch("wgrad_skinny_kernel");
+        if (rc) return rc;
+        hipLaunchKernelGGL(skinny_reduce4_kernel, dim3((K * N4 + 15) / 16), dim3(256), 0, s, ws4, sp, K * N4, N4,
+                           reinterpret_cast<float4 *>(W), ldw / 4, accumulate);
+        return check_launch("skinny_reduce4_kernel");
+    }
     const int splits = wgrad_splits(M, K, N);
     const int rows = (M + splits - 1) / splits;
     int rc;

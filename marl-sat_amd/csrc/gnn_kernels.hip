@@ -20,18 +20,27 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __ex
 
 // ------------------------------------------------------------------ gathers --
 // slots: (Nc, 3) int32, (var_row << 1) | neg, or -1.  One wave per clause row.
+// Positive literals read src_pos rows, negative ones src_neg rows (both H wide, ld_src).
+//   split  (merged = 0): dst[c] (+)= [sum_{pos} src_pos[v] | sum_{neg} src_neg[v]]   (2H wide)
+//   merged (merged = 1): dst[c] (+)= sum_{pos} src_pos[v] + sum_{neg} src_neg[v]      (H wide)
+// The merged form is the transpose of var_gather with one shared source (the backward of
+// the gather-first var messages); per output the slots are summed in slot order.
 __global__ void __launch_bounds__(kRowThreads)
-clause_gather_kernel(const float *__restrict__ src, int lds_, const int *__restrict__ slots, float *__restrict__ dst,
-                     int ldd, int Nc, int H, int accumulate) {
+clause_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ src_neg, int lds_,
+                     const int *__restrict__ slots, float *__restrict__ dst, int ldd, int Nc, int H, int merged,
+                     int accumulate) {
     const int lane = threadIdx.x & 63;
+    const int W = merged ? H : 2 * H;
     for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < Nc; c += gridDim.x * 4) {
         const int s0 = slots[3 * (size_t)c], s1 = slots[3 * (size_t)c + 1], s2 = slots[3 * (size_t)c + 2];
-        for (int j = lane * 4; j < 2 * H; j += 256) {
-            const int want = j < H ? 0 : 1;  // first half: positive literals, second: negative
+        for (int j = lane * 4; j < W; j += 256) {
+            const int want = j < H ? 0 : 1;  // split: first half positive literals, second negative
+            const int col = j < H ? j : j - H;
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #define MSAT_ADD_SLOT(S)                                                                          \
-    if ((S) >= 0 && ((S)&1) == want) {                                                            \
-        const float4 v = *reinterpret_cast<const float4 *>(src + (size_t)((S) >> 1) * lds_ + j);  \
+    if ((S) >= 0 && (merged || ((S)&1) == want)) {                                                \
+        const float *src = ((S)&1) ? src_neg : src_pos;                                           \
+        const float4 v = *reinterpret_cast<const float4 *>(src + (size_t)((S) >> 1) * lds_ + col); \
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;                                   \
     }
             MSAT_ADD_SLOT(s0) MSAT_ADD_SLOT(s1) MSAT_ADD_SLOT(s2)
@@ -46,23 +55,28 @@ clause_gather_kernel(const float *__restrict__ src, int lds_, const int *__restr
     }
 }
 
-// CSR over var rows: entries (clause_row << 1) | neg.
+// CSR over var rows: entries (clause_row << 1) | neg.  One wave per var row:
+//   dst_pos[v] (+)= sum_{pos entries} src_pos[c],  dst_neg[v] (+)= sum_{neg entries} src_neg[c]
+// (src_pos == src_neg: both halves gather the same H-wide clause rows).
 __global__ void __launch_bounds__(kRowThreads)
-var_gather_kernel(const float *__restrict__ src, int lds_, const int *__restrict__ ptr, const int *__restrict__ inc,
-                  float *__restrict__ dst, int ldd, int Nv, int H, int accumulate) {
+var_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ src_neg, int lds_,
+                  const int *__restrict__ ptr, const int *__restrict__ inc, float *__restrict__ dst_pos,
+                  float *__restrict__ dst_neg, int ldd, int Nv, int H, int accumulate) {
     const int lane = threadIdx.x & 63;
     for (int v = blockIdx.x * 4 + (threadIdx.x >> 6); v < Nv; v += gridDim.x * 4) {
         const int e0 = ptr[v], e1 = ptr[v + 1];
         for (int j = lane * 4; j < 2 * H; j += 256) {
             const int want = j < H ? 0 : 1;
+            const int col = j < H ? j : j - H;
+            const float *src = want ? src_neg : src_pos;
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
             for (int e = e0; e < e1; ++e) {
                 const int s = inc[e];
                 if ((s & 1) != want) continue;
-                const float4 x = *reinterpret_cast<const float4 *>(src + (size_t)(s >> 1) * lds_ + j);
+                const float4 x = *reinterpret_cast<const float4 *>(src + (size_t)(s >> 1) * lds_ + col);
                 acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
             }
-            float4 *d = reinterpret_cast<float4 *>(dst + (size_t)v * ldd + j);
+            float4 *d = reinterpret_cast<float4 *>((want ? dst_neg : dst_pos) + (size_t)v * ldd + col);
             if (accumulate) {
                 const float4 o = *d;
                 acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
@@ -321,7 +335,7 @@ assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__rest
                             const int *__restrict__ t_inc, const int *__restrict__ voff, const int *__restrict__ coff,
                             const int *__restrict__ eoff, const int *__restrict__ poff, const int *__restrict__ gv,
                             const int *__restrict__ gc, float *__restrict__ vfeat, float *__restrict__ cfeat,
-                            int *__restrict__ slots, int *__restrict__ ptr, int *__restrict__ inc,
+                            float *__restrict__ cdeg, int *__restrict__ slots, int *__restrict__ ptr, int *__restrict__ inc,
                             int *__restrict__ g_vbase, int *__restrict__ g_nv, int *__restrict__ g_cbase,
                             int *__restrict__ g_nc, int Nv, int nnz) {
     const int s = blockIdx.x;
@@ -334,13 +348,20 @@ assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__rest
     const uint8_t *xs = x + (size_t)s * V;
     for (int t = threadIdx.x; t < nvr; t += blockDim.x) {
         const int gid = t_vgid[tv0 + t];
-        float *f = vfeat + (size_t)(vr0 + t) * 4;
+        float *f = vfeat + (size_t)(vr0 + t) * 8;
         const float *sv = svf + ((size_t)n * V + gid) * 3;
+        const int pb = t_ptr[tp0 + t], pe = t_ptr[tp0 + t + 1];
+        int nneg = 0;
+        for (int e = pb; e < pe; ++e) nneg += t_inc[te0 + e] & 1;
         f[0] = (float)(xs[gid] & 1u);
         f[1] = sv[0];
         f[2] = sv[1];
         f[3] = sv[2];
-        ptr[vr0 + t] = e0 + t_ptr[tp0 + t];
+        f[4] = (float)(pe - pb - nneg);  // incidences of the var row in its graph: positive, negative
+        f[5] = (float)nneg;
+        f[6] = 0.0f;
+        f[7] = 0.0f;
+        ptr[vr0 + t] = e0 + pb;
     }
     for (int e = threadIdx.x; e < ne; e += blockDim.x) {
         const int ent = t_inc[te0 + e];
@@ -348,10 +369,20 @@ assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__rest
     }
     for (int t = threadIdx.x; t < ncr; t += blockDim.x) {
         const int gcid = t_cgid[tc0 + t];
+        int npos = 0, nneg = 0;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             const int sl = t_slots[(size_t)(tc0 + t) * 3 + j];
             slots[(size_t)(cr0 + t) * 3 + j] = sl < 0 ? -1 : (((vr0 + (sl >> 1)) << 1) | (sl & 1));
+            npos += sl >= 0 && !(sl & 1);
+            nneg += sl >= 0 && (sl & 1);
+        }
+        if (cdeg) {
+            float *d = cdeg + (size_t)(cr0 + t) * 4;
+            d[0] = (float)npos;
+            d[1] = (float)nneg;
+            d[2] = 0.0f;
+            d[3] = 0.0f;
         }
         const uint64_t w = pool[(size_t)n * C + gcid];
         int ntrue = 0;
@@ -433,22 +464,44 @@ extern "C" int msat_colsum(const float *G, int32_t ldg, int32_t M, int32_t N, fl
     return colsum_det(G, ldg, M, N, out, accumulate, workspace, (hipStream_t)stream);
 }
 
+extern "C" int msat_clause_gather2(const float *src_pos, const float *src_neg, int32_t ld_src, const int32_t *slots,
+                                   float *dst, int32_t ld_dst, int32_t num_clause_rows, int32_t H, int32_t merged,
+                                   int32_t accumulate, void *stream) {
+    if (num_clause_rows == 0) return MSAT_OK;
+    MSAT_REQUIRE(src_pos && src_neg && slots && dst && H % 32 == 0 && ld_src % 4 == 0 && ld_dst % 4 == 0 &&
+                     a16(src_pos) && a16(src_neg) && a16(dst) && ld_src >= H && ld_dst >= (merged ? H : 2 * H),
+                 "bad clause_gather args");
+    hipLaunchKernelGGL(clause_gather_kernel, dim3(grid_rows(num_clause_rows)), dim3(kRowThreads), 0,
+                       (hipStream_t)stream, src_pos, src_neg, ld_src, slots, dst, ld_dst, num_clause_rows, H,
+                       merged ? 1 : 0, accumulate);
+    return check_launch("clause_gather_kernel");
+}
+
 extern "C" int msat_clause_gather(const float *src, int32_t ld_src, const int32_t *slots, float *dst, int32_t ld_dst,
                                   int32_t num_clause_rows, int32_t H, int32_t accumulate, void *stream) {
-    MSAT_REQUIRE(src && slots && dst && H % 32 == 0 && ld_src % 4 == 0 && ld_dst % 4 == 0, "bad clause_gather args");
-    if (num_clause_rows == 0) return MSAT_OK;
-    hipLaunchKernelGGL(clause_gather_kernel, dim3(grid_rows(num_clause_rows)), dim3(kRowThreads), 0,
-                       (hipStream_t)stream, src, ld_src, slots, dst, ld_dst, num_clause_rows, H, accumulate);
-    return check_launch("clause_gather_kernel");
+    MSAT_REQUIRE(src || num_clause_rows == 0, "bad clause_gather args");
+    return msat_clause_gather2(src, src ? src + H : nullptr, ld_src, slots, dst, ld_dst, num_clause_rows, H, 0,
+                               accumulate, stream);
+}
+
+extern "C" int msat_var_gather2(const float *src_pos, const float *src_neg, int32_t ld_src, const int32_t *ptr,
+                                const int32_t *inc, float *dst_pos, float *dst_neg, int32_t ld_dst,
+                                int32_t num_var_rows, int32_t H, int32_t accumulate, void *stream) {
+    if (num_var_rows == 0) return MSAT_OK;
+    MSAT_REQUIRE(src_pos && src_neg && ptr && inc && dst_pos && dst_neg && H % 32 == 0 && ld_src % 4 == 0 &&
+                     ld_dst % 4 == 0 && a16(src_pos) && a16(src_neg) && a16(dst_pos) && a16(dst_neg) &&
+                     ld_src >= H && ld_dst >= H,
+                 "bad var_gather args");
+    hipLaunchKernelGGL(var_gather_kernel, dim3(grid_rows(num_var_rows)), dim3(kRowThreads), 0, (hipStream_t)stream,
+                       src_pos, src_neg, ld_src, ptr, inc, dst_pos, dst_neg, ld_dst, num_var_rows, H, accumulate);
+    return check_launch("var_gather_kernel");
 }
 
 extern "C" int msat_var_gather(const float *src, int32_t ld_src, const int32_t *ptr, const int32_t *inc, float *dst,
                                int32_t ld_dst, int32_t num_var_rows, int32_t H, int32_t accumulate, void *stream) {
-    MSAT_REQUIRE(src && ptr && inc && dst && H % 32 == 0 && ld_src % 4 == 0 && ld_dst % 4 == 0, "bad var_gather args");
-    if (num_var_rows == 0) return MSAT_OK;
-    hipLaunchKernelGGL(var_gather_kernel, dim3(grid_rows(num_var_rows)), dim3(kRowThreads), 0, (hipStream_t)stream,
-                       src, ld_src, ptr, inc, dst, ld_dst, num_var_rows, H, accumulate);
-    return check_launch("var_gather_kernel");
+    MSAT_REQUIRE((src && dst) || num_var_rows == 0, "bad var_gather args");
+    return msat_var_gather2(src, src ? src + H : nullptr, ld_src, ptr, inc, dst, dst ? dst + H : nullptr, ld_dst,
+                            num_var_rows, H, accumulate, stream);
 }
 
 extern "C" int msat_gru_ln_fwd(const float *Gi, int32_t ldi, const float *Gh, int32_t ldh, const float *hprev,
@@ -546,7 +599,7 @@ extern "C" int msat_assemble_graph_batch(
     const uint16_t *pool, const int32_t *sample_bases, const int32_t *t_vgid, const int32_t *t_cgid,
     const int32_t *t_slots, const int32_t *t_ptr, const int32_t *t_inc, const int32_t *voff, const int32_t *coff,
     const int32_t *eoff, const int32_t *poff, const int32_t *gv, const int32_t *gc, float *vfeat, float *cfeat,
-    int32_t *slots, int32_t *ptr, int32_t *inc, int32_t *g_vbase, int32_t *g_nv, int32_t *g_cbase, int32_t *g_nc,
+    float *cdeg, int32_t *slots, int32_t *ptr, int32_t *inc, int32_t *g_vbase, int32_t *g_nv, int32_t *g_cbase, int32_t *g_nc,
     int32_t Nv, int32_t nnz, void *stream) {
     MSAT_REQUIRE(inst && x && svf && pool && sample_bases && t_vgid && t_cgid && t_slots && t_ptr && t_inc && voff &&
                      coff && eoff && poff && gv && gc && vfeat && cfeat && slots && ptr && inc && g_vbase && g_nv &&
@@ -556,7 +609,7 @@ extern "C" int msat_assemble_graph_batch(
     if (!S) return MSAT_OK;
     hipLaunchKernelGGL(assemble_graph_batch_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, S, G, A, V, C, inst, x,
                        svf, reinterpret_cast<const uint64_t *>(pool), sample_bases, t_vgid, t_cgid, t_slots, t_ptr,
-                       t_inc, voff, coff, eoff, poff, gv, gc, vfeat, cfeat, slots, ptr, inc, g_vbase, g_nv, g_cbase,
+                       t_inc, voff, coff, eoff, poff, gv, gc, vfeat, cfeat, cdeg, slots, ptr, inc, g_vbase, g_nv, g_cbase,
                        g_nc, Nv, nnz);
     return check_launch("assemble_graph_batch_kernel");
 }

@@ -111,9 +111,11 @@ def _load():
     sig["msat_gemm_wgrad_workspace_bytes"] = (c_size_t, [c_int32, c_int32, c_int32])
     sig["msat_gemm_wgrad"] = (c_int32, [P, c_int32, P, c_int32, P, c_int32, c_int32, c_int32, c_int32, c_int32, P, P])
     I, F, Z, U = c_int32, c_float, c_size_t, c_uint64
-    sig["msat_assemble_graph_batch"] = (I, [I, I, I, I, I] + [P] * 25 + [I, I, P])
+    sig["msat_assemble_graph_batch"] = (I, [I, I, I, I, I] + [P] * 26 + [I, I, P])
     sig["msat_clause_gather"] = (I, [P, I, P, P, I, I, I, I, P])
     sig["msat_var_gather"] = (I, [P, I, P, P, P, I, I, I, I, P])
+    sig["msat_clause_gather2"] = (I, [P, P, I, P, P, I, I, I, I, I, P])
+    sig["msat_var_gather2"] = (I, [P, P, I, P, P, P, P, I, I, I, I, P])
     sig["msat_gru_ln_fwd"] = (I, [P, I, P, I, P, I, P, P, P, I, I, I, P])
     sig["msat_gru_ln_fused_fwd"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, P, P, P, P, P, P, I, P, I, I, I, P])
     sig["msat_gru_ln_bwd_g4"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, I, P])
@@ -155,6 +157,8 @@ EXPORTED = (
     "msat_assemble_graph_batch",
     "msat_clause_gather",
     "msat_var_gather",
+    "msat_clause_gather2",
+    "msat_var_gather2",
     "msat_gru_ln_fwd",
     "msat_gru_ln_fused_fwd",
     "msat_gru_ln_bwd_g4",

@@ -13,6 +13,7 @@ order: the whole update is bitwise reproducible).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -62,9 +63,9 @@ class StepTape:
     Hp: torch.Tensor
     Hn: torch.Tensor
     Hc: torch.Tensor
-    GIN: torch.Tensor  # (Nc, 2H) gathered clause input
+    GIN: torch.Tensor  # (Nc, 2H) clause GRU input: gathered [sum H_v+ | sum H_v-] (fused) or messages (ref)
     G4c: torch.Tensor  # (Nc, 4H) clause GRU pre-activations [r | z | gin | ghn]
-    NV: torch.Tensor  # (Nv, 2H) var-side messages
+    NV: torch.Tensor  # (Nv, 2H) var GRU inputs: gathered [sum H_c over + | over -] (fused) or messages (ref)
     G4p: torch.Tensor  # (Nv, 4H) update_v_pos pre-activations
     G4n: torch.Tensor  # (Nv, 4H) update_v_neg pre-activations
 
@@ -142,15 +143,17 @@ class GNNActorCritic:
         _chk(L_.msat_colsum(G, ldg, M, N, out, acc, ws.data_ptr(), self.stream), "msat_colsum")
 
     def _gru(self, cell: str, segs, hprev: torch.Tensor, ln_row: torch.Tensor, out: torch.Tensor,
-             g4: Optional[torch.Tensor], R: int):
-        """One fused GRU cell + LayerNorm (msat_gru_ln_fused_fwd): segs = [(ptr, ld, width)] of x."""
+             g4: Optional[torch.Tensor], R: int, wi: Optional[torch.Tensor] = None):
+        """One fused GRU cell + LayerNorm (msat_gru_ln_fused_fwd): segs = [(ptr, ld, width)] of x;
+        wi overrides the cell's input matrix (the phi-folded matrices of the fused encoder)."""
         H = self.H
         segs = list(segs) + [(0, 0, 0)] * (3 - len(segs))
         kx = sum(w for _, _, w in segs)
         GNNActorCritic.flops += 2 * R * 3 * H * (H + (kx + 15) // 16 * 16)
         (p0, l0, w0), (p1, l1, w1), (p2, l2, w2) = segs
         _chk(L_.msat_gru_ln_fused_fwd(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
-                                      self.p(f"enc.{cell}_wi").data_ptr(), self.p(f"enc.{cell}_bi").data_ptr(),
+                                      (self.p(f"enc.{cell}_wi") if wi is None else wi).data_ptr(),
+                                      self.p(f"enc.{cell}_bi").data_ptr(),
                                       self.p(f"enc.{cell}_wh").data_ptr(), self.p(f"enc.{cell}_bh").data_ptr(),
                                       self._ptr(ln_row), self._ptr(ln_row, H), out.data_ptr(), H,
                                       g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
@@ -162,18 +165,199 @@ class GNNActorCritic:
 
     # ---------------------------------------------------------- encoder ----
     def encode(self, b: GraphBatch, save: bool):
+        return self._encode_fused(b, save) if self.fuse_phi else self._encode_ref(b, save)
+
+    def encode_backward(self, b: GraphBatch, tape: List[StepTape], Hc_final, dHp, dHn, dHc):
+        if self.fuse_phi:
+            self._encode_backward_fused(b, tape, Hc_final, dHp, dHn, dHc)
+        else:
+            self._encode_backward_ref(b, tape, Hc_final, dHp, dHn, dHc)
+
+    def _embed(self, b: GraphBatch):
+        """literal / clause embeddings (learner:57-59): vfeat[:, 1:4] = svf, cfeat = clause features."""
+        H, e = self.H, lambda *shape: torch.empty(shape, dtype=torch.float32, device=self.device)
+        pp = self._ptr
+        Hp, Hn, Hc = e(b.Nv, H), e(b.Nv, H), e(b.Nc, H)
+        self._gemm(pp(b.vfeat, 1), 8, self.p("enc.lpe_w").data_ptr(), H, 0, Hp.data_ptr(), H,
+                   self.p("enc.lpe_b").data_ptr(), b.Nv, H, 3)
+        self._gemm(pp(b.vfeat, 1), 8, self.p("enc.lne_w").data_ptr(), H, 0, Hn.data_ptr(), H,
+                   self.p("enc.lne_b").data_ptr(), b.Nv, H, 3)
+        self._gemm(b.cfeat.data_ptr(), 3, self.p("enc.ce_w").data_ptr(), H, 0, Hc.data_ptr(), H,
+                   self.p("enc.ce_b").data_ptr(), b.Nc, H, 3)
+        return Hp, Hn, Hc
+
+    def _embed_backward(self, b: GraphBatch, dHp, dHn, dHc):
+        H, pp = self.H, self._ptr
+        Nv, Nc = b.Nv, b.Nc
+        self._wgrad(pp(b.vfeat, 1), 8, dHp.data_ptr(), H, self.g("enc.lpe_w").data_ptr(), H, Nv, 3, H)
+        self._colsum(dHp.data_ptr(), H, Nv, H, self.g("enc.lpe_b").data_ptr())
+        self._wgrad(pp(b.vfeat, 1), 8, dHn.data_ptr(), H, self.g("enc.lne_w").data_ptr(), H, Nv, 3, H)
+        self._colsum(dHn.data_ptr(), H, Nv, H, self.g("enc.lne_b").data_ptr())
+        self._wgrad(b.cfeat.data_ptr(), 3, dHc.data_ptr(), H, self.g("enc.ce_w").data_ptr(), H, Nc, 3, H)
+        self._colsum(dHc.data_ptr(), H, Nc, H, self.g("enc.ce_b").data_ptr())
+
+    # Fused encoder ("gather first, phi folded into the GRU input matrix").  Per message step
+    # the reference computes m_c+ = A+^T (H_v+ Wcp + bcp) and feeds [m_c+ | m_c-] through
+    # update_c's input matrix Wi_c (learner:66-69); by linearity
+    #     [m_c+ | m_c-] Wi_c = [A+^T H_v+ | A-^T H_v-] [[Wcp Wi_c+], [Wcn Wi_c-]] + n+ (bcp Wi_c+) + n- (bcn Wi_c-)
+    # with n+/- the clause row's positive / negative slot counts, and likewise on the var side
+    # n_v+ Wi_vp,n = (A+ H_c)(Wv+ Wi_vp,n) + deg+ (bv+ Wi_vp,n)  (learner:72-79).  So each step
+    # is two gathers of the node STATES plus the three fused GRU kernels, with the folded
+    # matrices F (rows: [products | count-column rows]) rebuilt once per forward; the phi GEMMs
+    # (forward, input-gradient and weight-gradient) disappear and the weight gradients of
+    # phi / Wi are recovered from dF once per backward (_unfuse_grads).  Same function,
+    # different fp32 association: parity is the 1e-5 fp32 bar, not bitwise.
+    fuse_phi = os.environ.get("MARLSAT_FUSE_PHI", "1") != "0"
+
+    def _fold_views(self):
+        H = self.H
+        if getattr(self, "_F", None) is None:
+            rows = (2 * H + 4) + 2 * (H + 8)
+            self._F = torch.zeros((rows, 3 * H), dtype=torch.float32, device=self.device)
+            self._gF = torch.zeros_like(self._F)
+        c, v = 2 * H + 4, H + 8
+        sl = lambda T: (T[:c], T[c:c + v], T[c + v:c + 2 * v])
+        return sl(self._F), sl(self._gF)
+
+    def _fold_weights(self):
+        """F_c (2H+4, 3H) = [Wcp Wi_c[:H]; Wcn Wi_c[H:]; bcp Wi_c[:H]; bcn Wi_c[H:]; 0; 0]
+        F_v+ (H+8, 3H) = [Wv+ Wi_vp[:H]; Wi_vp[H:H+4]; bv+ Wi_vp[:H]; 0; 0; 0]
+        F_v- (H+8, 3H) = [Wv- Wi_vn[:H]; Wi_vn[H:H+4]; 0; bv- Wi_vn[:H]; 0; 0]  (pad rows stay 0)."""
+        H, pp = self.H, self._ptr
+        (Fc, Fp, Fn), _ = self._fold_views()
+        W3 = 3 * H
+        wic = self.p("enc.gru_c_wi")
+        for half, nm in ((0, "phi_cp"), (1, "phi_cn")):
+            B = pp(wic[half * H])
+            self._gemm(self.p(f"enc.{nm}_w").data_ptr(), H, B, W3, 0, pp(Fc[half * H]), W3, None, H, W3, H)
+            self._gemm(self.p(f"enc.{nm}_b").data_ptr(), H, B, W3, 0, pp(Fc[2 * H + half]), W3, None, 1, W3, H)
+        wv, bv = self.p("enc.phi_v_w"), self.p("enc.phi_v_b")
+        for half, cell, F in ((0, "gru_vp", Fp), (1, "gru_vn", Fn)):
+            wi = self.p(f"enc.{cell}_wi")
+            self._gemm(pp(wv, half * H), 2 * H, wi.data_ptr(), W3, 0, F.data_ptr(), W3, None, H, W3, H)
+            F[H:H + 4].copy_(wi[H:H + 4])
+            self._gemm(pp(bv, half * H), H, wi.data_ptr(), W3, 0, pp(F[H + 4 + half]), W3, None, 1, W3, H)
+
+    def _unfuse_grads(self):
+        """dF -> phi / Wi gradients (F = W Wi: dW = dF Wi^T, dWi = W^T dF; bias rows likewise)."""
+        H, pp = self.H, self._ptr
+        _, (gFc, gFp, gFn) = self._fold_views()
+        W3 = 3 * H
+        wic, gwic = self.p("enc.gru_c_wi"), self.g("enc.gru_c_wi")
+        for half, nm in ((0, "phi_cp"), (1, "phi_cn")):
+            B, gB = pp(wic[half * H]), pp(gwic[half * H])
+            self._gemm(pp(gFc[half * H]), W3, B, W3, 1, self.g(f"enc.{nm}_w").data_ptr(), H, None, H, H, W3, 1)
+            self._gemm(pp(gFc[2 * H + half]), W3, B, W3, 1, self.g(f"enc.{nm}_b").data_ptr(), H, None, 1, H, W3, 1)
+            self._wgrad(self.p(f"enc.{nm}_w").data_ptr(), H, pp(gFc[half * H]), W3, gB, W3, H, H, W3)
+            self._wgrad(self.p(f"enc.{nm}_b").data_ptr(), H, pp(gFc[2 * H + half]), W3, gB, W3, 1, H, W3)
+        wv, bv = self.p("enc.phi_v_w"), self.p("enc.phi_v_b")
+        gwv, gbv = self.g("enc.phi_v_w"), self.g("enc.phi_v_b")
+        for half, cell, gF in ((0, "gru_vp", gFp), (1, "gru_vn", gFn)):
+            wi, gwi = self.p(f"enc.{cell}_wi"), self.g(f"enc.{cell}_wi")
+            self._gemm(gF.data_ptr(), W3, wi.data_ptr(), W3, 1, pp(gwv, half * H), 2 * H, None, H, H, W3, 1)
+            self._gemm(pp(gF[H + 4 + half]), W3, wi.data_ptr(), W3, 1, pp(gbv, half * H), H, None, 1, H, W3, 1)
+            self._wgrad(pp(wv, half * H), 2 * H, gF.data_ptr(), W3, gwi.data_ptr(), W3, H, H, W3)
+            self._wgrad(pp(bv, half * H), H, pp(gF[H + 4 + half]), W3, gwi.data_ptr(), W3, 1, H, W3)
+            self._colsum(pp(gF[H]), 4 * W3, 1, 4 * W3, pp(gwi[H]))  # the x / svf rows map 1:1
+
+    def _encode_fused(self, b: GraphBatch, save: bool):
         H, dev = self.H, self.device
         Nv, Nc = b.Nv, b.Nc
         e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)
         pp = self._ptr
-        Hp, Hn, Hc = e(Nv, H), e(Nv, H), e(Nc, H)
-        # literal / clause embeddings (learner:57-59): vfeat = [x | svf(3)]
-        self._gemm(pp(b.vfeat, 1), 4, self.p("enc.lpe_w").data_ptr(), H, 0, Hp.data_ptr(), H,
-                   self.p("enc.lpe_b").data_ptr(), Nv, H, 3)
-        self._gemm(pp(b.vfeat, 1), 4, self.p("enc.lne_w").data_ptr(), H, 0, Hn.data_ptr(), H,
-                   self.p("enc.lne_b").data_ptr(), Nv, H, 3)
-        self._gemm(b.cfeat.data_ptr(), 3, self.p("enc.ce_w").data_ptr(), H, 0, Hc.data_ptr(), H,
-                   self.p("enc.ce_b").data_ptr(), Nc, H, 3)
+        self._fold_weights()
+        (Fc, Fp, Fn), _ = self._fold_views()
+        Hp, Hn, Hc = self._embed(b)
+        tape: List[StepTape] = []
+        ln = self.p("enc.ln")
+        for l in range(self.L):
+            GIN = e(Nc, 2 * H)  # [A+^T H_v+ | A-^T H_v-]
+            _chk(L_.msat_clause_gather2(Hp.data_ptr(), Hn.data_ptr(), H, b.slots.data_ptr(), GIN.data_ptr(), 2 * H,
+                                        Nc, H, 0, 0, self.stream), "clause_gather2")
+            Hc1 = e(Nc, H)
+            G4c = e(Nc, 4 * H) if save else None
+            self._gru("gru_c", [(GIN.data_ptr(), 2 * H, 2 * H), (b.cdeg.data_ptr(), 4, 4)], Hc, ln[3 * l], Hc1, G4c,
+                      Nc, wi=Fc)
+            NV = e(Nv, 2 * H)  # [A+ H_c | A- H_c]
+            _chk(L_.msat_var_gather2(Hc1.data_ptr(), Hc1.data_ptr(), H, b.ptr.data_ptr(), b.inc.data_ptr(),
+                                     NV.data_ptr(), pp(NV, H), 2 * H, Nv, H, 0, self.stream), "var_gather2")
+            outs = []
+            for half, cell, Hx, k, F in ((0, "gru_vp", Hp, 3 * l + 1, Fp), (1, "gru_vn", Hn, 3 * l + 2, Fn)):
+                Hx1 = e(Nv, H)
+                G4 = e(Nv, 4 * H) if save else None
+                # input [n_v | x | svf | n+ n- 0 0] against F rows [fold | Wi x/svf | count rows]
+                self._gru(cell, [(pp(NV, half * H), 2 * H, H), (b.vfeat.data_ptr(), 8, 8)], Hx, ln[k], Hx1, G4, Nv,
+                          wi=F)
+                outs.append((G4, Hx1))
+            if save:
+                tape.append(StepTape(Hp, Hn, Hc, GIN, G4c, NV, outs[0][0], outs[1][0]))
+            Hp, Hn, Hc = outs[0][1], outs[1][1], Hc1
+        return Hp, Hn, Hc, tape
+
+    def _encode_backward_fused(self, b: GraphBatch, tape: List[StepTape], Hc_final, dHp, dHn, dHc):
+        H, dev = self.H, self.device
+        Nv, Nc = b.Nv, b.Nc
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)
+        pp = self._ptr
+        W3 = 3 * H
+        ln, dln = self.p("enc.ln"), self.g("enc.ln")
+        (Fc, Fp, Fn), (gFc, gFp, gFn) = self._fold_views()
+        self._gF.zero_()
+        for l in range(self.L - 1, -1, -1):
+            t = tape[l]
+            dNV = e(Nv, 2 * H)
+            dprev = {}
+            for half, cell, Hx, G4, dHx, k, F, gF in ((0, "gru_vp", t.Hp, t.G4p, dHp, 3 * l + 1, Fp, gFp),
+                                                     (1, "gru_vn", t.Hn, t.G4n, dHn, 3 * l + 2, Fn, gFn)):
+                dGI, dGH = e(Nv, W3), e(Nv, W3)
+                dHx0 = torch.zeros((Nv, H), dtype=torch.float32, device=dev)
+                part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nv, H)))
+                _chk(L_.msat_gru_ln_bwd_g4(dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, pp(ln[k]),
+                                           dGI.data_ptr(), W3, dGH.data_ptr(), W3, dHx0.data_ptr(), H,
+                                           pp(dln[k]), pp(dln[k], H), self.g(f"enc.{cell}_bi").data_ptr(),
+                                           pp(self.g(f"enc.{cell}_bh"), 2 * H), part.data_ptr(), Nv, H, 1,
+                                           self.stream), "gru_ln_bwd_g4")
+                wh, gwh = self.p(f"enc.{cell}_wh"), self.g(f"enc.{cell}_wh")
+                self._gemm(dGH.data_ptr(), W3, wh.data_ptr(), W3, 1, dHx0.data_ptr(), H, None, Nv, H, W3, 1)
+                self._wgrad(Hx.data_ptr(), H, dGH.data_ptr(), W3, gwh.data_ptr(), W3, Nv, H, W3)
+                # input path: d(gathered) and dF rows [fold | x/svf | counts]
+                self._gemm(dGI.data_ptr(), W3, F.data_ptr(), W3, 1, pp(dNV, half * H), 2 * H, None, Nv, H, W3, 0)
+                self._wgrad(pp(t.NV, half * H), 2 * H, dGI.data_ptr(), W3, gF.data_ptr(), W3, Nv, H, W3)
+                self._wgrad(b.vfeat.data_ptr(), 8, dGI.data_ptr(), W3, pp(gF[H]), W3, Nv, 8, W3)
+                dprev[half] = dHx0
+            # var gather backward: dH_c (+)= A+^T dNV+ + A-^T dNV-  (one merged clause gather)
+            _chk(L_.msat_clause_gather2(dNV.data_ptr(), pp(dNV, H), 2 * H, b.slots.data_ptr(), dHc.data_ptr(), H, Nc,
+                                        H, 1, 1, self.stream), "clause_gather2")
+            # clause GRU
+            dGI, dGH = e(Nc, W3), e(Nc, W3)
+            dHc0 = torch.zeros((Nc, H), dtype=torch.float32, device=dev)
+            part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nc, H)))
+            _chk(L_.msat_gru_ln_bwd_g4(dHc.data_ptr(), H, t.G4c.data_ptr(), 4 * H, t.Hc.data_ptr(), H, pp(ln[3 * l]),
+                                       dGI.data_ptr(), W3, dGH.data_ptr(), W3, dHc0.data_ptr(), H,
+                                       pp(dln[3 * l]), pp(dln[3 * l], H), self.g("enc.gru_c_bi").data_ptr(),
+                                       pp(self.g("enc.gru_c_bh"), 2 * H), part.data_ptr(), Nc, H, 1, self.stream),
+                 "gru_ln_bwd_g4")
+            self._gemm(dGH.data_ptr(), W3, self.p("enc.gru_c_wh").data_ptr(), W3, 1, dHc0.data_ptr(), H, None,
+                       Nc, H, W3, 1)
+            self._wgrad(t.Hc.data_ptr(), H, dGH.data_ptr(), W3, self.g("enc.gru_c_wh").data_ptr(), W3, Nc, H, W3)
+            dGIN = e(Nc, 2 * H)
+            self._gemm(dGI.data_ptr(), W3, Fc.data_ptr(), W3, 1, dGIN.data_ptr(), 2 * H, None, Nc, 2 * H, W3, 0)
+            self._wgrad(t.GIN.data_ptr(), 2 * H, dGI.data_ptr(), W3, gFc.data_ptr(), W3, Nc, 2 * H, W3)
+            self._wgrad(b.cdeg.data_ptr(), 4, dGI.data_ptr(), W3, pp(gFc[2 * H]), W3, Nc, 4, W3)
+            # clause gather backward: dH_v+/- (+)= A+/- dGIN+/-
+            _chk(L_.msat_var_gather2(dGIN.data_ptr(), pp(dGIN, H), 2 * H, b.ptr.data_ptr(), b.inc.data_ptr(),
+                                     dprev[0].data_ptr(), dprev[1].data_ptr(), H, Nv, H, 1, self.stream),
+                 "var_gather2")
+            dHp, dHn, dHc = dprev[0], dprev[1], dHc0
+        self._embed_backward(b, dHp, dHn, dHc)
+        self._unfuse_grads()
+
+    def _encode_ref(self, b: GraphBatch, save: bool):
+        H, dev = self.H, self.device
+        Nv, Nc = b.Nv, b.Nc
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)
+        pp = self._ptr
+        Hp, Hn, Hc = self._embed(b)
         tape: List[StepTape] = []
         ln = self.p("enc.ln")
         for l in range(self.L):
@@ -199,14 +383,14 @@ class GNNActorCritic:
                 # input [n_v | x | svf] (learner:75,78)
                 Hx1 = e(Nv, H)
                 G4 = e(Nv, 4 * H) if save else None
-                self._gru(cell, [(pp(NV, half * H), 2 * H, H), (b.vfeat.data_ptr(), 4, 4)], Hx, ln[k], Hx1, G4, Nv)
+                self._gru(cell, [(pp(NV, half * H), 2 * H, H), (b.vfeat.data_ptr(), 8, 4)], Hx, ln[k], Hx1, G4, Nv)
                 outs.append((G4, Hx1))
             if save:
                 tape.append(StepTape(Hp, Hn, Hc, GIN, G4c, NV, outs[0][0], outs[1][0]))
             Hp, Hn, Hc = outs[0][1], outs[1][1], Hc1
         return Hp, Hn, Hc, tape
 
-    def encode_backward(self, b: GraphBatch, tape: List[StepTape], Hc_final, dHp, dHn, dHc):
+    def _encode_backward_ref(self, b: GraphBatch, tape: List[StepTape], Hc_final, dHp, dHn, dHc):
         H, dev = self.H, self.device
         Nv, Nc = b.Nv, b.Nc
         e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)
@@ -236,7 +420,7 @@ class GNNActorCritic:
                 self._gemm(dGI.data_ptr(), 3 * H, wi.data_ptr(), 3 * H, 1, pp(dNV, half * H), 2 * H, None, Nv, H,
                            3 * H, 0)
                 self._wgrad(pp(t.NV, half * H), 2 * H, dGI.data_ptr(), 3 * H, gwi.data_ptr(), 3 * H, Nv, H, 3 * H)
-                self._wgrad(b.vfeat.data_ptr(), 4, dGI.data_ptr(), 3 * H, pp(gwi[H]), 3 * H, Nv, 4, 3 * H)
+                self._wgrad(b.vfeat.data_ptr(), 8, dGI.data_ptr(), 3 * H, pp(gwi[H]), 3 * H, Nv, 4, 3 * H)
                 dprev[half] = dHx0
             # var gather backward = clause gather of dNV
             dTPN = e(Nc, 2 * H)
@@ -275,13 +459,7 @@ class GNNActorCritic:
                 self._wgrad(Hx.data_ptr(), H, pp(dMV, half * H), 2 * H, self.g(f"enc.{nm}_w").data_ptr(), H, Nv, H, H)
                 self._colsum(pp(dMV, half * H), 2 * H, Nv, H, self.g(f"enc.{nm}_b").data_ptr())
             dHp, dHn, dHc = dprev[0], dprev[1], dHc0
-        # embeddings
-        self._wgrad(pp(b.vfeat, 1), 4, dHp.data_ptr(), H, self.g("enc.lpe_w").data_ptr(), H, Nv, 3, H)
-        self._colsum(dHp.data_ptr(), H, Nv, H, self.g("enc.lpe_b").data_ptr())
-        self._wgrad(pp(b.vfeat, 1), 4, dHn.data_ptr(), H, self.g("enc.lne_w").data_ptr(), H, Nv, 3, H)
-        self._colsum(dHn.data_ptr(), H, Nv, H, self.g("enc.lne_b").data_ptr())
-        self._wgrad(b.cfeat.data_ptr(), 3, dHc.data_ptr(), H, self.g("enc.ce_w").data_ptr(), H, Nc, 3, H)
-        self._colsum(dHc.data_ptr(), H, Nc, H, self.g("enc.ce_b").data_ptr())
+        self._embed_backward(b, dHp, dHn, dHc)
 
     # ------------------------------------------------------------ heads ----
     def _gr(self, b: GraphBatch):

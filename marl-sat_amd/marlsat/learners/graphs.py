@@ -160,8 +160,9 @@ class GraphBatch:
     Nv: int
     Nc: int
     nnz: int
-    vfeat: torch.Tensor  # (Nv, 4) [x, deg+/C, deg-/C, 0]
+    vfeat: torch.Tensor  # (Nv, 8) [x, deg+/C, deg-/C, 0, n+, n-, 0, 0] (n: incidences in the row's graph)
     cfeat: torch.Tensor  # (Nc, 3) [is_sat, ntrue/3, 1]
+    cdeg: torch.Tensor  # (Nc, 4) [n+, n-, 0, 0] positive / negative literal slots
     slots: torch.Tensor  # (Nc, 3)
     ptr: torch.Tensor  # (Nv + 1,)
     inc: torch.Tensor  # (nnz,)
@@ -185,8 +186,9 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
     Nv, Nc, nnz = (int(t) for t in torch.stack([vb[-1], cb[-1], eb[-1]]).tolist())
     dev = inst.device
     out = GraphBatch(S, G, Nv, Nc, nnz,
-                     torch.empty((Nv, 4), dtype=torch.float32, device=dev),
+                     torch.empty((Nv, 8), dtype=torch.float32, device=dev),
                      torch.empty((Nc, 3), dtype=torch.float32, device=dev),
+                     torch.empty((Nc, 4), dtype=torch.float32, device=dev),
                      torch.empty((Nc, 3), dtype=torch.int32, device=dev),
                      torch.empty((Nv + 1,), dtype=torch.int32, device=dev),
                      torch.empty((max(nnz, 1),), dtype=torch.int32, device=dev),
@@ -201,7 +203,7 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
         S, G, tpl.A, V, C, inst.data_ptr(), x.data_ptr(), svf.data_ptr(), pool_packed.data_ptr(), sb.data_ptr(),
         tpl.vgid.data_ptr(), tpl.cgid.data_ptr(), tpl.slots.data_ptr(), tpl.ptr.data_ptr(), tpl.inc.data_ptr(),
         tpl.voff.data_ptr(), tpl.coff.data_ptr(), tpl.eoff.data_ptr(), tpl.poff.data_ptr(), tpl.gv.data_ptr(),
-        tpl.gc.data_ptr(), out.vfeat.data_ptr(), out.cfeat.data_ptr(), out.slots.data_ptr(), out.ptr.data_ptr(),
+        tpl.gc.data_ptr(), out.vfeat.data_ptr(), out.cfeat.data_ptr(), out.cdeg.data_ptr(), out.slots.data_ptr(), out.ptr.data_ptr(),
         out.inc.data_ptr(), out.vbase.data_ptr(), out.nv.data_ptr(), out.cbase.data_ptr(), out.nc.data_ptr(),
         Nv, nnz, _lib.stream_ptr(dev)), "msat_assemble_graph_batch")
     return out

@@ -115,6 +115,35 @@ def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
         _ref_close(W, ref, absprod)
 
 
+@pytest.mark.parametrize("M,K,N,lda,aoff,ldw", [(1, 1, 4, 1, 0, 4), (1000, 3, 384, 4, 1, 384), (300001, 4, 384, 8, 4, 384),
+                                                (77777, 8, 260, 8, 0, 264), (5000, 5, 128, 7, 2, 132),
+                                                (64, 2, 768, 2, 0, 768)])
+def test_wgrad_skinny(M, K, N, lda, aoff, ldw):
+    """K <= 8 weight gradients (input features, degree columns) take the streaming reduction:
+    unaligned / strided A rows, strided W, accumulate, bitwise repeatable."""
+    from marlsat import _lib
+
+    g = torch.Generator(device="cuda").manual_seed(M + 13 * K + N)
+    abuf = torch.randn(M * lda + aoff + 8, device="cuda", generator=g)
+    A = abuf[aoff:aoff + M * lda].view(M, lda)
+    G = torch.randn(M, N, device="cuda", generator=g)
+    W0 = torch.randn(K, ldw, device="cuda", generator=g)
+    ws = torch.empty(int(_lib.lib.msat_gemm_wgrad_workspace_bytes(M, K, N)) // 4 + 4, device="cuda")
+    for acc in (0, 1):
+        outs = []
+        for _ in range(2):
+            W = W0.clone()
+            _lib.check(_lib.lib.msat_gemm_wgrad(A.data_ptr(), lda, G.data_ptr(), N, W.data_ptr(), ldw, M, K, N, acc,
+                                                ws.data_ptr(), _lib.stream_ptr()), "wgrad")
+            outs.append(W)
+        assert torch.equal(outs[0], outs[1])
+        Ad = A[:, :K].double()
+        ref = Ad.t() @ G.double() + (W0[:, :N].double() if acc else 0)
+        absprod = Ad.abs().t() @ G.double().abs() + (W0[:, :N].double().abs() if acc else 0)
+        _ref_close(outs[0][:, :N], ref, absprod)
+        assert torch.equal(outs[0][:, N:], W0[:, N:])
+
+
 @pytest.mark.parametrize("M,N,ld,off", [(1, 4, 4, 0), (221000, 128, 256, 128), (5000, 384, 384, 0), (777, 7, 9, 1),
                                         (0, 8, 8, 0), (100, 130, 132, 2)])
 def test_colsum_deterministic(M, N, ld, off):
