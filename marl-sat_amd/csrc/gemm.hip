@@ -244,9 +244,11 @@ __global__ void wgrad_reduce_kernel(const float *__restrict__ part, int splits, 
 // order, and part[split][k][n] is reduced by skinny_reduce4_kernel (fixed split order).
 constexpr int kSkinnyK = 8;
 
+template <bool AV>
 __global__ void __launch_bounds__(256)
 wgrad_skinny_kernel(const float *__restrict__ A, int lda, const float4 *__restrict__ G, int ldg4, int M, int K, int N4,
                     int rows_per, float4 *__restrict__ part) {
+    constexpr int U = 4;  // rows in flight per thread (independent loads issued before use)
     __shared__ float4 red[16][16];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int c = blockIdx.x * 16 + tx;
@@ -254,17 +256,49 @@ wgrad_skinny_kernel(const float *__restrict__ A, int lda, const float4 *__restri
     float4 acc[kSkinnyK];
 #pragma unroll
     for (int k = 0; k < kSkinnyK; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < N4)
-        for (int r = r0 + ty; r < r1; r += 16) {
+    if (c < N4) {
+        int r = r0 + ty;
+        for (; r + 16 * (U - 1) < r1; r += 16 * U) {
+            float4 g[U];
+            float a[U][kSkinnyK];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int rr = r + 16 * u;
+                g[u] = G[(size_t)rr * ldg4 + c];
+                const float *ap = A + (size_t)rr * lda;
+                if (AV) {
+                    const float4 a0 = *reinterpret_cast<const float4 *>(ap);
+                    a[u][0] = a0.x; a[u][1] = a0.y; a[u][2] = a0.z; a[u][3] = a0.w;
+                    if (K > 4) {
+                        const float4 a1 = *reinterpret_cast<const float4 *>(ap + 4);
+                        a[u][4] = a1.x; a[u][5] = a1.y; a[u][6] = a1.z; a[u][7] = a1.w;
+                    } else {
+                        a[u][4] = a[u][5] = a[u][6] = a[u][7] = 0.0f;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < kSkinnyK; ++k) a[u][k] = k < K ? ap[k] : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int k = 0; k < kSkinnyK; ++k) {
+                    const float av = a[u][k];
+                    acc[k].x += av * g[u].x; acc[k].y += av * g[u].y; acc[k].z += av * g[u].z; acc[k].w += av * g[u].w;
+                }
+        }
+        for (; r < r1; r += 16) {
             const float4 g = G[(size_t)r * ldg4 + c];
-            const float *a = A + (size_t)r * lda;
+            const float *ap = A + (size_t)r * lda;
 #pragma unroll
             for (int k = 0; k < kSkinnyK; ++k)
                 if (k < K) {
-                    const float av = a[k];
+                    const float av = ap[k];
                     acc[k].x += av * g.x; acc[k].y += av * g.y; acc[k].z += av * g.z; acc[k].w += av * g.w;
                 }
         }
+    }
 #pragma unroll
     for (int k = 0; k < kSkinnyK; ++k) {
         if (k >= K) break;
@@ -379,8 +413,13 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
     if (!legacy_gemm() && skinny_ok(G, ldg, W, ldw, K, N) && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0) {
         const int sp = skinny_splits(M, N), rows_per = (M + sp - 1) / sp, N4 = N / 4;
         float4 *ws4 = reinterpret_cast<float4 *>(workspace);
-        hipLaunchKernelGGL(wgrad_skinny_kernel, dim3((N4 + 15) / 16, sp), dim3(256), 0, s, A, lda,
-                           reinterpret_cast<const float4 *>(G), ldg / 4, M, K, N4, rows_per, ws4);
+        const bool av = lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
+        if (av)
+            hipLaunchKernelGGL((wgrad_skinny_kernel<true>), dim3((N4 + 15) / 16, sp), dim3(256), 0, s, A, lda,
+                               reinterpret_cast<const float4 *>(G), ldg / 4, M, K, N4, rows_per, ws4);
+        else
+            hipLaunchKernelGGL((wgrad_skinny_kernel<false>), dim3((N4 + 15) / 16, sp), dim3(256), 0, s, A, lda,
+                               reinterpret_cast<const float4 *>(G), ldg / 4, M, K, N4, rows_per, ws4);
         const int rc = check_launch("wgrad_skinny_kernel");
         if (rc) return rc;
         hipLaunchKernelGGL(skinny_reduce4_kernel, dim3((K * N4 + 15) / 16), dim3(256), 0, s, ws4, sp, K * N4, N4,
