@@ -49,6 +49,33 @@ __host__ __device__ __forceinline__ uint4 reset_rng_block(uint64_t seed, uint64_
                          (uint32_t)(seed >> 32));
 }
 
+// ------------------------------------------------------------- LDS-DMA ----
+// global_load_lds_dwordx4 issued from inline asm: 16 bytes per lane from `src` into LDS at
+// the wave-uniform byte address `lds` + 16 * lane.  The builtin form is tracked by hipcc, which
+// then waits vmcnt(0) before EVERY later ds_read (it cannot tell the DMA's target buffer from
+// the one being read), so the next slab's load never overlaps the current slab's MFMAs.  The
+// asm form is invisible to hipcc's wait bookkeeping: the caller retires it with a counted
+// wait_vmcnt<N>() and a barrier before reading the buffer.  M0 is saved and restored in the
+// same statement (it is compiler-reserved).
+__device__ __forceinline__ void glds16_async(const void *src, const void *lds) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(dst)
+        : "memory");
+}
+
+// s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory operations are done.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// workgroup barrier that waits only for this wave's LDS operations (not for vector memory)
+__device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // ----------------------------------------------------------- reductions ----
 __device__ __forceinline__ int wave_sum_i32(int v) {
 #pragma unroll

@@ -39,9 +39,7 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-__device__ __forceinline__ void glds16(const float *src, float *dst) {
-    __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-}
+__device__ __forceinline__ void glds16(const float *src, float *dst) { glds16_async(src, dst); }
 
 // chunk swizzle of a k-major image row o (D/4 chunks of 4 floats per row)
 template <int D>
@@ -131,12 +129,15 @@ __device__ __forceinline__ void mfma_slab(const float *Ai, const float *Bi, int 
 }
 
 // C[M,N] (+)= A[M,K] @ op(B) + bias; A k-major; B o-major (B[K][N]) or k-major (B[N][K]).
-template <int D, bool BK>
-__global__ void __launch_bounds__(kG2T, D == 16 ? 4 : 2)
+// NST = 2: double buffer, slab s+1 lands while slab s is multiplied.  NST = 3: slabs s+1 and
+// s+2 in flight; each wave waits (counted vmcnt) only for slab s.  Both retire the asm LDS-DMA
+// with explicit vmcnt waits + an LDS-only barrier (common.h glds16_async).
+template <int D, bool BK, int NST = 2>
+__global__ void __launch_bounds__(kG2T, NST == 3 ? 3 : (D == 16 ? 4 : 2))
 gemm2_kernel(const float *__restrict__ A, int lda, const float *__restrict__ B, int ldb, float *__restrict__ C,
              int ldc, const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
     constexpr int IMG = kG2M * D;
-    __shared__ __attribute__((aligned(16))) float lds[4 * IMG];  // [buf][A|B]
+    __shared__ __attribute__((aligned(16))) float lds[(NST == 3 ? 6 : 4) * IMG];  // [buf][A|B]
     const int id = xcd_remap(blockIdx.x, gridDim.x);
     const int m0 = (id / ntn) * kG2M, n0 = (id % ntn) * kG2M;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -153,14 +154,34 @@ gemm2_kernel(const float *__restrict__ A, int lda, const float *__restrict__ B, 
         if (BK) fill_kmajor<D>(Bi, B, ldb, n0, N, s * D);
         else fill_omajor<D>(Bi, B, ldb, n0, N, s * D, K);
     };
-    fill(0, 0);
-    __syncthreads();
-    for (int s = 0; s < ns; ++s) {
-        const int buf = s & 1;
-        if (s + 1 < ns) fill(s + 1, buf ^ 1);
-        const float *Ai = lds + buf * 2 * IMG;
-        mfma_slab<D, true, BK>(Ai, Ai + IMG, wr, wc, acc);
-        __syncthreads();  // next image landed (vmcnt) and this one fully read
+    if (NST == 3) {
+        // glds per thread per slab: A image kG2M*D/1024 instructions per wave... (fill_* NI), both operands
+        constexpr int G = 2 * (D / 8);
+        fill(0, 0);
+        if (ns > 1) fill(1, 1);
+        for (int s = 0; s < ns; ++s) {
+            __builtin_amdgcn_sched_barrier(0);  // slab s-1's MFMAs stay above the wait
+            if (s + 1 < ns) wait_vmcnt<G>();  // slab s landed (this wave's part); slab s+1 may fly
+            else wait_vmcnt<0>();
+            barrier_lds();  // every wave's part of slab s landed; slab s-1 fully read
+            if (s + 2 < ns) fill(s + 2, (s + 2) % 3);
+            const float *Ai = lds + (s % 3) * 2 * IMG;
+            mfma_slab<D, true, BK>(Ai, Ai + IMG, wr, wc, acc);
+        }
+        __syncthreads();  // last slab read by every wave before the epilogue reuses LDS
+    } else {
+        fill(0, 0);
+        wait_vmcnt<0>();
+        barrier_lds();
+        for (int s = 0; s < ns; ++s) {
+            const int buf = s & 1;
+            if (s + 1 < ns) fill(s + 1, buf ^ 1);  // lands while slab s is multiplied
+            const float *Ai = lds + buf * 2 * IMG;
+            mfma_slab<D, true, BK>(Ai, Ai + IMG, wr, wc, acc);
+            __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs above the wait (they hide the load)
+            wait_vmcnt<0>();
+            barrier_lds();  // next image landed (every wave) and this one fully read
+        }
     }
     if (vec_out) {
         // LDS-staged epilogue: each wave's 32x64 half-tile goes through its own 8 KiB LDS region
@@ -254,14 +275,17 @@ wgrad2_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G,
     };
     if (ns > 0) {
         fill(0, 0);
-        __syncthreads();
+        wait_vmcnt<0>();
+        barrier_lds();
     }
     for (int sl = 0; sl < ns; ++sl) {
         const int buf = sl & 1;
-        if (sl + 1 < ns) fill(sl + 1, buf ^ 1);
+        if (sl + 1 < ns) fill(sl + 1, buf ^ 1);  // lands while slab sl is multiplied
         const float *Ai = lds + buf * 2 * IMG;
         mfma_slab<D, false, false>(Ai, Ai + IMG, wr, wc, acc);
-        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);
+        wait_vmcnt<0>();
+        barrier_lds();
     }
     float *P = part + (size_t)s * K * N;
 #pragma unroll
@@ -291,6 +315,12 @@ static int slab_depth() {
     return (e && atoi(e) == 32) ? 32 : 16;
 }
 
+// MARLSAT_GEMM_STAGES selects the GEMM pipeline depth (2: double buffer; 3: two slabs in flight).
+static int gemm_stages() {
+    const char *e = getenv("MARLSAT_GEMM_STAGES");
+    return (e && atoi(e) == 3) ? 3 : 2;
+}
+
 bool msat_gemm2_ok(const float *A, int lda, const float *B, int ldb, int transB, int N, int K) {
     if (K % 32 || K == 0 || lda % 4 || ldb % 4 || !al16(A) || !al16(B)) return false;
     if (!transB && N % 4) return false;  // o-major B chunks are 4 columns wide
@@ -305,12 +335,17 @@ int msat_gemm2_launch(const float *A, int lda, const float *B, int ldb, int tran
     const int vec = (N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!bias || al16(bias))) ? 1 : 0;
 #define MSAT_G2(D, T) hipLaunchKernelGGL((gemm2_kernel<D, T>), grid, blk, 0, s, A, lda, B, ldb, C, ldc, bias, M, N, K, \
                                          accumulate, ntn, vec)
-    if (slab_depth() == 16) {
+#define MSAT_G3(T) hipLaunchKernelGGL((gemm2_kernel<16, T, 3>), grid, blk, 0, s, A, lda, B, ldb, C, ldc, bias, M, N, \
+                                      K, accumulate, ntn, vec)
+    if (gemm_stages() == 3 && slab_depth() == 16) {
+        if (transB) MSAT_G3(true); else MSAT_G3(false);
+    } else if (slab_depth() == 16) {
         if (transB) MSAT_G2(16, true); else MSAT_G2(16, false);
     } else {
         if (transB) MSAT_G2(32, true); else MSAT_G2(32, false);
     }
 #undef MSAT_G2
+#undef MSAT_G3
     return check_launch("gemm2_kernel");
 }
 

@@ -108,7 +108,7 @@ gru_ln_fused_fwd_kernel(GruFwdArgs a) {
             const int r = f / (BW / 4), c4 = f - r * (BW / 4);
             const float *src = W + (size_t)min(kb + r, klast) * BW + 4 * c4;
             float *dst = Bs[buf] + 4 * (i * T + 64 * w);  // wave-uniform base; lane l lands at +16 l bytes
-            __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+            glds16_async(src, dst);  // retired by the explicit vmcnt wait before the slab barrier
         }
     };
     auto storeA = [&](int buf) {
@@ -155,15 +155,20 @@ gru_ln_fused_fwd_kernel(GruFwdArgs a) {
     issueB(0, 0);
     loadA(0);
     storeA(0);
-    __syncthreads();
-    // two loops (hidden slabs, then input slabs) so each carries one accumulator subset
+    wait_vmcnt<0>();
+    barrier_lds();
+    // two loops (hidden slabs, then input slabs) so each carries one accumulator subset.  Slab
+    // s+1 (B by LDS-DMA, A into registers) is in flight while slab s is multiplied; the
+    // scheduling barriers keep the MFMAs ahead of the waits that retire it.
     int buf = 0;
     for (int s = 0; s < nsh; ++s) {
         issueB(s + 1, buf ^ 1);  // ns > nsh: there is always a next slab here
         loadA(s + 1);
         slab(buf, true);
+        __builtin_amdgcn_sched_barrier(0);
         storeA(buf ^ 1);
-        __syncthreads();  // drains the LDS-DMA (vmcnt) and the A stores before the next slab
+        wait_vmcnt<0>();
+        barrier_lds();  // B image and A stores of slab s+1 complete; slab s fully read
         buf ^= 1;
     }
     for (int s = nsh; s < ns; ++s) {
@@ -173,8 +178,10 @@ gru_ln_fused_fwd_kernel(GruFwdArgs a) {
             loadA(s + 1);
         }
         slab(buf, false);
+        __builtin_amdgcn_sched_barrier(0);
         if (more) storeA(buf ^ 1);
-        __syncthreads();
+        wait_vmcnt<0>();
+        barrier_lds();
         buf ^= 1;
     }
 

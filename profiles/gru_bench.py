@@ -7,9 +7,11 @@ import torch
 from marlsat import _lib
 
 H = 128
-for kind, R, segs_w in (("var", 887000, (H, 4)), ("clause", 857000, (2 * H,))):
+# bench training shapes (uf50, micro-batch 1,366): var cells read [gathered half (ld 2H) | vfeat (8)],
+# the clause cell [gathered (2H) | counts (4)]
+for kind, R, segs_w, segs_ld in (("var", 407000, (H, 8), (2 * H, 8)), ("clause", 1036000, (2 * H, 4), (2 * H, 4))):
     g = torch.Generator(device="cuda").manual_seed(0)
-    X = [torch.randn(R, w if w != H else 2 * H, device="cuda", generator=g) for w in segs_w]
+    X = [torch.randn(R, ld, device="cuda", generator=g) for ld in segs_ld]
     h = torch.randn(R, H, device="cuda", generator=g)
     Kx = sum(segs_w)
     wi = torch.randn(Kx, 3 * H, device="cuda", generator=g) / Kx ** 0.5

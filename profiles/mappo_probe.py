@@ -46,7 +46,10 @@ if "rollout" in phases:
   t, fl = timed(lambda: lr.policy(st, PRNGKey(1)))
   res["rollout_forward"] = {"samples": S_roll, "s": t, "samples_per_s": S_roll / t, "tflops": fl / t / 1e12,
                           "frac_fp32_mfma_peak": fl / t / 157.3e12}
-pidx = st.problem_idx[:S_train].contiguous(); x = st.variable_assignments[:S_train].contiguous()
+# training samples: the rollout states, tiled when S_train exceeds the rollout batch
+rep = -(-S_train // st.num_envs)
+pidx = st.problem_idx.repeat(rep)[:S_train].contiguous()
+x = st.variable_assignments.repeat(rep, 1)[:S_train].contiguous()
 def train_step():
     gb = lr._batch(pidx, x)
     logits, value, state = net.forward(gb, save=True)
