@@ -24,6 +24,15 @@ int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ldb, int32_t 
               int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, int32_t accumulate,
               void *stream);
 
+/* fp32 GEMM on the bf16 matrix cores (gemm_x3.hip): operands split exactly into three bf16
+ * parts, six bf16 MFMAs per 16-deep k step keep every product term above fp32 rounding.
+ * msat_split_bf16x3: planes (3 x rows x cols bf16, contiguous) of W (rows x cols, ldw).
+ * msat_gemm_x3: C[M,N] (+)= A[M,K] @ W^T (+ bias), W [N][K] given as its split planes;
+ *   K % 16 == 0, lda % 4 == 0, 16-byte aligned A / planes. */
+int msat_split_bf16x3(const float *W, int32_t rows, int32_t cols, int32_t ldw, void *planes, void *stream);
+int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, float *C, int32_t ldc, const float *bias,
+                 int32_t M, int32_t N, int32_t K, int32_t accumulate, void *stream);
+
 /* W[K,N] (+)= A[M,K]^T @ G[M,N]: split over M, partial slabs reduced in a fixed order.
  * K <= 8 (feature / degree columns) streams G once instead of running 128-row MFMA tiles. */
 size_t msat_gemm_wgrad_workspace_bytes(int32_t M, int32_t K, int32_t N);

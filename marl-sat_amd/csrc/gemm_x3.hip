@@ -1,0 +1,234 @@
+// fp32 GEMM on the bf16 matrix cores by three-way operand splitting ("bf16x3").
+//
+// An fp32 value x is split exactly into three bf16 parts x = x1 + x2 + x3 + O(2^-24 |x|)
+// (x1 = bf16(x), x2 = bf16(x - x1), x3 = bf16(x - x1 - x2); each difference is exact in fp32).
+// A product a*b then keeps every term above the fp32 rounding level:
+//     a b ~= a1 b1 + (a1 b2 + a2 b1) + (a1 b3 + a2 b2 + a3 b1)          (dropped terms <= 3 * 2^-24 |a b|)
+// and bf16 x bf16 products are exact in fp32, so six v_mfma_f32_32x32x16_bf16 per 16-deep k step
+// reproduce the fp32 dot product to fp32 rounding (the 1e-5 parity bar holds with margin; see
+// tests/test_gemm_gpu.py).  Six bf16 MFMAs (32 cycles each per SIMD) replace eight f32 32x32x2
+// MFMAs (64 cycles each): 2.67x fewer matrix-core cycles for the same fp32 result.
+//
+// msat_gemm_x3: C[M,N] (+)= A[M,K] @ W^T (+ bias) with W [N][K] given as pre-split bf16 planes
+// (msat_split_bf16x3, once per weight update).  The activation operand A is split while it is
+// staged: global fp32 -> registers -> three bf16 planes in LDS; the weight planes arrive by
+// LDS-DMA.  128x128 tile per 256-thread workgroup (wave = 64x64 = 2x2 MFMA tiles), 16-deep slabs,
+// double-buffered (slab s+1 lands while slab s is multiplied).
+#include <stdlib.h>
+
+#include <algorithm>
+
+#include "common.h"
+
+namespace msat {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+
+constexpr int kX3T = 256;
+constexpr int kX3M = 128;  // tile rows / cols
+constexpr int kX3D = 16;   // slab depth (one bf16 MFMA k step)
+// LDS plane: 128 rows x 16 k bf16 = 4 KiB = 256 uint4 (row r, k-half h at uint4 index 2r + h)
+constexpr int kX3Plane = kX3M * kX3D / 8;
+
+__device__ __forceinline__ int xcd_remap_x3(int orig, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+struct Split8 {
+    uint4 p[3];
+};
+
+__device__ __forceinline__ Split8 split8(const float4 &u, const float4 &v) {
+    const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+    bf16x8 h, m, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const __bf16 a = (__bf16)x[j];
+        const float r = x[j] - (float)a;
+        const __bf16 b = (__bf16)r;
+        const float r2 = r - (float)b;
+        h[j] = a;
+        m[j] = b;
+        l[j] = (__bf16)r2;
+    }
+    Split8 s;
+    s.p[0] = __builtin_bit_cast(uint4, h);
+    s.p[1] = __builtin_bit_cast(uint4, m);
+    s.p[2] = __builtin_bit_cast(uint4, l);
+    return s;
+}
+
+__global__ void split_bf16x3_kernel(const float *__restrict__ W, int rows, int cols, int ldw, __bf16 *__restrict__ out) {
+    const size_t n = (size_t)rows * cols;
+    const size_t plane = n;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / cols, c = i - r * cols;
+        const float x = W[r * ldw + c];
+        const __bf16 a = (__bf16)x;
+        const float res = x - (float)a;
+        const __bf16 b = (__bf16)res;
+        out[i] = a;
+        out[plane + i] = b;
+        out[2 * plane + i] = (__bf16)(res - (float)b);
+    }
+}
+
+// C[M,N] (+)= A[M,K] @ W^T + bias, W planes [3][N][K] bf16.  K % 16 == 0, lda % 4 == 0, A 16-B aligned.
+__global__ void __launch_bounds__(kX3T, 3)
+gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ Wp, float *__restrict__ C, int ldc,
+               const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
+    __shared__ uint4 lds[2][6][kX3Plane];  // [buf][A planes 0..2 | W planes 3..5], 48 KiB
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    const int m0 = (id / ntn) * kX3M, n0 = (id % ntn) * kX3M;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
+    const int srow = t >> 1, shalf = t & 1;  // staging: one row-half (8 k values) per thread
+    const float *arow = A + (size_t)min(m0 + srow, M - 1) * lda + 8 * shalf;
+    const size_t NK = (size_t)N * K;
+    const __bf16 *wrow = Wp + (size_t)min(n0 + srow, N - 1) * K + 8 * shalf;
+    f32x16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16v{};
+    const int ns = K / kX3D;
+    float4 a0, a1;
+    auto loadA = [&](int s) {
+        const float4 *p = reinterpret_cast<const float4 *>(arow + s * kX3D);
+        a0 = p[0];
+        a1 = p[1];
+    };
+    auto storeA = [&](int buf) {
+        const Split8 sp = split8(a0, a1);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) lds[buf][q][t] = sp.p[q];
+    };
+    auto issueW = [&](int s, int buf) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) glds16_async(wrow + q * NK + s * kX3D, &lds[buf][3 + q][w * 64]);
+    };
+    const int li = lane & 31, h = lane >> 5;
+    auto slab = [&](int buf) {
+        bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                fa[i][q] = __builtin_bit_cast(bf16x8, lds[buf][q][(wr + 32 * i + li) * 2 + h]);
+                fb[i][q] = __builtin_bit_cast(bf16x8, lds[buf][3 + q][(wc + 32 * i + li) * 2 + h]);
+            }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x16v c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+                acc[i][j] = c;
+            }
+    };
+    issueW(0, 0);
+    loadA(0);
+    storeA(0);
+    wait_vmcnt<0>();
+    barrier_lds();
+    for (int s = 0; s < ns; ++s) {
+        const int buf = s & 1;
+        const bool more = s + 1 < ns;
+        if (more) {
+            issueW(s + 1, buf ^ 1);
+            loadA(s + 1);
+        }
+        slab(buf);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) storeA(buf ^ 1);
+        wait_vmcnt<0>();
+        barrier_lds();
+    }
+    float *ldsf = reinterpret_cast<float *>(&lds[0][0][0]);
+    if (vec_out) {
+        // LDS-staged epilogue: each wave's 32x64 half-tile leaves as whole 256-byte rows of float4
+        float *stage = ldsf + w * 32 * 64;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg)
+                    stage[((reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)) * 64 + 32 * j + (lane & 31)] = acc[i][j][reg];
+            __syncthreads();
+            const int col = n0 + wc + (lane & 15) * 4;
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (bias && col < N) bv = *reinterpret_cast<const float4 *>(bias + col);
+#pragma unroll
+            for (int it = 0; it < 8; ++it) {
+                const int r = it * 4 + (lane >> 4);
+                const int row = m0 + wr + 32 * i + r;
+                float4 v = *reinterpret_cast<const float4 *>(stage + r * 64 + (lane & 15) * 4);
+                v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+                if (row < M && col < N) {
+                    float4 *c = reinterpret_cast<float4 *>(C + (size_t)row * ldc + col);
+                    if (accumulate) {
+                        const float4 o = *c;
+                        v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
+                    }
+                    *c = v;
+                }
+            }
+            __syncthreads();
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wc + 32 * j + (lane & 31);
+            if (col >= N) continue;
+            const float bv = bias ? bias[col] : 0.0f;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = m0 + wr + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+                if (row >= M) continue;
+                float *c = C + (size_t)row * ldc + col;
+                const float v = acc[i][j][reg] + bv;
+                *c = accumulate ? *c + v : v;
+            }
+        }
+}
+
+static bool a16x3(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace msat
+
+using namespace msat;
+
+extern "C" int msat_split_bf16x3(const float *W, int32_t rows, int32_t cols, int32_t ldw, void *planes, void *stream) {
+    if (rows == 0 || cols == 0) return MSAT_OK;
+    MSAT_REQUIRE(W && planes && rows > 0 && cols > 0 && ldw >= cols, "bad split_bf16x3 args");
+    const size_t n = (size_t)rows * cols;
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(split_bf16x3_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, W, rows, cols, ldw,
+                       reinterpret_cast<__bf16 *>(planes));
+    return check_launch("split_bf16x3_kernel");
+}
+
+extern "C" int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, float *C, int32_t ldc, const float *bias,
+                            int32_t M, int32_t N, int32_t K, int32_t accumulate, void *stream) {
+    if (M == 0) return MSAT_OK;
+    MSAT_REQUIRE(A && Wplanes && C && M > 0 && N > 0 && K > 0, "bad gemm_x3 args");
+    MSAT_REQUIRE(K % kX3D == 0 && lda % 4 == 0 && lda >= K && ldc >= N && a16x3(A) && a16x3(Wplanes) &&
+                     (K * 2) % 16 == 0,
+                 "gemm_x3: K %% 16, lda %% 4 and 16-byte aligned operands required");
+    const int ntm = (M + kX3M - 1) / kX3M, ntn = (N + kX3M - 1) / kX3M;
+    const int vec = (N % 4 == 0 && ldc % 4 == 0 && a16x3(C) && (!bias || a16x3(bias))) ? 1 : 0;
+    hipLaunchKernelGGL(gemm_x3_kernel, dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
+                       reinterpret_cast<const __bf16 *>(Wplanes), C, ldc, bias, M, N, K, accumulate, ntn, vec);
+    return check_launch("gemm_x3_kernel");
+}

@@ -114,6 +114,8 @@ def _load():
     sig["msat_assemble_graph_batch"] = (I, [I, I, I, I, I] + [P] * 26 + [I, I, P])
     sig["msat_clause_gather"] = (I, [P, I, P, P, I, I, I, I, P])
     sig["msat_var_gather"] = (I, [P, I, P, P, P, I, I, I, I, P])
+    sig["msat_split_bf16x3"] = (I, [P, I, I, I, P, P])
+    sig["msat_gemm_x3"] = (I, [P, I, P, P, I, P, I, I, I, I, P])
     sig["msat_clause_gather2"] = (I, [P, P, I, P, P, I, I, I, I, I, P])
     sig["msat_var_gather2"] = (I, [P, P, I, P, P, P, P, I, I, I, I, P])
     sig["msat_gru_ln_fwd"] = (I, [P, I, P, I, P, I, P, P, P, I, I, I, P])
@@ -157,6 +159,8 @@ EXPORTED = (
     "msat_assemble_graph_batch",
     "msat_clause_gather",
     "msat_var_gather",
+    "msat_split_bf16x3",
+    "msat_gemm_x3",
     "msat_clause_gather2",
     "msat_var_gather2",
     "msat_gru_ln_fwd",

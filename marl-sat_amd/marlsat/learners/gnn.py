@@ -129,6 +129,27 @@ class GNNActorCritic:
         GNNActorCritic.flops += 2 * M * N * K
         _chk(L_.msat_gemm(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, self.stream), "msat_gemm")
 
+    # fp32-accurate bf16x3 split GEMM for the backward's C (+)= dG @ W^T products (gemm_x3.hip)
+    use_x3 = os.environ.get("MARLSAT_GEMM_X3", "1") != "0"
+
+    def _split_weights(self, mats):
+        """bf16x3 planes of each (rows, 3H) weight block (once per backward): {key: planes tensor}."""
+        out = {}
+        for key, Wm in mats.items():
+            rows, cols = Wm.shape
+            buf = torch.empty(3 * rows * cols + 8, dtype=torch.int16, device=self.device)
+            _chk(L_.msat_split_bf16x3(Wm.data_ptr(), rows, cols, cols, buf.data_ptr(), self.stream), "split_bf16x3")
+            out[key] = buf
+        return out
+
+    def _dgrad(self, A, lda, Wm: torch.Tensor, planes, C, ldc, M, N, K, acc):
+        """C[M,N] (+)= A[M,K] @ Wm[:N]^T (Wm rows = N, row stride K)."""
+        if planes is None:
+            self._gemm(A, lda, Wm.data_ptr(), K, 1, C, ldc, None, M, N, K, acc)
+            return
+        GNNActorCritic.flops += 2 * M * N * K
+        _chk(L_.msat_gemm_x3(A, lda, planes.data_ptr(), C, ldc, None, M, N, K, acc, self.stream), "msat_gemm_x3")
+
     def _wgrad(self, A, lda, G, ldg, W, ldw, M, K, N, acc=1):
         if M == 0:
             return
@@ -303,6 +324,9 @@ class GNNActorCritic:
         ln, dln = self.p("enc.ln"), self.g("enc.ln")
         (Fc, Fp, Fn), (gFc, gFp, gFn) = self._fold_views()
         self._gF.zero_()
+        mats = {"wh_c": self.p("enc.gru_c_wh"), "wh_vp": self.p("enc.gru_vp_wh"), "wh_vn": self.p("enc.gru_vn_wh"),
+                "Fc": Fc[:2 * H], "Fp": Fp[:H], "Fn": Fn[:H]}
+        pl = self._split_weights(mats) if self.use_x3 else {k: None for k in mats}
         for l in range(self.L - 1, -1, -1):
             t = tape[l]
             dNV = e(Nv, 2 * H)
@@ -318,10 +342,12 @@ class GNNActorCritic:
                                            pp(self.g(f"enc.{cell}_bh"), 2 * H), part.data_ptr(), Nv, H, 1,
                                            self.stream), "gru_ln_bwd_g4")
                 wh, gwh = self.p(f"enc.{cell}_wh"), self.g(f"enc.{cell}_wh")
-                self._gemm(dGH.data_ptr(), W3, wh.data_ptr(), W3, 1, dHx0.data_ptr(), H, None, Nv, H, W3, 1)
+                sfx = cell[-2:]
+                self._dgrad(dGH.data_ptr(), W3, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1)
                 self._wgrad(Hx.data_ptr(), H, dGH.data_ptr(), W3, gwh.data_ptr(), W3, Nv, H, W3)
                 # input path: d(gathered) and dF rows [fold | x/svf | counts]
-                self._gemm(dGI.data_ptr(), W3, F.data_ptr(), W3, 1, pp(dNV, half * H), 2 * H, None, Nv, H, W3, 0)
+                self._dgrad(dGI.data_ptr(), W3, F, pl["Fp" if half == 0 else "Fn"], pp(dNV, half * H), 2 * H, Nv, H,
+                            W3, 0)
                 self._wgrad(pp(t.NV, half * H), 2 * H, dGI.data_ptr(), W3, gF.data_ptr(), W3, Nv, H, W3)
                 self._wgrad(b.vfeat.data_ptr(), 8, dGI.data_ptr(), W3, pp(gF[H]), W3, Nv, 8, W3)
                 dprev[half] = dHx0
@@ -337,11 +363,10 @@ class GNNActorCritic:
                                        pp(dln[3 * l]), pp(dln[3 * l], H), self.g("enc.gru_c_bi").data_ptr(),
                                        pp(self.g("enc.gru_c_bh"), 2 * H), part.data_ptr(), Nc, H, 1, self.stream),
                  "gru_ln_bwd_g4")
-            self._gemm(dGH.data_ptr(), W3, self.p("enc.gru_c_wh").data_ptr(), W3, 1, dHc0.data_ptr(), H, None,
-                       Nc, H, W3, 1)
+            self._dgrad(dGH.data_ptr(), W3, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1)
             self._wgrad(t.Hc.data_ptr(), H, dGH.data_ptr(), W3, self.g("enc.gru_c_wh").data_ptr(), W3, Nc, H, W3)
             dGIN = e(Nc, 2 * H)
-            self._gemm(dGI.data_ptr(), W3, Fc.data_ptr(), W3, 1, dGIN.data_ptr(), 2 * H, None, Nc, 2 * H, W3, 0)
+            self._dgrad(dGI.data_ptr(), W3, Fc, pl["Fc"], dGIN.data_ptr(), 2 * H, Nc, 2 * H, W3, 0)
             self._wgrad(t.GIN.data_ptr(), 2 * H, dGI.data_ptr(), W3, gFc.data_ptr(), W3, Nc, 2 * H, W3)
             self._wgrad(b.cdeg.data_ptr(), 4, dGI.data_ptr(), W3, pp(gFc[2 * H]), W3, Nc, 4, W3)
             # clause gather backward: dH_v+/- (+)= A+/- dGIN+/-

@@ -33,6 +33,13 @@ for M, N, K, tb, what in GEMMS:
     us = timeit(f)
     print(json.dumps({"what": "gemm " + what, "M": M, "N": N, "K": K, "us": round(us, 1),
                       "tflops": round(2 * M * N * K / us / 1e6, 1)}))
+    if tb:  # bf16x3 split GEMM on the same shape (weights pre-split)
+        planes = torch.empty(3 * N * K, dtype=torch.int16, device="cuda")
+        L.msat_split_bf16x3(B.data_ptr(), N, K, K, planes.data_ptr(), s)
+        f3 = lambda: L.msat_gemm_x3(A.data_ptr(), K, planes.data_ptr(), C.data_ptr(), N, 0, M, N, K, 1, s)
+        us = timeit(f3)
+        print(json.dumps({"what": "gemm_x3 " + what, "M": M, "N": N, "K": K, "us": round(us, 1),
+                          "tflops": round(2 * M * N * K / us / 1e6, 1)}))
     del A, B, C
 for M, K, N, what in WGRADS:
     A = torch.randn(M, K, device="cuda"); G = torch.randn(M, N, device="cuda"); W = torch.empty(K, N, device="cuda")

@@ -171,3 +171,31 @@ def test_colsum_deterministic(M, N, ld, off):
     bound = 2e-6 * (G[:, :N].double().abs().sum(0) if M else torch.zeros(N, dtype=torch.float64, device="cuda"))
     assert bool((err[oo:oo + N] <= bound + 1e-6).all())
     assert torch.equal(res[0][:oo], out0[:oo]) and torch.equal(res[0][oo + N:], out0[oo + N:])
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 4, 16), (130, 132, 64), (1000, 384, 384), (5000, 128, 384), (257, 256, 128),
+                                   (3, 7, 32)])
+def test_gemm_x3_fp32_accuracy(M, N, K):
+    """bf16x3 split GEMM: C = A @ W^T (+ bias, + C) at fp32 accuracy (same bound as the f32 MFMA
+    kernels: 2e-6 of sum |a b|), including values spanning many binades."""
+    from marlsat import _lib
+
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn(M, K, device="cuda", generator=g) * torch.exp2(torch.randint(-6, 7, (M, K), device="cuda",
+                                                                                generator=g).float())
+    W = torch.randn(N, K, device="cuda", generator=g)
+    bias = torch.randn(N, device="cuda", generator=g)
+    C0 = torch.randn(M, N, device="cuda", generator=g)
+    planes = torch.empty(3 * N * K + 8, dtype=torch.int16, device="cuda")
+    s = _lib.stream_ptr()
+    _lib.check(_lib.lib.msat_split_bf16x3(W.data_ptr(), N, K, K, planes.data_ptr(), s), "split")
+    hi, mid, lo = (planes[i * N * K:(i + 1) * N * K].view(torch.bfloat16).float().view(N, K) for i in range(3))
+    assert float(((hi.double() + mid.double() + lo.double()) - W.double()).abs().max()) <= \
+        2.0 ** -24 * float(W.abs().max())
+    for acc in (0, 1):
+        C = C0.clone()
+        _lib.check(_lib.lib.msat_gemm_x3(A.data_ptr(), K, planes.data_ptr(), C.data_ptr(), N, bias.data_ptr(), M, N,
+                                         K, acc, s), "gemm_x3")
+        ref = A.double() @ W.double().t() + bias.double() + (C0.double() if acc else 0)
+        absprod = A.double().abs() @ W.double().abs().t() + bias.double().abs() + (C0.double().abs() if acc else 0)
+        _ref_close(C, ref, absprod)
