@@ -100,6 +100,15 @@ int msat_gru_ln_fused_fwd(const float *x0, int32_t ld0, int32_t w0, const float 
                           const float *wi, const float *bi, const float *wh, const float *bh,
                           const float *ln_scale, const float *ln_bias, float *out, int32_t ldo, float *g4,
                           int32_t ldg, int32_t R, int32_t H, void *stream);
+/* Same cell with transposed weights wiT (3H, Kp) / whT (3H, H), Kp = Kx rounded up to 16 and
+ * zero-padded (msat_transpose_pad): k-major operand images read with ds_read_b128 fragments.
+ * H = 64 or 128. */
+int msat_transpose_pad(const float *W, int32_t K, int32_t N, int32_t ldw, float *out, int32_t Kp, void *stream);
+int msat_gru_ln_fused_fwd_t(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
+                            const float *x2, int32_t ld2, int32_t w2, const float *hprev, int32_t ldp,
+                            const float *wiT, const float *bi, const float *whT, const float *bh,
+                            const float *ln_scale, const float *ln_bias, float *out, int32_t ldo, float *g4,
+                            int32_t ldg, int32_t R, int32_t H, void *stream);
 /* msat_gru_ln_bwd from the fused forward's g4 tape (same outputs).  dbi (3H) / dbh_n (H), both
  * or neither, receive (+=) the gate-bias gradients sum_rows dGi and sum_rows dGh[:, 2H:3H]
  * (b_ir|b_iz|b_in and b_hn) from the same pass.  partial >= msat_gru_ln_bwd_partial_floats. */

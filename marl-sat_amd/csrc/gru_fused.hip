@@ -49,6 +49,69 @@ struct GruFwdArgs {
 
 __device__ __forceinline__ float fsig(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
+// GRU gate algebra + LayerNorm on the accumulators of a 64-row tile (shared by both kernels):
+// acc[rt][0..3] = [r_pre | z_pre | gin | ghn] (biases not yet added) for rows wrow + 32 rt + ...
+template <int NW, int RS>
+__device__ __forceinline__ void gru_ln_epilogue(const GruFwdArgs &a, f32x16 (&acc)[2 / RS][4], float *red_lds,
+                                                int row0, int wu, int wrow, int li, int lk) {
+    constexpr int H = 32 * NW, RT = 2 / RS;
+    const int u = 32 * wu + li;
+    const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
+    const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
+    float2 *red = reinterpret_cast<float2 *>(red_lds);  // [NW][64]
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int lr = wrow + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
+            const int row = row0 + lr;
+            const float rp = acc[rt][0][reg] + br, zp = acc[rt][1][reg] + bz;
+            const float gi = acc[rt][2][reg] + bni, gh = acc[rt][3][reg] + bnh;
+            float hv = 0.0f;
+            if (row < a.R) {
+                hv = a.hp[(size_t)row * a.ldp + u];
+                if (a.g4) {
+                    float *q = a.g4 + (size_t)row * a.ldg + u;
+                    q[0] = rp;
+                    q[H] = zp;
+                    q[2 * H] = gi;
+                    q[3 * H] = gh;
+                }
+            }
+            const float rg = fsig(rp), zg = fsig(zp);
+            const float ng = tanhf(gi + rg * gh);
+            const float hn = (1.0f - zg) * ng + zg * hv;
+            acc[rt][0][reg] = hn;
+            float s1 = hn, s2 = hn * hn;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                s1 += __shfl_xor(s1, o, 64);
+                s2 += __shfl_xor(s2, o, 64);
+            }
+            if (li == 0) red[wu * kFR + lr] = make_float2(s1, s2);
+        }
+    __syncthreads();
+    const float sc = a.ln_scale[u], lb = a.ln_bias[u];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int lr = wrow + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
+            const int row = row0 + lr;
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int v = 0; v < NW; ++v) {
+                const float2 p = red[v * kFR + lr];
+                s1 += p.x;
+                s2 += p.y;
+            }
+            const float mean = s1 / (float)H;
+            const float var = fmaxf(s2 / (float)H - mean * mean, 0.0f);
+            const float rs = rsqrtf(var + 1e-6f);
+            if (row < a.R) a.out[(size_t)row * a.ldo + u] = (acc[rt][0][reg] - mean) * (rs * sc) + lb;
+        }
+}
+
 // NW = H / 32 unit groups; RS = waves per unit group (row split of the 64-row tile): wave w
 // owns units [32 (w % NW), +32) of all four gates for rows [(w / NW) * 64 / RS, +64 / RS).
 template <int NW, int RS>
@@ -186,61 +249,171 @@ gru_ln_fused_fwd_kernel(GruFwdArgs a) {
     }
 
     // ---------------------------------------------------------------- epilogue --
-    const int u = 32 * wu + li;
-    const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
-    const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
-    float2 *red = reinterpret_cast<float2 *>(&As[0][0]);  // [NW][64] (As is free after the last sync)
+    gru_ln_epilogue<NW, RS>(a, acc, &As[0][0], row0, wu, wrow, li, lk);  // As is free after the last sync
+}
+
+// ---------------------------------------------------------------------------------------------
+// Transposed-weight form (msat_gru_ln_fused_fwd_t): the weights arrive as W^T [3H][Kp] (k
+// contiguous, zero-padded to a multiple of 16), so both operand slabs are k-major 16-deep images
+// [o][16] with the 16-byte chunk c of row o at slot c ^ ((o >> 2) & 3) (conflict-free
+// ds_read_b128).  A lane's float4 then covers four MFMA k steps (step 4q + r takes k = 8q + r on
+// lanes 0-31 and 8q + 4 + r on lanes 32-63, the same permutation on both operands), so a wave
+// reads each slab with (RT + 3) x 2 ds_read_b128 instead of 4 ds_read_b32 per k step.
+__device__ __forceinline__ int gswz(int o) { return (o >> 2) & 3; }
+
+template <int NW, int RS>
+__global__ void __launch_bounds__(64 * NW * RS, 2)
+gru_ln_fused_fwd_t_kernel(GruFwdArgs a) {
+    constexpr int H = 32 * NW, T = 64 * NW * RS, BW = 3 * H, RT = 2 / RS;
+    constexpr int AN = (kFR * kFK / 4 + T - 1) / T;  // float4 A chunks per thread
+    constexpr int BN = (BW * kFK / 4) / T;           // float4 B chunks per thread
+    static_assert((BW * kFK / 4) % T == 0, "B slab split");
+    __shared__ __attribute__((aligned(16))) float As[2][kFR * kFK];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BW * kFK];
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wu = w % NW, wrow = (w / NW) * (kFR / RS);
+    const int row0 = blockIdx.x * kFR;
+    const int nsh = H / kFK;
+    const int ns = nsh + (a.Kx + kFK - 1) / kFK;
+    const int kxp = (a.Kx + kFK - 1) / kFK * kFK;
+
+    float4 ra[AN];
+    auto loadA = [&](int s) {
+        const bool hid = s < nsh;
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+        for (int i = 0; i < AN; ++i) {
+            const int idx = t + i * T;
+            ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (idx < kFR * kFK / 4) {
+                const int r = row0 + (idx >> 2), kq = (idx & 3) * 4;
+                if (r < a.R) {
+                    const float *p = nullptr;
+                    if (hid) {
+                        p = a.hp + (size_t)r * a.ldp + s * kFK + kq;
+                    } else {
+                        int k = (s - nsh) * kFK + kq;
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int lr = wrow + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
-            const int row = row0 + lr;
-            const float rp = acc[rt][0][reg] + br, zp = acc[rt][1][reg] + bz;
-            const float gi = acc[rt][2][reg] + bni, gh = acc[rt][3][reg] + bnh;
-            float hv = 0.0f;
-            if (row < a.R) {
-                hv = a.hp[(size_t)row * a.ldp + u];
-                if (a.g4) {
-                    float *q = a.g4 + (size_t)row * a.ldg + u;
-                    q[0] = rp;
-                    q[H] = zp;
-                    q[2 * H] = gi;
-                    q[3 * H] = gh;
+                        for (int g = 0; g < 3; ++g) {
+                            if (!p && k < a.seg_w[g]) p = a.seg[g] + (size_t)r * a.seg_ld[g] + k;
+                            k -= a.seg_w[g];
+                        }
+                    }
+                    if (p) ra[i] = *reinterpret_cast<const float4 *>(p);
                 }
             }
-            const float rg = fsig(rp), zg = fsig(zp);
-            const float ng = tanhf(gi + rg * gh);
-            const float hn = (1.0f - zg) * ng + zg * hv;
-            acc[rt][0][reg] = hn;
-            float s1 = hn, s2 = hn * hn;
-#pragma unroll
-            for (int o = 1; o < 32; o <<= 1) {
-                s1 += __shfl_xor(s1, o, 64);
-                s2 += __shfl_xor(s2, o, 64);
-            }
-            if (li == 0) red[wu * kFR + lr] = make_float2(s1, s2);
         }
+    };
+    auto storeA = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AN; ++i) {
+            const int idx = t + i * T;
+            if (idx < kFR * kFK / 4) {
+                const int r = idx >> 2, c = idx & 3;
+                *reinterpret_cast<float4 *>(As[buf] + r * kFK + 4 * (c ^ gswz(r))) = ra[i];
+            }
+        }
+    };
+    auto issueB = [&](int s, int buf) {
+        const bool hid = s < nsh;
+        const float *W = hid ? a.wh : a.wi;  // transposed: [3H][H] / [3H][kxp]
+        const int ldk = hid ? H : kxp;
+        const int kb = hid ? s * kFK : (s - nsh) * kFK;
+#pragma unroll
+        for (int i = 0; i < BN; ++i) {
+            const int f = i * T + t;  // float4 slot of the image: row o = f >> 2, slot f & 3
+            const int o = f >> 2, c = (f & 3) ^ gswz(o);
+            glds16_async(W + (size_t)o * ldk + kb + 4 * c, Bs[buf] + 4 * (i * T + 64 * w));
+        }
+    };
+
+    f32x16 acc[RT][4];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[i][g] = f32x16{};
+
+    const int li = lane & 31, lk = lane >> 5;
+    auto slab = [&](int buf, bool hid) {
+        float4 af[2][RT], bf[2][3];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const int r = wrow + 32 * rt + li;
+                af[q][rt] = *reinterpret_cast<const float4 *>(As[buf] + r * kFK + 4 * ((2 * q + lk) ^ gswz(r)));
+            }
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                const int o = g * H + 32 * wu + li;
+                bf[q][g] = *reinterpret_cast<const float4 *>(Bs[buf] + o * kFK + 4 * ((2 * q + lk) ^ gswz(o)));
+            }
+        }
+#define MSAT_GSTEP(Q, C)                                                                                      \
+    for (int rt = 0; rt < RT; ++rt) {                                                                         \
+        acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[Q][rt].C, bf[Q][0].C, acc[rt][0], 0, 0, 0);      \
+        acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[Q][rt].C, bf[Q][1].C, acc[rt][1], 0, 0, 0);      \
+        if (hid) acc[rt][3] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[Q][rt].C, bf[Q][2].C, acc[rt][3], 0, 0, 0); \
+        else acc[rt][2] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[Q][rt].C, bf[Q][2].C, acc[rt][2], 0, 0, 0);     \
+    }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (q == 0) {
+                MSAT_GSTEP(0, x) MSAT_GSTEP(0, y) MSAT_GSTEP(0, z) MSAT_GSTEP(0, w)
+            } else {
+                MSAT_GSTEP(1, x) MSAT_GSTEP(1, y) MSAT_GSTEP(1, z) MSAT_GSTEP(1, w)
+            }
+        }
+#undef MSAT_GSTEP
+    };
+
+    issueB(0, 0);
+    loadA(0);
+    storeA(0);
+    wait_vmcnt<0>();
+    barrier_lds();
+    int buf = 0;
+    for (int s = 0; s < nsh; ++s) {
+        issueB(s + 1, buf ^ 1);
+        loadA(s + 1);
+        slab(buf, true);
+        __builtin_amdgcn_sched_barrier(0);
+        storeA(buf ^ 1);
+        wait_vmcnt<0>();
+        barrier_lds();
+        buf ^= 1;
+    }
+    for (int s = nsh; s < ns; ++s) {
+        const bool more = s + 1 < ns;
+        if (more) {
+            issueB(s + 1, buf ^ 1);
+            loadA(s + 1);
+        }
+        slab(buf, false);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) storeA(buf ^ 1);
+        wait_vmcnt<0>();
+        barrier_lds();
+        buf ^= 1;
+    }
+    gru_ln_epilogue<NW, RS>(a, acc, &As[0][0], row0, wu, wrow, li, lk);
+}
+
+// out[c][k] = k < K ? W[k][c] : 0 for c < N, k < Kp (weights -> transposed, zero-padded)
+__global__ void transpose_pad_kernel(const float *__restrict__ W, int K, int N, int ldw, float *__restrict__ out,
+                                     int Kp) {
+    __shared__ float tile[32][33];
+    const int k0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
+    for (int j = ty; j < 32; j += 8) {
+        const int k = k0 + j, c = c0 + tx;
+        tile[j][tx] = (k < K && c < N) ? W[(size_t)k * ldw + c] : 0.0f;
+    }
     __syncthreads();
-    const float sc = a.ln_scale[u], lb = a.ln_bias[u];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int lr = wrow + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
-            const int row = row0 + lr;
-            float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-            for (int v = 0; v < NW; ++v) {
-                const float2 p = red[v * kFR + lr];
-                s1 += p.x;
-                s2 += p.y;
-            }
-            const float mean = s1 / (float)H;
-            const float var = fmaxf(s2 / (float)H - mean * mean, 0.0f);
-            const float rs = rsqrtf(var + 1e-6f);
-            if (row < a.R) a.out[(size_t)row * a.ldo + u] = (acc[rt][0][reg] - mean) * (rs * sc) + lb;
-        }
+    for (int j = ty; j < 32; j += 8) {
+        const int c = c0 + j, k = k0 + tx;
+        if (c < N && k < Kp) out[(size_t)c * Kp + k] = tile[tx][j];
+    }
 }
 
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -307,4 +480,64 @@ extern "C" int msat_gru_ln_fused_fwd(const float *x0, int32_t ld0, int32_t w0, c
         hipLaunchKernelGGL((gru_ln_fused_fwd_kernel<8, 1>), grid, dim3(512), 0, s, a);
     }
     return check_launch("gru_ln_fused_fwd_kernel");
+}
+
+extern "C" int msat_transpose_pad(const float *W, int32_t K, int32_t N, int32_t ldw, float *out, int32_t Kp,
+                                  void *stream) {
+    if (K == 0 || N == 0) return MSAT_OK;
+    MSAT_REQUIRE(W && out && K > 0 && N > 0 && ldw >= N && Kp >= K, "bad transpose_pad args");
+    const dim3 grid((Kp + 31) / 32, (N + 31) / 32);
+    hipLaunchKernelGGL(transpose_pad_kernel, grid, dim3(256), 0, (hipStream_t)stream, W, K, N, ldw, out, Kp);
+    return check_launch("transpose_pad_kernel");
+}
+
+extern "C" int msat_gru_ln_fused_fwd_t(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1,
+                                       int32_t w1, const float *x2, int32_t ld2, int32_t w2, const float *hprev,
+                                       int32_t ldp, const float *wiT, const float *bi, const float *whT,
+                                       const float *bh, const float *ln_scale, const float *ln_bias, float *out,
+                                       int32_t ldo, float *g4, int32_t ldg, int32_t R, int32_t H, void *stream) {
+    MSAT_REQUIRE(H == 64 || H == 128, "gru_ln_fused_fwd_t: H must be 64 or 128 (got %d)", H);
+    MSAT_REQUIRE(R >= 0, "gru_ln_fused_fwd_t: R < 0");
+    if (R == 0) return MSAT_OK;
+    MSAT_REQUIRE(x0 && hprev && wiT && bi && whT && bh && ln_scale && ln_bias && out, "NULL pointer");
+    MSAT_REQUIRE(ldo >= H && ldp >= H && (!g4 || ldg >= 4 * H), "gru_ln_fused_fwd_t: bad dims");
+    const float *seg[3] = {x0, x1, x2};
+    const int lds_[3] = {ld0, ld1, ld2}, ws[3] = {w0, w1, w2};
+    int Kx = 0;
+    for (int g = 0; g < 3; ++g) {
+        MSAT_REQUIRE(ws[g] >= 0 && ws[g] % 4 == 0, "gru_ln_fused_fwd_t: segment %d width %d must be a multiple of 4",
+                     g, ws[g]);
+        if (ws[g] == 0) continue;
+        MSAT_REQUIRE(seg[g] && aligned16(seg[g]) && lds_[g] % 4 == 0 && lds_[g] >= ws[g],
+                     "gru_ln_fused_fwd_t: segment %d must be 16-byte aligned with ld %% 4 == 0", g);
+        Kx += ws[g];
+    }
+    MSAT_REQUIRE(Kx > 0 && w0 > 0, "gru_ln_fused_fwd_t: empty input");
+    MSAT_REQUIRE(aligned16(hprev) && ldp % 4 == 0 && aligned16(wiT) && aligned16(whT),
+                 "gru_ln_fused_fwd_t: hprev / weights must be 16-byte aligned");
+    GruFwdArgs a;
+    for (int g = 0; g < 3; ++g) {
+        a.seg[g] = ws[g] ? seg[g] : nullptr;
+        a.seg_ld[g] = lds_[g];
+        a.seg_w[g] = ws[g];
+    }
+    a.hp = hprev;
+    a.ldp = ldp;
+    a.wi = wiT;
+    a.bi = bi;
+    a.wh = whT;
+    a.bh = bh;
+    a.ln_scale = ln_scale;
+    a.ln_bias = ln_bias;
+    a.out = out;
+    a.ldo = ldo;
+    a.g4 = g4;
+    a.ldg = ldg;
+    a.R = R;
+    a.Kx = Kx;
+    const dim3 grid((R + kFR - 1) / kFR);
+    hipStream_t s = (hipStream_t)stream;
+    if (H == 64) hipLaunchKernelGGL((gru_ln_fused_fwd_t_kernel<2, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((gru_ln_fused_fwd_t_kernel<4, 2>), grid, dim3(512), 0, s, a);
+    return check_launch("gru_ln_fused_fwd_t_kernel");
 }

@@ -114,12 +114,14 @@ def _load():
     sig["msat_assemble_graph_batch"] = (I, [I, I, I, I, I] + [P] * 26 + [I, I, P])
     sig["msat_clause_gather"] = (I, [P, I, P, P, I, I, I, I, P])
     sig["msat_var_gather"] = (I, [P, I, P, P, P, I, I, I, I, P])
+    sig["msat_transpose_pad"] = (I, [P, I, I, I, P, I, P])
     sig["msat_split_bf16x3"] = (I, [P, I, I, I, P, P])
     sig["msat_gemm_x3"] = (I, [P, I, P, P, I, P, I, I, I, I, P])
     sig["msat_clause_gather2"] = (I, [P, P, I, P, P, I, I, I, I, I, P])
     sig["msat_var_gather2"] = (I, [P, P, I, P, P, P, P, I, I, I, I, P])
     sig["msat_gru_ln_fwd"] = (I, [P, I, P, I, P, I, P, P, P, I, I, I, P])
     sig["msat_gru_ln_fused_fwd"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, P, P, P, P, P, P, I, P, I, I, I, P])
+    sig["msat_gru_ln_fused_fwd_t"] = sig["msat_gru_ln_fused_fwd"]
     sig["msat_gru_ln_bwd_g4"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, I, P])
     sig["msat_gru_ln_bwd_partial_floats"] = (Z, [I, I])
     sig["msat_gru_ln_bwd"] = (I, [P, I, P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, I, I, I, P])
@@ -159,6 +161,8 @@ EXPORTED = (
     "msat_assemble_graph_batch",
     "msat_clause_gather",
     "msat_var_gather",
+    "msat_transpose_pad",
+    "msat_gru_ln_fused_fwd_t",
     "msat_split_bf16x3",
     "msat_gemm_x3",
     "msat_clause_gather2",

@@ -163,15 +163,29 @@ class GNNActorCritic:
         ws = self.scr.get_part(int(L_.msat_colsum_workspace_floats(M, N)))
         _chk(L_.msat_colsum(G, ldg, M, N, out, acc, ws.data_ptr(), self.stream), "msat_colsum")
 
+    # transposed-weight GRU kernel (k-major images, ds_read_b128 fragments): measured equal to the
+    # [K][3H] form (profiles/gru_bench.py: 855-3060 vs 888-3049 us) plus the per-forward transposes,
+    # so it is opt-in (MARLSAT_GRU_T=1)
+    use_gru_t = os.environ.get("MARLSAT_GRU_T", "0") == "1"
+
     def _gru(self, cell: str, segs, hprev: torch.Tensor, ln_row: torch.Tensor, out: torch.Tensor,
-             g4: Optional[torch.Tensor], R: int, wi: Optional[torch.Tensor] = None):
+             g4: Optional[torch.Tensor], R: int, wi: Optional[torch.Tensor] = None, wt=None):
         """One fused GRU cell + LayerNorm (msat_gru_ln_fused_fwd): segs = [(ptr, ld, width)] of x;
-        wi overrides the cell's input matrix (the phi-folded matrices of the fused encoder)."""
+        wi overrides the cell's input matrix (the phi-folded matrices of the fused encoder);
+        wt = (wiT, whT) selects the transposed-weight kernel."""
         H = self.H
         segs = list(segs) + [(0, 0, 0)] * (3 - len(segs))
         kx = sum(w for _, _, w in segs)
         GNNActorCritic.flops += 2 * R * 3 * H * (H + (kx + 15) // 16 * 16)
         (p0, l0, w0), (p1, l1, w1), (p2, l2, w2) = segs
+        if wt is not None:
+            _chk(L_.msat_gru_ln_fused_fwd_t(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
+                                            wt[0].data_ptr(), self.p(f"enc.{cell}_bi").data_ptr(),
+                                            wt[1].data_ptr(), self.p(f"enc.{cell}_bh").data_ptr(),
+                                            self._ptr(ln_row), self._ptr(ln_row, H), out.data_ptr(), H,
+                                            g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
+                 "msat_gru_ln_fused_fwd_t")
+            return
         _chk(L_.msat_gru_ln_fused_fwd(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
                                       (self.p(f"enc.{cell}_wi") if wi is None else wi).data_ptr(),
                                       self.p(f"enc.{cell}_bi").data_ptr(),
@@ -281,6 +295,17 @@ class GNNActorCritic:
             self._wgrad(pp(bv, half * H), H, pp(gF[H + 4 + half]), W3, gwi.data_ptr(), W3, 1, H, W3)
             self._colsum(pp(gF[H]), 4 * W3, 1, 4 * W3, pp(gwi[H]))  # the x / svf rows map 1:1
 
+    def _transposed_weights(self, mats):
+        """{key: (K, 3H) matrix} -> {key: (3H, Kp) transposed, zero-padded to Kp = K rounded up to 16}."""
+        out = {}
+        for key, Wm in mats.items():
+            K, N = Wm.shape
+            Kp = (K + 15) // 16 * 16
+            T = torch.empty((N, Kp), dtype=torch.float32, device=self.device)
+            _chk(L_.msat_transpose_pad(Wm.data_ptr(), K, N, N, T.data_ptr(), Kp, self.stream), "transpose_pad")
+            out[key] = T
+        return out
+
     def _encode_fused(self, b: GraphBatch, save: bool):
         H, dev = self.H, self.device
         Nv, Nc = b.Nv, b.Nc
@@ -288,6 +313,11 @@ class GNNActorCritic:
         pp = self._ptr
         self._fold_weights()
         (Fc, Fp, Fn), _ = self._fold_views()
+        wt = {"gru_c": None, "gru_vp": None, "gru_vn": None}
+        if self.use_gru_t and H in (64, 128):
+            T = self._transposed_weights({"c": Fc, "vp": Fp, "vn": Fn, "hc": self.p("enc.gru_c_wh"),
+                                          "hvp": self.p("enc.gru_vp_wh"), "hvn": self.p("enc.gru_vn_wh")})
+            wt = {"gru_c": (T["c"], T["hc"]), "gru_vp": (T["vp"], T["hvp"]), "gru_vn": (T["vn"], T["hvn"])}
         Hp, Hn, Hc = self._embed(b)
         tape: List[StepTape] = []
         ln = self.p("enc.ln")
@@ -298,7 +328,7 @@ class GNNActorCritic:
             Hc1 = e(Nc, H)
             G4c = e(Nc, 4 * H) if save else None
             self._gru("gru_c", [(GIN.data_ptr(), 2 * H, 2 * H), (b.cdeg.data_ptr(), 4, 4)], Hc, ln[3 * l], Hc1, G4c,
-                      Nc, wi=Fc)
+                      Nc, wi=Fc, wt=wt["gru_c"])
             NV = e(Nv, 2 * H)  # [A+ H_c | A- H_c]
             _chk(L_.msat_var_gather2(Hc1.data_ptr(), Hc1.data_ptr(), H, b.ptr.data_ptr(), b.inc.data_ptr(),
                                      NV.data_ptr(), pp(NV, H), 2 * H, Nv, H, 0, self.stream), "var_gather2")
@@ -308,7 +338,7 @@ class GNNActorCritic:
                 G4 = e(Nv, 4 * H) if save else None
                 # input [n_v | x | svf | n+ n- 0 0] against F rows [fold | Wi x/svf | count rows]
                 self._gru(cell, [(pp(NV, half * H), 2 * H, H), (b.vfeat.data_ptr(), 8, 8)], Hx, ln[k], Hx1, G4, Nv,
-                          wi=F)
+                          wi=F, wt=wt[cell])
                 outs.append((G4, Hx1))
             if save:
                 tape.append(StepTape(Hp, Hn, Hc, GIN, G4c, NV, outs[0][0], outs[1][0]))

@@ -24,13 +24,24 @@ for kind, R, segs_w, segs_ld in (("var", 407000, (H, 8), (2 * H, 8)), ("clause",
     for x, w in zip(X, segs_w):
         args += [x.data_ptr(), x.shape[1], w]
     args += [0, 0, 0] * (3 - len(segs_w))
+    Kp = (Kx + 15) // 16 * 16
+    wiT = torch.empty(3 * H, Kp, device="cuda"); whT = torch.empty(3 * H, H, device="cuda")
+    _lib.lib.msat_transpose_pad(wi.data_ptr(), Kx, 3 * H, 3 * H, wiT.data_ptr(), Kp, _lib.stream_ptr())
+    _lib.lib.msat_transpose_pad(wh.data_ptr(), H, 3 * H, 3 * H, whT.data_ptr(), H, _lib.stream_ptr())
     for tape in (False, True):
-        for rs in ("1", "2"):
-            os.environ["MARLSAT_GRU_RS"] = rs
-            f = lambda: _lib.lib.msat_gru_ln_fused_fwd(*args, h.data_ptr(), H, wi.data_ptr(), bi.data_ptr(),
-                                                       wh.data_ptr(), bh.data_ptr(), sc.data_ptr(), lb.data_ptr(),
-                                                       out.data_ptr(), H, g4.data_ptr() if tape else 0, 4 * H, R, H,
-                                                       _lib.stream_ptr())
+        for rs in ("1", "2", "t"):
+            os.environ["MARLSAT_GRU_RS"] = rs if rs != "t" else "2"
+            if rs == "t":
+                f = lambda: _lib.lib.msat_gru_ln_fused_fwd_t(*args, h.data_ptr(), H, wiT.data_ptr(), bi.data_ptr(),
+                                                             whT.data_ptr(), bh.data_ptr(), sc.data_ptr(),
+                                                             lb.data_ptr(), out.data_ptr(), H,
+                                                             g4.data_ptr() if tape else 0, 4 * H, R, H,
+                                                             _lib.stream_ptr())
+            else:
+                f = lambda: _lib.lib.msat_gru_ln_fused_fwd(*args, h.data_ptr(), H, wi.data_ptr(), bi.data_ptr(),
+                                                           wh.data_ptr(), bh.data_ptr(), sc.data_ptr(), lb.data_ptr(),
+                                                           out.data_ptr(), H, g4.data_ptr() if tape else 0, 4 * H, R,
+                                                           H, _lib.stream_ptr())
             f(); torch.cuda.synchronize()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()

@@ -34,6 +34,18 @@ def _setup(R, H, kind, seed):
         segs = [(NV, H, 2 * H, H), (vf, 0, 4, 4)]  # (tensor, col offset, ld, width)
         x = torch.cat([NV[:, H:], vf], 1)
         Kx = H + 4
+    elif kind == "var8":  # fused encoder: [gathered half | x, svf, n+, n-, 0, 0]
+        NV = rnd(R, 2 * H)
+        vf = rnd(R, 8)
+        segs = [(NV, 0, 2 * H, H), (vf, 0, 8, 8)]
+        x = torch.cat([NV[:, :H], vf], 1)
+        Kx = H + 8
+    elif kind == "clause4":  # fused encoder: [gathered (2H) | n+, n-, 0, 0]
+        GIN = rnd(R, 2 * H)
+        cd = rnd(R, 4)
+        segs = [(GIN, 0, 2 * H, 2 * H), (cd, 0, 4, 4)]
+        x = torch.cat([GIN, cd], 1)
+        Kx = 2 * H + 4
     else:
         GIN = rnd(R, 2 * H)
         segs = [(GIN, 0, 2 * H, 2 * H)]
@@ -49,13 +61,34 @@ def _setup(R, H, kind, seed):
     return segs, x, h, wi, bi, wh, bh, sc, lb
 
 
-def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4):
+def _transposed(W):
+    """msat_transpose_pad: W (K, N) -> W^T (N, Kp) zero-padded to Kp = K rounded up to 16."""
+    from marlsat import _lib
+
+    K, N = W.shape
+    Kp = (K + 15) // 16 * 16
+    out = torch.full((N, Kp), float("nan"), device="cuda")
+    _lib.check(_lib.lib.msat_transpose_pad(W.data_ptr(), K, N, N, out.data_ptr(), Kp, _lib.stream_ptr()),
+               "transpose_pad")
+    return out
+
+
+def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
     from marlsat import _lib
 
     out = torch.empty(R, H, device="cuda")
     args = []
     for t, off, ld, w in segs + [(None, 0, 0, 0)] * (3 - len(segs)):
         args += [t.data_ptr() + 4 * off if t is not None else 0, ld, w]
+    if layout == "t":  # transposed-weight kernel (k-major images, ds_read_b128 fragments)
+        wiT, whT = _transposed(wi), _transposed(wh)
+        assert bool((wiT[:, wi.shape[0]:] == 0).all()) and torch.equal(wiT[:, :wi.shape[0]], wi.t())
+        _lib.check(_lib.lib.msat_gru_ln_fused_fwd_t(*args, h.data_ptr(), H, wiT.data_ptr(), bi.data_ptr(),
+                                                    whT.data_ptr(), bh.data_ptr(), sc.data_ptr(), lb.data_ptr(),
+                                                    out.data_ptr(), H, g4.data_ptr() if g4 is not None else 0, 4 * H,
+                                                    R, H, _lib.stream_ptr()), "gru_ln_fused_fwd_t")
+        torch.cuda.synchronize()
+        return out
     _lib.check(_lib.lib.msat_gru_ln_fused_fwd(*args, h.data_ptr(), H, wi.data_ptr(), bi.data_ptr(), wh.data_ptr(),
                                               bh.data_ptr(), sc.data_ptr(), lb.data_ptr(), out.data_ptr(), H,
                                               g4.data_ptr() if g4 is not None else 0, 4 * H, R, H,
@@ -63,16 +96,19 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4):
     return out
 
 
+@pytest.mark.parametrize("layout", ["plain", "t"])
 @pytest.mark.parametrize("R", [0, 1, 77, 1000, 70000])
 @pytest.mark.parametrize("H", [64, 128, 256])
-@pytest.mark.parametrize("kind", ["var", "clause"])
-def test_fused_forward_matches_reference(R, H, kind):
+@pytest.mark.parametrize("kind", ["var", "clause", "var8", "clause4"])
+def test_fused_forward_matches_reference(R, H, kind, layout):
     if R == 70000 and H != 128:
         pytest.skip("large case at the production width only")
+    if layout == "t" and H == 256:
+        pytest.skip("transposed-weight kernel: H 64 / 128")
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=R + H)
     g4 = torch.full((R, 4 * H), float("nan"), device="cuda")
-    out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4)
-    out_nt = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, None)  # inference form (no tape)
+    out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout)
+    out_nt = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, None, layout)  # inference form (no tape)
     torch.cuda.synchronize()
     assert torch.equal(out, out_nt)
     if R == 0:
