@@ -13,7 +13,8 @@
 // (msat_split_bf16x3, once per weight update).  The activation operand A is split while it is
 // staged: global fp32 -> registers -> three bf16 planes in LDS; the weight planes arrive by
 // LDS-DMA.  128x128 tile per 256-thread workgroup (wave = 64x64 = 2x2 MFMA tiles), 16-deep slabs,
-// double-buffered (slab s+1 lands while slab s is multiplied).
+// double-buffered in LDS, A prefetched two slabs ahead in registers (the six bf16 MFMAs of a slab
+// are too short to cover an HBM load issued one slab ahead).
 #include <stdlib.h>
 
 #include <algorithm>
@@ -94,14 +95,18 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16v{};
     const int ns = K / kX3D;
-    float4 a0, a1;
-    auto loadA = [&](int s) {
+    // A is prefetched two slabs ahead in registers (slots R0 / R1 by slab parity), the weight planes
+    // one slab ahead by LDS-DMA.  Per slab s: issue W(s+1), then load A(s+2) (so waiting for W(s+1)
+    // never waits for A(s+2): vector-memory counts retire in issue order), multiply slab s, split
+    // and store A(s+1), barrier.
+    float4 R0[2], R1[2];
+    auto loadA = [&](int s, float4 (&r)[2]) {
         const float4 *p = reinterpret_cast<const float4 *>(arow + s * kX3D);
-        a0 = p[0];
-        a1 = p[1];
+        r[0] = p[0];
+        r[1] = p[1];
     };
-    auto storeA = [&](int buf) {
-        const Split8 sp = split8(a0, a1);
+    auto storeA = [&](const float4 (&r)[2], int buf) {
+        const Split8 sp = split8(r[0], r[1]);
 #pragma unroll
         for (int q = 0; q < 3; ++q) lds[buf][q][t] = sp.p[q];
     };
@@ -133,23 +138,31 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
                 acc[i][j] = c;
             }
     };
+    loadA(0, R0);
+    if (ns > 1) loadA(1, R1);
     issueW(0, 0);
-    loadA(0);
-    storeA(0);
+    storeA(R0, 0);
     wait_vmcnt<0>();
     barrier_lds();
-    for (int s = 0; s < ns; ++s) {
+    if (ns > 2) loadA(2, R0);
+    // Rn holds A(s+1); Rf is free and receives A(s+2)
+    auto iter = [&](int s, float4 (&Rn)[2], float4 (&Rf)[2]) {
         const int buf = s & 1;
         const bool more = s + 1 < ns;
-        if (more) {
-            issueW(s + 1, buf ^ 1);
-            loadA(s + 1);
-        }
+        if (more) issueW(s + 1, buf ^ 1);
+        if (s >= 1 && s + 2 < ns) loadA(s + 2, Rf);  // s = 0: A(2) was issued in the prologue
         slab(buf);
         __builtin_amdgcn_sched_barrier(0);
-        if (more) storeA(buf ^ 1);
-        wait_vmcnt<0>();
+        if (more) storeA(Rn, buf ^ 1);
+        // W(s+1) and A(s+1) landed; A(s+2) (issued after W(s+1) for s >= 1) may fly.  At s = 0,
+        // A(2) precedes W(1) in issue order, so the wait drains everything.
+        if (s >= 1 && s + 2 < ns) wait_vmcnt<2>();
+        else wait_vmcnt<0>();
         barrier_lds();
+    };
+    for (int s = 0; s < ns; s += 2) {
+        iter(s, R1, R0);
+        if (s + 1 < ns) iter(s + 1, R0, R1);
     }
     float *ldsf = reinterpret_cast<float *>(&lds[0][0][0]);
     if (vec_out) {
