@@ -111,7 +111,9 @@ int msat_gru_ln_fused_fwd_t(const float *x0, int32_t ld0, int32_t w0, const floa
                             int32_t ldg, int32_t R, int32_t H, void *stream);
 /* msat_gru_ln_bwd from the fused forward's g4 tape (same outputs).  dbi (3H) / dbh_n (H), both
  * or neither, receive (+=) the gate-bias gradients sum_rows dGi and sum_rows dGh[:, 2H:3H]
- * (b_ir|b_iz|b_in and b_hn) from the same pass.  partial >= msat_gru_ln_bwd_partial_floats. */
+ * (b_ir|b_iz|b_in and b_hn) from the same pass.  partial >= msat_gru_ln_bwd_partial_floats.
+ * accumulate_ln: bit 0 accumulates the LN grads (else overwrites them); bit 1 overwrites dhprev
+ * (its prior contents are never read) instead of accumulating into it. */
 int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
                        int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
                        float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *dbi, float *dbh_n,

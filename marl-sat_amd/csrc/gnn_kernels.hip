@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(kRowThreads)
 gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
                   const float *__restrict__ scale, float *__restrict__ dGi, int lddi, float *__restrict__ dGh, int lddh,
-                  float *__restrict__ dh, int lddh_prev, float *__restrict__ part, int R, int H) {
+                  float *__restrict__ dh, int lddh_prev, float *__restrict__ part, int R, int H, int dh_assign) {
     __shared__ float s_part[4][NQ * 64 * PER];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     float pq[NQ][PER];
@@ -205,7 +205,8 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
             dhh[j] = dar;
             dhh[H + j] = daz;
             dhh[2 * H + j] = dan * rg[u];
-            dh[(size_t)r * lddh_prev + j] += dhn * zg[u];
+            float *dhp = dh + (size_t)r * lddh_prev + j;
+            *dhp = dh_assign ? dhn * zg[u] : *dhp + dhn * zg[u];
             if constexpr (NQ == 6) {
                 pq[2][u] += dar;
                 pq[3][u] += daz;
@@ -536,9 +537,9 @@ extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, in
     hipStream_t s = (hipStream_t)stream;
     const int nb = bwd_blocks(R);
     const dim3 g(nb), b(kRowThreads);
-    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
-    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
-    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0);
+    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0);
+    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0);
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
     return reduce_partials(partial, nb, 2 * H, dln_scale, accumulate_ln, partial + (size_t)nb * 2 * H, s);
@@ -559,14 +560,16 @@ extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4,
     const int nb = bwd_blocks(R);
     const dim3 g(nb), b(kRowThreads);
     const bool bias = dbi != nullptr;
+    const int dh_assign = (accumulate_ln >> 1) & 1;  // bit 1: dhprev = ..., else dhprev += ...
+    accumulate_ln &= 1;
     const int NQ = bias ? 6 : 2;
 #define MSAT_BWD(PER)                                                                                              \
     if (bias)                                                                                                      \
         hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, 6>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,    \
-                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);                           \
+                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign);                \
     else                                                                                                           \
         hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, 2>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,    \
-                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H);
+                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign);
     if (H == 64) { MSAT_BWD(1) }
     else if (H == 128) { MSAT_BWD(2) }
     else { MSAT_BWD(4) }

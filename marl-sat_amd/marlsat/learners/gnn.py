@@ -364,12 +364,12 @@ class GNNActorCritic:
             for half, cell, Hx, G4, dHx, k, F, gF in ((0, "gru_vp", t.Hp, t.G4p, dHp, 3 * l + 1, Fp, gFp),
                                                      (1, "gru_vn", t.Hn, t.G4n, dHn, 3 * l + 2, Fn, gFn)):
                 dGI, dGH = e(Nv, W3), e(Nv, W3)
-                dHx0 = torch.zeros((Nv, H), dtype=torch.float32, device=dev)
+                dHx0 = e(Nv, H)  # written (not accumulated) by the backward kernel: flags bit 1
                 part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nv, H)))
                 _chk(L_.msat_gru_ln_bwd_g4(dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, pp(ln[k]),
                                            dGI.data_ptr(), W3, dGH.data_ptr(), W3, dHx0.data_ptr(), H,
                                            pp(dln[k]), pp(dln[k], H), self.g(f"enc.{cell}_bi").data_ptr(),
-                                           pp(self.g(f"enc.{cell}_bh"), 2 * H), part.data_ptr(), Nv, H, 1,
+                                           pp(self.g(f"enc.{cell}_bh"), 2 * H), part.data_ptr(), Nv, H, 3,
                                            self.stream), "gru_ln_bwd_g4")
                 wh, gwh = self.p(f"enc.{cell}_wh"), self.g(f"enc.{cell}_wh")
                 sfx = cell[-2:]
@@ -386,12 +386,12 @@ class GNNActorCritic:
                                         H, 1, 1, self.stream), "clause_gather2")
             # clause GRU
             dGI, dGH = e(Nc, W3), e(Nc, W3)
-            dHc0 = torch.zeros((Nc, H), dtype=torch.float32, device=dev)
+            dHc0 = e(Nc, H)
             part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nc, H)))
             _chk(L_.msat_gru_ln_bwd_g4(dHc.data_ptr(), H, t.G4c.data_ptr(), 4 * H, t.Hc.data_ptr(), H, pp(ln[3 * l]),
                                        dGI.data_ptr(), W3, dGH.data_ptr(), W3, dHc0.data_ptr(), H,
                                        pp(dln[3 * l]), pp(dln[3 * l], H), self.g("enc.gru_c_bi").data_ptr(),
-                                       pp(self.g("enc.gru_c_bh"), 2 * H), part.data_ptr(), Nc, H, 1, self.stream),
+                                       pp(self.g("enc.gru_c_bh"), 2 * H), part.data_ptr(), Nc, H, 3, self.stream),
                  "gru_ln_bwd_g4")
             self._dgrad(dGH.data_ptr(), W3, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1)
             self._wgrad(t.Hc.data_ptr(), H, dGH.data_ptr(), W3, self.g("enc.gru_c_wh").data_ptr(), W3, Nc, H, W3)

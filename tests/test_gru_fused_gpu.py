@@ -126,8 +126,9 @@ def test_fused_forward_matches_reference(R, H, kind, layout):
     assert bool((terr <= 2e-6 * ab + 1e-30).all()), float((terr / (ab + 1e-30)).max())
 
 
+@pytest.mark.parametrize("assign", [False, True])  # flags bit 1: dhprev overwritten, never read
 @pytest.mark.parametrize("R,H", [(77, 64), (1000, 128), (300, 256)])
-def test_g4_backward_matches_autograd(R, H):
+def test_g4_backward_matches_autograd(R, H, assign):
     from marlsat import _lib
 
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, "var", seed=7 * R + H)
@@ -136,7 +137,7 @@ def test_g4_backward_matches_autograd(R, H):
     dy = torch.randn(R, H, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
     dGi = torch.empty(R, 3 * H, device="cuda")
     dGh = torch.empty(R, 3 * H, device="cuda")
-    dh = torch.zeros(R, H, device="cuda")
+    dh = torch.full((R, H), float("nan"), device="cuda") if assign else torch.zeros(R, H, device="cuda")
     dln = torch.zeros(2 * H, device="cuda")
     dbi = torch.full((3 * H,), 0.5, device="cuda")  # accumulated into
     dbh = torch.full((3 * H,), 0.5, device="cuda")
@@ -144,7 +145,7 @@ def test_g4_backward_matches_autograd(R, H):
     _lib.check(_lib.lib.msat_gru_ln_bwd_g4(dy.data_ptr(), H, g4.data_ptr(), 4 * H, h.data_ptr(), H, sc.data_ptr(),
                                            dGi.data_ptr(), 3 * H, dGh.data_ptr(), 3 * H, dh.data_ptr(), H,
                                            dln.data_ptr(), dln.data_ptr() + 4 * H, dbi.data_ptr(),
-                                           dbh.data_ptr() + 4 * 2 * H, part.data_ptr(), R, H, 1,
+                                           dbh.data_ptr() + 4 * 2 * H, part.data_ptr(), R, H, 3 if assign else 1,
                                            _lib.stream_ptr()), "gru_ln_bwd_g4")
     torch.cuda.synchronize()
     # autograd through the float64 reference w.r.t. gi, gh (pre-activation gate vectors), h, LN params
