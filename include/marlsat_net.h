@@ -30,6 +30,9 @@ int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ldb, int32_t 
  * msat_gemm_x3: C[M,N] (+)= A[M,K] @ W^T (+ bias), W [N][K] given as its split planes;
  *   K % 16 == 0, lda % 4 == 0, 16-byte aligned A / planes. */
 int msat_split_bf16x3(const float *W, int32_t rows, int32_t cols, int32_t ldw, void *planes, void *stream);
+/* the same with the columns rotated: planes[q][r][c] = part q of W[r][(c + rot) % cols] */
+int msat_split_bf16x3_rot(const float *W, int32_t rows, int32_t cols, int32_t ldw, int32_t rot, void *planes,
+                          void *stream);
 int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, float *C, int32_t ldc, const float *bias,
                  int32_t M, int32_t N, int32_t K, int32_t accumulate, void *stream);
 
@@ -113,7 +116,9 @@ int msat_gru_ln_fused_fwd_t(const float *x0, int32_t ld0, int32_t w0, const floa
  * or neither, receive (+=) the gate-bias gradients sum_rows dGi and sum_rows dGh[:, 2H:3H]
  * (b_ir|b_iz|b_in and b_hn) from the same pass.  partial >= msat_gru_ln_bwd_partial_floats.
  * accumulate_ln: bit 0 accumulates the LN grads (else overwrites them); bit 1 overwrites dhprev
- * (its prior contents are never read) instead of accumulating into it. */
+ * (its prior contents are never read) instead of accumulating into it; bit 2 packs each row as
+ * [dan | dar | daz | dan*r] (4H, dGh = dGi + H, lddi = lddh >= 4H): dGi is then in gate order
+ * (n, r, z) and the r / z columns are written once for both. */
 int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
                        int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
                        float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *dbi, float *dbh_n,

@@ -61,12 +61,15 @@ __device__ __forceinline__ Split8 split8(const float4 &u, const float4 &v) {
     return s;
 }
 
-__global__ void split_bf16x3_kernel(const float *__restrict__ W, int rows, int cols, int ldw, __bf16 *__restrict__ out) {
+// planes[q][r][c] = part q of W[r][(c + rot) % cols]  (rot: a column rotation of the gate blocks)
+__global__ void split_bf16x3_kernel(const float *__restrict__ W, int rows, int cols, int ldw, int rot,
+                                    __bf16 *__restrict__ out) {
     const size_t n = (size_t)rows * cols;
     const size_t plane = n;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const size_t r = i / cols, c = i - r * cols;
-        const float x = W[r * ldw + c];
+        const size_t cs = c + rot < (size_t)cols ? c + rot : c + rot - cols;
+        const float x = W[r * ldw + cs];
         const __bf16 a = (__bf16)x;
         const float res = x - (float)a;
         const __bf16 b = (__bf16)res;
@@ -222,14 +225,20 @@ static bool a16x3(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) 
 
 using namespace msat;
 
-extern "C" int msat_split_bf16x3(const float *W, int32_t rows, int32_t cols, int32_t ldw, void *planes, void *stream) {
+extern "C" int msat_split_bf16x3_rot(const float *W, int32_t rows, int32_t cols, int32_t ldw, int32_t rot,
+                                     void *planes, void *stream) {
     if (rows == 0 || cols == 0) return MSAT_OK;
-    MSAT_REQUIRE(W && planes && rows > 0 && cols > 0 && ldw >= cols, "bad split_bf16x3 args");
+    MSAT_REQUIRE(W && planes && rows > 0 && cols > 0 && ldw >= cols && rot >= 0 && rot < cols,
+                 "bad split_bf16x3 args");
     const size_t n = (size_t)rows * cols;
     const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(split_bf16x3_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, W, rows, cols, ldw,
+    hipLaunchKernelGGL(split_bf16x3_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, W, rows, cols, ldw, rot,
                        reinterpret_cast<__bf16 *>(planes));
     return check_launch("split_bf16x3_kernel");
+}
+
+extern "C" int msat_split_bf16x3(const float *W, int32_t rows, int32_t cols, int32_t ldw, void *planes, void *stream) {
+    return msat_split_bf16x3_rot(W, rows, cols, ldw, 0, planes, stream);
 }
 
 extern "C" int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, float *C, int32_t ldc, const float *bias,

@@ -137,7 +137,8 @@ __global__ void __launch_bounds__(kRowThreads)
 gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
                   const float *__restrict__ scale, float *__restrict__ dGi, int lddi, float *__restrict__ dGh, int lddh,
-                  float *__restrict__ dh, int lddh_prev, float *__restrict__ part, int R, int H, int dh_assign) {
+                  float *__restrict__ dh, int lddh_prev, float *__restrict__ part, int R, int H, int dh_assign,
+                  int packed) {
     __shared__ float s_part[4][NQ * 64 * PER];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     float pq[NQ][PER];
@@ -199,12 +200,19 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
             const float dar = dr * rg[u] * (1.0f - rg[u]);
             const float daz = dz * zg[u] * (1.0f - zg[u]);
             float *di = dGi + (size_t)r * lddi, *dhh = dGh + (size_t)r * lddh;
-            di[j] = dar;
-            di[H + j] = daz;
-            di[2 * H + j] = dan;
-            dhh[j] = dar;
-            dhh[H + j] = daz;
-            dhh[2 * H + j] = dan * rg[u];
+            if (packed) {  // one row [dan | dar | daz | dan r]: dGi = cols 0..3H (gate order n, r, z), dGh = cols H..4H
+                di[j] = dan;
+                di[H + j] = dar;
+                di[2 * H + j] = daz;
+                di[3 * H + j] = dan * rg[u];
+            } else {
+                di[j] = dar;
+                di[H + j] = daz;
+                di[2 * H + j] = dan;
+                dhh[j] = dar;
+                dhh[H + j] = daz;
+                dhh[2 * H + j] = dan * rg[u];
+            }
             float *dhp = dh + (size_t)r * lddh_prev + j;
             *dhp = dh_assign ? dhn * zg[u] : *dhp + dhn * zg[u];
             if constexpr (NQ == 6) {
@@ -537,9 +545,9 @@ extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, in
     hipStream_t s = (hipStream_t)stream;
     const int nb = bwd_blocks(R);
     const dim3 g(nb), b(kRowThreads);
-    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0);
-    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0);
-    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0);
+    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0);
+    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0);
+    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0);
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
     return reduce_partials(partial, nb, 2 * H, dln_scale, accumulate_ln, partial + (size_t)nb * 2 * H, s);
@@ -561,15 +569,18 @@ extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4,
     const dim3 g(nb), b(kRowThreads);
     const bool bias = dbi != nullptr;
     const int dh_assign = (accumulate_ln >> 1) & 1;  // bit 1: dhprev = ..., else dhprev += ...
+    const int packed = (accumulate_ln >> 2) & 1;     // bit 2: packed [dan | dar | daz | dan r] rows
     accumulate_ln &= 1;
+    MSAT_REQUIRE(!packed || (dGh == dGi + H && lddi == lddh && lddi >= 4 * H),
+                 "gru_ln_bwd_g4: packed rows need dGh = dGi + H and a shared ld >= 4H");
     const int NQ = bias ? 6 : 2;
 #define MSAT_BWD(PER)                                                                                              \
     if (bias)                                                                                                      \
         hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, 6>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,    \
-                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign);                \
+                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed);                \
     else                                                                                                           \
         hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, 2>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,    \
-                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign);
+                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed);
     if (H == 64) { MSAT_BWD(1) }
     else if (H == 128) { MSAT_BWD(2) }
     else { MSAT_BWD(4) }

@@ -116,6 +116,7 @@ def _load():
     sig["msat_var_gather"] = (I, [P, I, P, P, P, I, I, I, I, P])
     sig["msat_transpose_pad"] = (I, [P, I, I, I, P, I, P])
     sig["msat_split_bf16x3"] = (I, [P, I, I, I, P, P])
+    sig["msat_split_bf16x3_rot"] = (I, [P, I, I, I, I, P, P])
     sig["msat_gemm_x3"] = (I, [P, I, P, P, I, P, I, I, I, I, P])
     sig["msat_clause_gather2"] = (I, [P, P, I, P, P, I, I, I, I, I, P])
     sig["msat_var_gather2"] = (I, [P, P, I, P, P, P, P, I, I, I, I, P])
@@ -164,6 +165,7 @@ EXPORTED = (
     "msat_transpose_pad",
     "msat_gru_ln_fused_fwd_t",
     "msat_split_bf16x3",
+    "msat_split_bf16x3_rot",
     "msat_gemm_x3",
     "msat_clause_gather2",
     "msat_var_gather2",

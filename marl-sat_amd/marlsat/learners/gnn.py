@@ -133,12 +133,15 @@ class GNNActorCritic:
     use_x3 = os.environ.get("MARLSAT_GEMM_X3", "1") != "0"
 
     def _split_weights(self, mats):
-        """bf16x3 planes of each (rows, 3H) weight block (once per backward): {key: planes tensor}."""
+        """bf16x3 planes of each (rows, 3H) weight block (once per backward): {key: planes tensor}.
+        mats: {key: (matrix, column rotation)}; rotation 2H puts the gate blocks in (n, r, z) order,
+        the order of the packed backward rows' dGi columns."""
         out = {}
-        for key, Wm in mats.items():
+        for key, (Wm, rot) in mats.items():
             rows, cols = Wm.shape
             buf = torch.empty(3 * rows * cols + 8, dtype=torch.int16, device=self.device)
-            _chk(L_.msat_split_bf16x3(Wm.data_ptr(), rows, cols, cols, buf.data_ptr(), self.stream), "split_bf16x3")
+            _chk(L_.msat_split_bf16x3_rot(Wm.data_ptr(), rows, cols, cols, rot, buf.data_ptr(), self.stream),
+                 "split_bf16x3")
             out[key] = buf
         return out
 
@@ -354,51 +357,74 @@ class GNNActorCritic:
         ln, dln = self.p("enc.ln"), self.g("enc.ln")
         (Fc, Fp, Fn), (gFc, gFp, gFn) = self._fold_views()
         self._gF.zero_()
-        mats = {"wh_c": self.p("enc.gru_c_wh"), "wh_vp": self.p("enc.gru_vp_wh"), "wh_vn": self.p("enc.gru_vn_wh"),
-                "Fc": Fc[:2 * H], "Fp": Fp[:H], "Fn": Fn[:H]}
+        # packed backward rows [dan | dar | daz | dan r] (4H): dGh = cols H..4H, dGi = cols 0..3H in gate
+        # order (n, r, z); needs the x3 path (its F planes are split with the gate blocks rotated)
+        packed = self.use_x3
+        rot = 2 * H if packed else 0
+        mats = {"wh_c": (self.p("enc.gru_c_wh"), 0), "wh_vp": (self.p("enc.gru_vp_wh"), 0),
+                "wh_vn": (self.p("enc.gru_vn_wh"), 0), "Fc": (Fc[:2 * H], rot), "Fp": (Fp[:H], rot),
+                "Fn": (Fn[:H], rot)}
         pl = self._split_weights(mats) if self.use_x3 else {k: None for k in mats}
+        flags = 3 | (4 if packed else 0)
+
+        def dG_buffers(R):
+            """-> (dGi ptr, dGh ptr, ld, keep-alive tensor)"""
+            if packed:
+                D = e(R, 4 * H)
+                return D.data_ptr(), pp(D, H), 4 * H, D
+            dGI, dGH = e(R, W3), e(R, W3)
+            return dGI.data_ptr(), dGH.data_ptr(), W3, (dGI, dGH)
+
+        def dF_wgrad(A, lda, dgi, ld, W, R, K):
+            """W (dF rows, ld 3H) += A^T dGi; in packed rows dGi's gate blocks are (n | r z)."""
+            if packed:
+                self._wgrad(A, lda, dgi, ld, pp_addr(W, 2 * H), W3, R, K, H)
+                self._wgrad(A, lda, dgi + 4 * H, ld, W, W3, R, K, 2 * H)
+            else:
+                self._wgrad(A, lda, dgi, ld, W, W3, R, K, W3)
+
+        pp_addr = lambda ptr, col: ptr + 4 * col
         for l in range(self.L - 1, -1, -1):
             t = tape[l]
             dNV = e(Nv, 2 * H)
             dprev = {}
             for half, cell, Hx, G4, dHx, k, F, gF in ((0, "gru_vp", t.Hp, t.G4p, dHp, 3 * l + 1, Fp, gFp),
                                                      (1, "gru_vn", t.Hn, t.G4n, dHn, 3 * l + 2, Fn, gFn)):
-                dGI, dGH = e(Nv, W3), e(Nv, W3)
+                dgi, dgh, ldd, keep = dG_buffers(Nv)
                 dHx0 = e(Nv, H)  # written (not accumulated) by the backward kernel: flags bit 1
                 part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nv, H)))
                 _chk(L_.msat_gru_ln_bwd_g4(dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, pp(ln[k]),
-                                           dGI.data_ptr(), W3, dGH.data_ptr(), W3, dHx0.data_ptr(), H,
+                                           dgi, ldd, dgh, ldd, dHx0.data_ptr(), H,
                                            pp(dln[k]), pp(dln[k], H), self.g(f"enc.{cell}_bi").data_ptr(),
-                                           pp(self.g(f"enc.{cell}_bh"), 2 * H), part.data_ptr(), Nv, H, 3,
+                                           pp(self.g(f"enc.{cell}_bh"), 2 * H), part.data_ptr(), Nv, H, flags,
                                            self.stream), "gru_ln_bwd_g4")
                 wh, gwh = self.p(f"enc.{cell}_wh"), self.g(f"enc.{cell}_wh")
                 sfx = cell[-2:]
-                self._dgrad(dGH.data_ptr(), W3, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1)
-                self._wgrad(Hx.data_ptr(), H, dGH.data_ptr(), W3, gwh.data_ptr(), W3, Nv, H, W3)
+                self._dgrad(dgh, ldd, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1)
+                self._wgrad(Hx.data_ptr(), H, dgh, ldd, gwh.data_ptr(), W3, Nv, H, W3)
                 # input path: d(gathered) and dF rows [fold | x/svf | counts]
-                self._dgrad(dGI.data_ptr(), W3, F, pl["Fp" if half == 0 else "Fn"], pp(dNV, half * H), 2 * H, Nv, H,
-                            W3, 0)
-                self._wgrad(pp(t.NV, half * H), 2 * H, dGI.data_ptr(), W3, gF.data_ptr(), W3, Nv, H, W3)
-                self._wgrad(b.vfeat.data_ptr(), 8, dGI.data_ptr(), W3, pp(gF[H]), W3, Nv, 8, W3)
+                self._dgrad(dgi, ldd, F, pl["Fp" if half == 0 else "Fn"], pp(dNV, half * H), 2 * H, Nv, H, W3, 0)
+                dF_wgrad(pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), Nv, H)
+                dF_wgrad(b.vfeat.data_ptr(), 8, dgi, ldd, pp(gF[H]), Nv, 8)
                 dprev[half] = dHx0
             # var gather backward: dH_c (+)= A+^T dNV+ + A-^T dNV-  (one merged clause gather)
             _chk(L_.msat_clause_gather2(dNV.data_ptr(), pp(dNV, H), 2 * H, b.slots.data_ptr(), dHc.data_ptr(), H, Nc,
                                         H, 1, 1, self.stream), "clause_gather2")
             # clause GRU
-            dGI, dGH = e(Nc, W3), e(Nc, W3)
+            dgi, dgh, ldd, keep = dG_buffers(Nc)
             dHc0 = e(Nc, H)
             part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nc, H)))
             _chk(L_.msat_gru_ln_bwd_g4(dHc.data_ptr(), H, t.G4c.data_ptr(), 4 * H, t.Hc.data_ptr(), H, pp(ln[3 * l]),
-                                       dGI.data_ptr(), W3, dGH.data_ptr(), W3, dHc0.data_ptr(), H,
+                                       dgi, ldd, dgh, ldd, dHc0.data_ptr(), H,
                                        pp(dln[3 * l]), pp(dln[3 * l], H), self.g("enc.gru_c_bi").data_ptr(),
-                                       pp(self.g("enc.gru_c_bh"), 2 * H), part.data_ptr(), Nc, H, 3, self.stream),
+                                       pp(self.g("enc.gru_c_bh"), 2 * H), part.data_ptr(), Nc, H, flags, self.stream),
                  "gru_ln_bwd_g4")
-            self._dgrad(dGH.data_ptr(), W3, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1)
-            self._wgrad(t.Hc.data_ptr(), H, dGH.data_ptr(), W3, self.g("enc.gru_c_wh").data_ptr(), W3, Nc, H, W3)
+            self._dgrad(dgh, ldd, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1)
+            self._wgrad(t.Hc.data_ptr(), H, dgh, ldd, self.g("enc.gru_c_wh").data_ptr(), W3, Nc, H, W3)
             dGIN = e(Nc, 2 * H)
-            self._dgrad(dGI.data_ptr(), W3, Fc, pl["Fc"], dGIN.data_ptr(), 2 * H, Nc, 2 * H, W3, 0)
-            self._wgrad(t.GIN.data_ptr(), 2 * H, dGI.data_ptr(), W3, gFc.data_ptr(), W3, Nc, 2 * H, W3)
-            self._wgrad(b.cdeg.data_ptr(), 4, dGI.data_ptr(), W3, pp(gFc[2 * H]), W3, Nc, 4, W3)
+            self._dgrad(dgi, ldd, Fc, pl["Fc"], dGIN.data_ptr(), 2 * H, Nc, 2 * H, W3, 0)
+            dF_wgrad(t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), Nc, 2 * H)
+            dF_wgrad(b.cdeg.data_ptr(), 4, dgi, ldd, pp(gFc[2 * H]), Nc, 4)
             # clause gather backward: dH_v+/- (+)= A+/- dGIN+/-
             _chk(L_.msat_var_gather2(dGIN.data_ptr(), pp(dGIN, H), 2 * H, b.ptr.data_ptr(), b.inc.data_ptr(),
                                      dprev[0].data_ptr(), dprev[1].data_ptr(), H, Nv, H, 1, self.stream),
