@@ -37,14 +37,23 @@ clause_gather_kernel(const float *__restrict__ src_pos, const float *__restrict_
             const int want = j < H ? 0 : 1;  // split: first half positive literals, second negative
             const int col = j < H ? j : j - H;
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#define MSAT_ADD_SLOT(S)                                                                          \
-    if ((S) >= 0 && (merged || ((S)&1) == want)) {                                                \
-        const float *src = ((S)&1) ? src_neg : src_pos;                                           \
-        const float4 v = *reinterpret_cast<const float4 *>(src + (size_t)((S) >> 1) * lds_ + col); \
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;                                   \
-    }
-            MSAT_ADD_SLOT(s0) MSAT_ADD_SLOT(s1) MSAT_ADD_SLOT(s2)
-#undef MSAT_ADD_SLOT
+            // all three slot loads in flight before the (slot-ordered) adds
+            const int sl[3] = {s0, s1, s2};
+            bool ok[3];
+            float4 x[3];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int S = sl[u];
+                ok[u] = S >= 0 && (merged || (S & 1) == want);
+                const float *src = (S & 1) ? src_neg : src_pos;
+                x[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (ok[u]) x[u] = *reinterpret_cast<const float4 *>(src + (size_t)(S >> 1) * lds_ + col);
+            }
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+                if (ok[u]) {
+                    acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
+                }
             float4 *d = reinterpret_cast<float4 *>(dst + (size_t)c * ldd + j);
             if (accumulate) {
                 const float4 o = *d;
@@ -62,7 +71,8 @@ __global__ void __launch_bounds__(kRowThreads)
 var_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ src_neg, int lds_,
                   const int *__restrict__ ptr, const int *__restrict__ inc, float *__restrict__ dst_pos,
                   float *__restrict__ dst_neg, int ldd, int Nv, int H, int accumulate) {
-    const int lane = threadIdx.x & 63;
+    __shared__ int s_idx[4][64];  // per wave: one chunk of the var row's entry list
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int v = blockIdx.x * 4 + (threadIdx.x >> 6); v < Nv; v += gridDim.x * 4) {
         const int e0 = ptr[v], e1 = ptr[v + 1];
         for (int j = lane * 4; j < 2 * H; j += 256) {
@@ -70,11 +80,46 @@ var_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ s
             const int col = j < H ? j : j - H;
             const float *src = want ? src_neg : src_pos;
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int e = e0; e < e1; ++e) {
-                const int s = inc[e];
-                if ((s & 1) != want) continue;
-                const float4 x = *reinterpret_cast<const float4 *>(src + (size_t)(s >> 1) * lds_ + col);
-                acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+            if (H % 128) {  // H = 64: half the wave idle in this loop, plain walk
+                for (int e = e0; e < e1; ++e) {
+                    const int s = inc[e];
+                    if ((s & 1) != want) continue;
+                    const float4 x = *reinterpret_cast<const float4 *>(src + (size_t)(s >> 1) * lds_ + col);
+                    acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+                }
+            }
+            // H % 128 == 0 (every lane active here): the entry list is fetched lane-parallel (64 per
+            // load) and split by sign with ballots; each half-wave walks its entries in ascending order
+            // (the same summation order as the plain walk), four row loads in flight
+            for (int cb = e0; H % 128 == 0 && cb < e1; cb += 64) {
+                const int n = min(64, e1 - cb);
+                const int my = lane < n ? inc[cb + lane] : 0;
+                const uint64_t negm = __ballot(lane < n && (my & 1));
+                const uint64_t posm = __ballot(lane < n && !(my & 1));
+                s_idx[wv][lane] = my;  // read back below by the (diverged) half-waves: no cross-lane ops there
+                uint64_t m = want ? negm : posm;
+                while (m) {
+                    int k[4];
+                    bool ok[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        ok[u] = m != 0;
+                        k[u] = ok[u] ? __builtin_ctzll(m) : 0;
+                        m &= m - 1;
+                    }
+                    float4 x[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int s = s_idx[wv][k[u]];
+                        x[u] = ok[u] ? *reinterpret_cast<const float4 *>(src + (size_t)(s >> 1) * lds_ + col)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (ok[u]) {
+                            acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
+                        }
+                }
             }
             float4 *d = reinterpret_cast<float4 *>((want ? dst_neg : dst_pos) + (size_t)v * ldd + col);
             if (accumulate) {
