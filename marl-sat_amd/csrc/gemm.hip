@@ -374,6 +374,15 @@ bool msat_gemm2_ok(const float *A, int lda, const float *B, int ldb, int transB,
 int msat_gemm2_launch(const float *A, int lda, const float *B, int ldb, int transB, float *C, int ldc,
                       const float *bias, int M, int N, int K, int accumulate, hipStream_t s);
 bool msat_wgrad2_ok(const float *A, int lda, const float *G, int ldg, int K, int N);
+bool msat_wgrad_x3_ok(const float *A, int lda, const float *G, int ldg, int K, int N);
+int msat_wgrad_x3_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
+                         int rows_per_split, hipStream_t s);
+
+// MARLSAT_WGRAD_X3=0 keeps the fp32-MFMA weight gradient (A/B measurements)
+static bool wgrad_x3() {
+    const char *e = getenv("MARLSAT_WGRAD_X3");
+    return !(e && e[0] == '0');
+}
 int msat_wgrad2_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
                        int rows_per_split, hipStream_t s);
 
@@ -429,7 +438,10 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
     const int splits = wgrad_splits(M, K, N);
     const int rows = (M + splits - 1) / splits;
     int rc;
-    if (!legacy_gemm() && msat_wgrad2_ok(A, lda, G, ldg, K, N)) {
+    if (!legacy_gemm() && wgrad_x3() && msat_wgrad_x3_ok(A, lda, G, ldg, K, N)) {
+        const int rows16 = ((rows + 15) / 16) * 16;
+        rc = msat_wgrad_x3_launch(A, lda, G, ldg, (float *)workspace, M, K, N, splits, rows16, s);
+    } else if (!legacy_gemm() && msat_wgrad2_ok(A, lda, G, ldg, K, N)) {
         const int rows32 = ((rows + 31) / 32) * 32;
         rc = msat_wgrad2_launch(A, lda, G, ldg, (float *)workspace, M, K, N, splits, rows32, s);
     } else {

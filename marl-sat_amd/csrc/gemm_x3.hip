@@ -62,6 +62,30 @@ __device__ __forceinline__ Split8 split8(const float4 &u, const float4 &v) {
 }
 
 // planes[q][r][c] = part q of W[r][(c + rot) % cols]  (rot: a column rotation of the gate blocks)
+struct Split4 {
+    uint2 p[3];
+};
+
+__device__ __forceinline__ Split4 split4(const float4 &u) {
+    const float x[4] = {u.x, u.y, u.z, u.w};
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 h, m, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const __bf16 a = (__bf16)x[j];
+        const float r = x[j] - (float)a;
+        const __bf16 b = (__bf16)r;
+        h[j] = a;
+        m[j] = b;
+        l[j] = (__bf16)(r - (float)b);
+    }
+    Split4 s;
+    s.p[0] = __builtin_bit_cast(uint2, h);
+    s.p[1] = __builtin_bit_cast(uint2, m);
+    s.p[2] = __builtin_bit_cast(uint2, l);
+    return s;
+}
+
 __global__ void split_bf16x3_kernel(const float *__restrict__ W, int rows, int cols, int ldw, int rot,
                                     __bf16 *__restrict__ out) {
     const size_t n = (size_t)rows * cols;
@@ -219,6 +243,130 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Weight gradient on the same split: part[s][k][n] = sum_{m in split s} A[m][k] G[m][n].
+// The MFMA reduction runs over the rows m, so both fragments are 8-row column strips.  Both
+// operands are staged row-major as three bf16 planes [16 rows][128 cols] (256-byte rows, chunks
+// XOR-swizzled for conflict-free transposed reads) and read with ds_read_b64_tr_b16: each
+// 16-lane group gets 4 rows x 16 columns delivered column-major, two reads per fragment.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+constexpr int kW3Plane = 16 * kX3M;  // bf16 elements per plane (16 rows x 128 cols)
+
+__device__ __forceinline__ int w3off(int row, int ch) {  // byte offset of 16-byte chunk ch of row
+    return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned short *plane, int r0, int c0, int lane) {
+    // lanes 16g..16g+15 of a half: rows r0..r0+3 then r0+4..r0+7, columns 8 c0 + 16 g' .. (see the map)
+    const int i = lane & 15, q = i >> 2, p = i & 3;
+    const char *b = reinterpret_cast<const char *>(plane);
+    typedef __attribute__((address_space(3))) s16x4 *lp;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(b + w3off(r0 + q, c0 + (p >> 1)) + 8 * (p & 1)));
+    const s16x4 hi =
+        __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(b + w3off(r0 + 4 + q, c0 + (p >> 1)) + 8 * (p & 1)));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ void __launch_bounds__(kX3T, 3)
+wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G, int ldg, float *__restrict__ part,
+                int M, int K, int N, int rows_per_split, int ntn, int tiles) {
+    __shared__ __attribute__((aligned(16))) unsigned short lds[2][6][kW3Plane];  // [buf][A planes | G planes]
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    const int sp = id / tiles, tile = id % tiles;
+    const int k0 = (tile / ntn) * kX3M, n0 = (tile % ntn) * kX3M;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
+    f32x16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16v{};
+    const int rb = sp * rows_per_split, re = min(M, rb + rows_per_split);
+    const int ns = (re - rb + 15) / 16;
+    // staging: thread t -> row t >> 4 of the slab, columns 4 (t & 15) and 4 (t & 15) + 64
+    const int srow = t >> 4, sc = (t & 15) * 4;
+    float4 ra[2], rg[2];
+    auto load = [&](int s) {
+        const int m = rb + s * 16 + srow;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int kc = k0 + sc + 64 * u, nc = n0 + sc + 64 * u;
+            ra[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            rg[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (m < re) {
+                if (kc < K) ra[u] = *reinterpret_cast<const float4 *>(A + (size_t)m * lda + kc);
+                if (nc < N) rg[u] = *reinterpret_cast<const float4 *>(G + (size_t)m * ldg + nc);
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int col = sc + 64 * u;
+            const int off = w3off(srow, col >> 3) + 8 * ((col >> 2) & 1);
+            const Split4 pa = split4(ra[u]), pg = split4(rg[u]);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(lds[buf][q]) + off) = pa.p[q];
+                *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(lds[buf][3 + q]) + off) = pg.p[q];
+            }
+        }
+    };
+    const int h = lane >> 5, g = (lane >> 4) & 1;
+    auto slab = [&](int buf) {
+        bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                fa[i][q] = tr_frag(lds[buf][q], 8 * h, (wr + 32 * i + 16 * g) >> 3, lane);
+                fb[i][q] = tr_frag(lds[buf][3 + q], 8 * h, (wc + 32 * i + 16 * g) >> 3, lane);
+            }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x16v c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+                acc[i][j] = c;
+            }
+    };
+    if (ns > 0) {
+        load(0);
+        store(0);
+        __syncthreads();
+    }
+    for (int s = 0; s < ns; ++s) {
+        const int buf = s & 1;
+        const bool more = s + 1 < ns;
+        if (more) load(s + 1);
+        slab(buf);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) store(buf ^ 1);
+        __syncthreads();
+    }
+    float *P = part + (size_t)sp * K * N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wc + 32 * j + (lane & 31);
+            if (col >= N) continue;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = k0 + wr + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+                if (row < K) P[(size_t)row * N + col] = acc[i][j][reg];
+            }
+        }
+}
+
 static bool a16x3(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace msat
@@ -253,4 +401,18 @@ extern "C" int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, fl
     hipLaunchKernelGGL(gemm_x3_kernel, dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
                        reinterpret_cast<const __bf16 *>(Wplanes), C, ldc, bias, M, N, K, accumulate, ntn, vec);
     return check_launch("gemm_x3_kernel");
+}
+
+// Launch of the split weight gradient (called from gemm.hip's msat_gemm_wgrad): K % 4, N % 4,
+// 16-byte aligned rows.  part >= splits * K * N floats.
+bool msat_wgrad_x3_ok(const float *A, int lda, const float *G, int ldg, int K, int N) {
+    return K % 4 == 0 && N % 4 == 0 && K >= 16 && lda % 4 == 0 && ldg % 4 == 0 && a16x3(A) && a16x3(G);
+}
+
+int msat_wgrad_x3_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
+                         int rows_per_split, hipStream_t s) {
+    const int ntk = (K + kX3M - 1) / kX3M, ntn = (N + kX3M - 1) / kX3M, tiles = ntk * ntn;
+    hipLaunchKernelGGL(wgrad_x3_kernel, dim3(tiles * splits), dim3(kX3T), 0, s, A, lda, G, ldg, part, M, K, N,
+                       rows_per_split, ntn, tiles);
+    return check_launch("wgrad_x3_kernel");
 }

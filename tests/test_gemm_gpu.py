@@ -94,13 +94,16 @@ def test_gemm_fast_path_shapes(M, N, K, transB, path, monkeypatch):
         _ref_close(C, ref, absprod)
 
 
-@pytest.mark.parametrize("path", ["1", "0"])
-@pytest.mark.parametrize("M,K,N", [(1, 4, 4), (33, 128, 384), (5000, 132, 384), (70001, 128, 128), (100, 256, 8)])
+@pytest.mark.parametrize("path", ["1", "0", "x3"])  # register-staged / fp32 LDS-DMA / bf16x3 split (default)
+@pytest.mark.parametrize("M,K,N", [(1, 4, 4), (33, 128, 384), (5000, 132, 384), (70001, 128, 128), (100, 256, 8),
+                                   (407001, 128, 384), (9999, 256, 260), (17, 16, 4)])
 def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
-    """Row tails (M % 32 != 0, splits of uneven length) go through the zero-filled register slab."""
+    """Row tails (M % 32 != 0, splits of uneven length) go through zero-filled slabs; the bf16x3
+    kernel (transposed LDS reads) is held to the same fp32 bound as the fp32 MFMA kernels."""
     from marlsat import _lib
 
-    monkeypatch.setenv("MARLSAT_GEMM", path)
+    monkeypatch.setenv("MARLSAT_GEMM", "0" if path == "x3" else path)
+    monkeypatch.setenv("MARLSAT_WGRAD_X3", "1" if path == "x3" else "0")
     g = torch.Generator(device="cuda").manual_seed(M + K + N)
     A = torch.randn(M, K, device="cuda", generator=g)
     G = torch.randn(M, N, device="cuda", generator=g)
