@@ -112,6 +112,14 @@ int msat_gru_ln_fused_fwd_t(const float *x0, int32_t ld0, int32_t w0, const floa
                             const float *wiT, const float *bi, const float *whT, const float *bh,
                             const float *ln_scale, const float *ln_bias, float *out, int32_t ldo, float *g4,
                             int32_t ldg, int32_t R, int32_t H, void *stream);
+/* Same cell on the bf16 matrix cores (exact bf16x3 split, fp32-accurate; H = 128): weights
+ * given as msat_split_bf16x3 planes of Wi zero-padded to kxp rows (kxp >= Kx, multiple of 16)
+ * and of Wh. */
+int msat_gru_ln_fused_fwd_x3(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
+                             const float *x2, int32_t ld2, int32_t w2, const float *hprev, int32_t ldp,
+                             const void *wi_planes, int32_t kxp, const float *bi, const void *wh_planes,
+                             const float *bh, const float *ln_scale, const float *ln_bias, float *out, int32_t ldo,
+                             float *g4, int32_t ldg, int32_t R, int32_t H, void *stream);
 /* msat_gru_ln_bwd from the fused forward's g4 tape (same outputs).  dbi (3H) / dbh_n (H), both
  * or neither, receive (+=) the gate-bias gradients sum_rows dGi and sum_rows dGh[:, 2H:3H]
  * (b_ir|b_iz|b_in and b_hn) from the same pass.  partial >= msat_gru_ln_bwd_partial_floats.

@@ -20,10 +20,10 @@
 #include <algorithm>
 
 #include "common.h"
+#include "split3.h"
 
 namespace msat {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 
 constexpr int kX3T = 256;
@@ -31,59 +31,11 @@ constexpr int kX3M = 128;  // tile rows / cols
 constexpr int kX3D = 16;   // slab depth (one bf16 MFMA k step)
 // LDS plane: 128 rows x 16 k bf16 = 4 KiB = 256 uint4 (row r, k-half h at uint4 index 2r + h)
 constexpr int kX3Plane = kX3M * kX3D / 8;
+constexpr int kW3Plane = 16 * kX3M;  // bf16 elements per weight-gradient plane (16 rows x 128 cols)
 
 __device__ __forceinline__ int xcd_remap_x3(int orig, int nwg) {
     const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-}
-
-struct Split8 {
-    uint4 p[3];
-};
-
-__device__ __forceinline__ Split8 split8(const float4 &u, const float4 &v) {
-    const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-    bf16x8 h, m, l;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const __bf16 a = (__bf16)x[j];
-        const float r = x[j] - (float)a;
-        const __bf16 b = (__bf16)r;
-        const float r2 = r - (float)b;
-        h[j] = a;
-        m[j] = b;
-        l[j] = (__bf16)r2;
-    }
-    Split8 s;
-    s.p[0] = __builtin_bit_cast(uint4, h);
-    s.p[1] = __builtin_bit_cast(uint4, m);
-    s.p[2] = __builtin_bit_cast(uint4, l);
-    return s;
-}
-
-// planes[q][r][c] = part q of W[r][(c + rot) % cols]  (rot: a column rotation of the gate blocks)
-struct Split4 {
-    uint2 p[3];
-};
-
-__device__ __forceinline__ Split4 split4(const float4 &u) {
-    const float x[4] = {u.x, u.y, u.z, u.w};
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    bf16x4 h, m, l;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const __bf16 a = (__bf16)x[j];
-        const float r = x[j] - (float)a;
-        const __bf16 b = (__bf16)r;
-        h[j] = a;
-        m[j] = b;
-        l[j] = (__bf16)(r - (float)b);
-    }
-    Split4 s;
-    s.p[0] = __builtin_bit_cast(uint2, h);
-    s.p[1] = __builtin_bit_cast(uint2, m);
-    s.p[2] = __builtin_bit_cast(uint2, l);
-    return s;
 }
 
 __global__ void split_bf16x3_kernel(const float *__restrict__ W, int rows, int cols, int ldw, int rot,
@@ -249,26 +201,6 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
 // operands are staged row-major as three bf16 planes [16 rows][128 cols] (256-byte rows, chunks
 // XOR-swizzled for conflict-free transposed reads) and read with ds_read_b64_tr_b16: each
 // 16-lane group gets 4 rows x 16 columns delivered column-major, two reads per fragment.
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-constexpr int kW3Plane = 16 * kX3M;  // bf16 elements per plane (16 rows x 128 cols)
-
-__device__ __forceinline__ int w3off(int row, int ch) {  // byte offset of 16-byte chunk ch of row
-    return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
-}
-
-__device__ __forceinline__ bf16x8 tr_frag(const unsigned short *plane, int r0, int c0, int lane) {
-    // lanes 16g..16g+15 of a half: rows r0..r0+3 then r0+4..r0+7, columns 8 c0 + 16 g' .. (see the map)
-    const int i = lane & 15, q = i >> 2, p = i & 3;
-    const char *b = reinterpret_cast<const char *>(plane);
-    typedef __attribute__((address_space(3))) s16x4 *lp;
-    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(b + w3off(r0 + q, c0 + (p >> 1)) + 8 * (p & 1)));
-    const s16x4 hi =
-        __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(b + w3off(r0 + 4 + q, c0 + (p >> 1)) + 8 * (p & 1)));
-    typedef short s16x8 __attribute__((ext_vector_type(8)));
-    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-}
-
 __global__ void __launch_bounds__(kX3T, 3)
 wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G, int ldg, float *__restrict__ part,
                 int M, int K, int N, int rows_per_split, int ntn, int tiles) {

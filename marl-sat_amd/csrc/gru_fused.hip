@@ -24,6 +24,7 @@
 #include <stdlib.h>
 
 #include "common.h"
+#include "split3.h"
 
 namespace msat {
 
@@ -40,6 +41,8 @@ struct GruFwdArgs {
     const float *hp;
     int ldp;
     const float *wi, *bi, *wh, *bh, *ln_scale, *ln_bias;
+    const __bf16 *wip, *whp;  // bf16x3 weight planes [3][kxp][3H] / [3][H][3H] (x3 kernel)
+    int kxp;
     float *out;
     int ldo;
     float *g4;
@@ -51,10 +54,10 @@ __device__ __forceinline__ float fsig(float x) { return 1.0f / (1.0f + __expf(-x
 
 // GRU gate algebra + LayerNorm on the accumulators of a 64-row tile (shared by both kernels):
 // acc[rt][0..3] = [r_pre | z_pre | gin | ghn] (biases not yet added) for rows wrow + 32 rt + ...
-template <int NW, int RS>
-__device__ __forceinline__ void gru_ln_epilogue(const GruFwdArgs &a, f32x16 (&acc)[2 / RS][4], float *red_lds,
+template <int NW, int RS, int ROWS = kFR>
+__device__ __forceinline__ void gru_ln_epilogue(const GruFwdArgs &a, f32x16 (&acc)[ROWS / 32 / RS][4], float *red_lds,
                                                 int row0, int wu, int wrow, int li, int lk) {
-    constexpr int H = 32 * NW, RT = 2 / RS;
+    constexpr int H = 32 * NW, RT = ROWS / 32 / RS;
     const int u = 32 * wu + li;
     const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
     const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
@@ -88,7 +91,7 @@ __device__ __forceinline__ void gru_ln_epilogue(const GruFwdArgs &a, f32x16 (&ac
                 s1 += __shfl_xor(s1, o, 64);
                 s2 += __shfl_xor(s2, o, 64);
             }
-            if (li == 0) red[wu * kFR + lr] = make_float2(s1, s2);
+            if (li == 0) red[wu * ROWS + lr] = make_float2(s1, s2);
         }
     __syncthreads();
     const float sc = a.ln_scale[u], lb = a.ln_bias[u];
@@ -101,7 +104,7 @@ __device__ __forceinline__ void gru_ln_epilogue(const GruFwdArgs &a, f32x16 (&ac
             float s1 = 0.f, s2 = 0.f;
 #pragma unroll
             for (int v = 0; v < NW; ++v) {
-                const float2 p = red[v * kFR + lr];
+                const float2 p = red[v * ROWS + lr];
                 s1 += p.x;
                 s2 += p.y;
             }
@@ -416,6 +419,134 @@ __global__ void transpose_pad_kernel(const float *__restrict__ W, int K, int N, 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// bf16x3 form (msat_gru_ln_fused_fwd_x3, H = 128): the same cell on the bf16 matrix cores with the
+// exact three-way operand split of gemm_x3.hip (six bf16 MFMAs per 16-deep k step, fp32-accurate).
+// 128-row tiles, 16 waves (4 unit groups x 4 row groups of 32).  Per 16-deep slab:
+//   A (h, then x) is split while staged: fp32 -> registers -> three bf16 planes [128 rows][16 k]
+//   (32-byte rows, chunk slot h ^ ((row >> 3) & 1)), read with ds_read_b128;
+//   the weights arrive pre-split ([3 planes][K][3H] bf16, msat_split_bf16x3) by LDS-DMA as
+//   [plane][gate][16 k][128 cols] images (256-byte rows, w3off swizzle applied on the source
+//   side), read as 8-row column fragments with ds_read_b64_tr_b16.
+constexpr int kXR = 128;  // rows per workgroup (x3 kernel)
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW * 4, 1)
+gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
+    constexpr int H = 32 * NW, T = 64 * NW * 4, BW = 3 * H, RS = 4;
+    static_assert(H == 128, "x3 GRU: one 128-column image per gate");
+    constexpr int APL = kXR * kFK;            // bf16 per A plane (128 rows x 16 k)
+    constexpr int BPL = kFK * H;              // bf16 per (plane, gate) image (16 k x 128 cols)
+    constexpr int BCH = 3 * 3 * BPL / 8;      // 16-byte chunks of a B slab (2304)
+    constexpr int BN = (BCH + T - 1) / T;     // glds per thread (3, guarded)
+    __shared__ __attribute__((aligned(16))) unsigned short As[2][3][APL];
+    __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * 3 * BPL];
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wu = w % NW, wrow = (w / NW) * 32;
+    const int row0 = blockIdx.x * kXR;
+    const int nsh = H / kFK;
+    const int ns = nsh + a.kxp / kFK;
+
+    // A staging: threads 0..511 -> row t >> 2, k quad t & 3
+    const bool stager = t < kXR * 4;
+    const int arow = (t >> 2) & (kXR - 1), akq = (t & 3) * 4;
+    float4 ra;
+    auto loadA = [&](int s) {
+        ra = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int r = row0 + arow;
+        if (!stager || r >= a.R) return;
+        const float *p = nullptr;
+        if (s < nsh) {
+            p = a.hp + (size_t)r * a.ldp + s * kFK + akq;
+        } else {
+            int k = (s - nsh) * kFK + akq;
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                if (!p && k < a.seg_w[g]) p = a.seg[g] + (size_t)r * a.seg_ld[g] + k;
+                k -= a.seg_w[g];
+            }
+        }
+        if (p) ra = *reinterpret_cast<const float4 *>(p);
+    };
+    auto storeA = [&](int buf) {
+        if (!stager) return;
+        const Split4 sp = split4(ra);
+        const int off = arow * 32 + 16 * ((akq >> 3) ^ ((arow >> 3) & 1)) + 8 * ((akq >> 2) & 1);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(As[buf][q]) + off) = sp.p[q];
+    };
+    auto issueB = [&](int s, int buf) {
+        const bool hid = s < nsh;
+        const __bf16 *W = hid ? a.whp : a.wip;
+        const int krows = hid ? H : a.kxp;
+        const int kb = hid ? s * kFK : (s - nsh) * kFK;
+#pragma unroll
+        for (int i = 0; i < BN; ++i) {
+            const int idx = i * T + t;  // chunk slot of [plane][gate][k row][16 slots]
+            if (idx < BCH) {
+                const int slot = idx & 15, r = (idx >> 4) & 15, pg = idx >> 8;  // pg = plane * 3 + gate
+                const int q = pg / 3, g = pg - 3 * q;
+                const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
+                glds16_async(W + ((size_t)q * krows + kb + r) * BW + g * H + 8 * ch,
+                             reinterpret_cast<char *>(Bs[buf]) + 16 * (i * T + 64 * w));
+            }
+        }
+    };
+
+    f32x16 acc[1][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[0][g] = f32x16{};
+    const int li = lane & 31, lk = lane >> 5, gl = (lane >> 4) & 1;
+    auto slab = [&](int buf, bool hid) {
+        bf16x8 fa[3];
+        const int r = wrow + li;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            fa[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(
+                                                   reinterpret_cast<const char *>(As[buf][q]) + r * 32 +
+                                                   16 * (lk ^ ((r >> 3) & 1))));
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            bf16x8 fb[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) fb[q] = tr_frag(Bs[buf] + (q * 3 + g) * BPL, 8 * lk, (32 * wu + 16 * gl) >> 3, lane);
+            const int ai = g < 2 ? g : (hid ? 3 : 2);
+            f32x16 c = acc[0][ai];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], c, 0, 0, 0);
+            acc[0][ai] = c;
+        }
+    };
+
+    issueB(0, 0);
+    loadA(0);
+    storeA(0);
+    wait_vmcnt<0>();
+    barrier_lds();
+    int buf = 0;
+#pragma unroll 1
+    for (int s = 0; s < ns; ++s) {
+        const bool more = s + 1 < ns;
+        if (more) {
+            issueB(s + 1, buf ^ 1);
+            loadA(s + 1);
+        }
+        slab(buf, s < nsh);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) storeA(buf ^ 1);
+        wait_vmcnt<0>();
+        barrier_lds();
+        buf ^= 1;
+    }
+    gru_ln_epilogue<NW, RS, kXR>(a, acc, reinterpret_cast<float *>(&As[0][0][0]), row0, wu, wrow, li, lk);
+}
+
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace msat
@@ -540,4 +671,56 @@ extern "C" int msat_gru_ln_fused_fwd_t(const float *x0, int32_t ld0, int32_t w0,
     if (H == 64) hipLaunchKernelGGL((gru_ln_fused_fwd_t_kernel<2, 2>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((gru_ln_fused_fwd_t_kernel<4, 2>), grid, dim3(512), 0, s, a);
     return check_launch("gru_ln_fused_fwd_t_kernel");
+}
+
+extern "C" int msat_gru_ln_fused_fwd_x3(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1,
+                                        int32_t w1, const float *x2, int32_t ld2, int32_t w2, const float *hprev,
+                                        int32_t ldp, const void *wi_planes, int32_t kxp, const float *bi,
+                                        const void *wh_planes, const float *bh, const float *ln_scale,
+                                        const float *ln_bias, float *out, int32_t ldo, float *g4, int32_t ldg,
+                                        int32_t R, int32_t H, void *stream) {
+    MSAT_REQUIRE(H == 128, "gru_ln_fused_fwd_x3: H must be 128 (got %d)", H);
+    MSAT_REQUIRE(R >= 0, "gru_ln_fused_fwd_x3: R < 0");
+    if (R == 0) return MSAT_OK;
+    MSAT_REQUIRE(x0 && hprev && wi_planes && bi && wh_planes && bh && ln_scale && ln_bias && out, "NULL pointer");
+    MSAT_REQUIRE(ldo >= H && ldp >= H && (!g4 || ldg >= 4 * H), "gru_ln_fused_fwd_x3: bad dims");
+    const float *seg[3] = {x0, x1, x2};
+    const int lds_[3] = {ld0, ld1, ld2}, ws[3] = {w0, w1, w2};
+    int Kx = 0;
+    for (int g = 0; g < 3; ++g) {
+        MSAT_REQUIRE(ws[g] >= 0 && ws[g] % 4 == 0, "gru_ln_fused_fwd_x3: segment %d width %d must be a multiple of 4",
+                     g, ws[g]);
+        if (ws[g] == 0) continue;
+        MSAT_REQUIRE(seg[g] && aligned16(seg[g]) && lds_[g] % 4 == 0 && lds_[g] >= ws[g],
+                     "gru_ln_fused_fwd_x3: segment %d must be 16-byte aligned with ld %% 4 == 0", g);
+        Kx += ws[g];
+    }
+    MSAT_REQUIRE(Kx > 0 && w0 > 0, "gru_ln_fused_fwd_x3: empty input");
+    MSAT_REQUIRE(kxp % kFK == 0 && kxp >= Kx, "gru_ln_fused_fwd_x3: kxp must be >= Kx and a multiple of 16");
+    MSAT_REQUIRE(aligned16(hprev) && ldp % 4 == 0 && aligned16(wi_planes) && aligned16(wh_planes),
+                 "gru_ln_fused_fwd_x3: hprev / weight planes must be 16-byte aligned");
+    GruFwdArgs a = {};
+    for (int g = 0; g < 3; ++g) {
+        a.seg[g] = ws[g] ? seg[g] : nullptr;
+        a.seg_ld[g] = lds_[g];
+        a.seg_w[g] = ws[g];
+    }
+    a.hp = hprev;
+    a.ldp = ldp;
+    a.wip = reinterpret_cast<const __bf16 *>(wi_planes);
+    a.whp = reinterpret_cast<const __bf16 *>(wh_planes);
+    a.kxp = kxp;
+    a.bi = bi;
+    a.bh = bh;
+    a.ln_scale = ln_scale;
+    a.ln_bias = ln_bias;
+    a.out = out;
+    a.ldo = ldo;
+    a.g4 = g4;
+    a.ldg = ldg;
+    a.R = R;
+    a.Kx = Kx;
+    hipLaunchKernelGGL((gru_ln_fused_fwd_x3_kernel<4>), dim3((R + kXR - 1) / kXR), dim3(1024), 0, (hipStream_t)stream,
+                       a);
+    return check_launch("gru_ln_fused_fwd_x3_kernel");
 }

@@ -123,6 +123,7 @@ def _load():
     sig["msat_gru_ln_fwd"] = (I, [P, I, P, I, P, I, P, P, P, I, I, I, P])
     sig["msat_gru_ln_fused_fwd"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, P, P, P, P, P, P, I, P, I, I, I, P])
     sig["msat_gru_ln_fused_fwd_t"] = sig["msat_gru_ln_fused_fwd"]
+    sig["msat_gru_ln_fused_fwd_x3"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, I, P, P, P, P, P, P, I, P, I, I, I, P])
     sig["msat_gru_ln_bwd_g4"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, I, P])
     sig["msat_gru_ln_bwd_partial_floats"] = (Z, [I, I])
     sig["msat_gru_ln_bwd"] = (I, [P, I, P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, I, I, I, P])
@@ -164,6 +165,7 @@ EXPORTED = (
     "msat_var_gather",
     "msat_transpose_pad",
     "msat_gru_ln_fused_fwd_t",
+    "msat_gru_ln_fused_fwd_x3",
     "msat_split_bf16x3",
     "msat_split_bf16x3_rot",
     "msat_gemm_x3",

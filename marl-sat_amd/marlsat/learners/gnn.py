@@ -166,6 +166,9 @@ class GNNActorCritic:
         ws = self.scr.get_part(int(L_.msat_colsum_workspace_floats(M, N)))
         _chk(L_.msat_colsum(G, ldg, M, N, out, acc, ws.data_ptr(), self.stream), "msat_colsum")
 
+    # bf16x3 split GRU kernel (fp32-accurate, bf16 matrix cores) for the fused encoder at H = 128
+    use_gru_x3 = os.environ.get("MARLSAT_GRU_X3", "1") != "0"
+
     # transposed-weight GRU kernel (k-major images, ds_read_b128 fragments): measured equal to the
     # [K][3H] form (profiles/gru_bench.py: 855-3060 vs 888-3049 us) plus the per-forward transposes,
     # so it is opt-in (MARLSAT_GRU_T=1)
@@ -181,6 +184,15 @@ class GNNActorCritic:
         kx = sum(w for _, _, w in segs)
         GNNActorCritic.flops += 2 * R * 3 * H * (H + (kx + 15) // 16 * 16)
         (p0, l0, w0), (p1, l1, w1), (p2, l2, w2) = segs
+        if isinstance(wt, dict):  # bf16x3 planes {"wi": (planes, kxp), "wh": planes}
+            _chk(L_.msat_gru_ln_fused_fwd_x3(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
+                                             wt["wi"][0].data_ptr(), wt["wi"][1],
+                                             self.p(f"enc.{cell}_bi").data_ptr(), wt["wh"].data_ptr(),
+                                             self.p(f"enc.{cell}_bh").data_ptr(), self._ptr(ln_row),
+                                             self._ptr(ln_row, H), out.data_ptr(), H,
+                                             g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
+                 "msat_gru_ln_fused_fwd_x3")
+            return
         if wt is not None:
             _chk(L_.msat_gru_ln_fused_fwd_t(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
                                             wt[0].data_ptr(), self.p(f"enc.{cell}_bi").data_ptr(),
@@ -247,14 +259,20 @@ class GNNActorCritic:
     # different fp32 association: parity is the 1e-5 fp32 bar, not bitwise.
     fuse_phi = os.environ.get("MARLSAT_FUSE_PHI", "1") != "0"
 
-    def _fold_views(self):
+    def _fold_views(self, padded: bool = False):
+        """Views of the folded matrices F_c (2H+4 rows), F_v+, F_v- (H+8 rows) and of their gradients.
+        Each block is followed by zero rows up to a multiple of 16 (padded=True returns those
+        views: the bf16x3 GRU kernel reads whole 16-row slabs)."""
         H = self.H
-        if getattr(self, "_F", None) is None:
-            rows = (2 * H + 4) + 2 * (H + 8)
-            self._F = torch.zeros((rows, 3 * H), dtype=torch.float32, device=self.device)
-            self._gF = torch.zeros_like(self._F)
         c, v = 2 * H + 4, H + 8
-        sl = lambda T: (T[:c], T[c:c + v], T[c + v:c + 2 * v])
+        cp, vp = (c + 15) // 16 * 16, (v + 15) // 16 * 16
+        if getattr(self, "_F", None) is None:
+            self._F = torch.zeros((cp + 2 * vp, 3 * H), dtype=torch.float32, device=self.device)
+            self._gF = torch.zeros_like(self._F)
+        if padded:
+            sl = lambda T: (T[:cp], T[cp:cp + vp], T[cp + vp:cp + 2 * vp])
+        else:
+            sl = lambda T: (T[:c], T[cp:cp + v], T[cp + vp:cp + vp + v])
         return sl(self._F), sl(self._gF)
 
     def _fold_weights(self):
@@ -317,7 +335,14 @@ class GNNActorCritic:
         self._fold_weights()
         (Fc, Fp, Fn), _ = self._fold_views()
         wt = {"gru_c": None, "gru_vp": None, "gru_vn": None}
-        if self.use_gru_t and H in (64, 128):
+        if self.use_gru_x3 and H == 128:
+            (Pc, Pp, Pn), _ = self._fold_views(padded=True)
+            pl = self._split_weights({"c": (Pc, 0), "vp": (Pp, 0), "vn": (Pn, 0), "hc": (self.p("enc.gru_c_wh"), 0),
+                                      "hvp": (self.p("enc.gru_vp_wh"), 0), "hvn": (self.p("enc.gru_vn_wh"), 0)})
+            wt = {"gru_c": {"wi": (pl["c"], Pc.shape[0]), "wh": pl["hc"]},
+                  "gru_vp": {"wi": (pl["vp"], Pp.shape[0]), "wh": pl["hvp"]},
+                  "gru_vn": {"wi": (pl["vn"], Pn.shape[0]), "wh": pl["hvn"]}}
+        elif self.use_gru_t and H in (64, 128):
             T = self._transposed_weights({"c": Fc, "vp": Fp, "vn": Fn, "hc": self.p("enc.gru_c_wh"),
                                           "hvp": self.p("enc.gru_vp_wh"), "hvn": self.p("enc.gru_vn_wh")})
             wt = {"gru_c": (T["c"], T["hc"]), "gru_vp": (T["vp"], T["hvp"]), "gru_vn": (T["vn"], T["hvn"])}

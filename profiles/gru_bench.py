@@ -28,10 +28,22 @@ for kind, R, segs_w, segs_ld in (("var", 407000, (H, 8), (2 * H, 8)), ("clause",
     wiT = torch.empty(3 * H, Kp, device="cuda"); whT = torch.empty(3 * H, H, device="cuda")
     _lib.lib.msat_transpose_pad(wi.data_ptr(), Kx, 3 * H, 3 * H, wiT.data_ptr(), Kp, _lib.stream_ptr())
     _lib.lib.msat_transpose_pad(wh.data_ptr(), H, 3 * H, 3 * H, whT.data_ptr(), H, _lib.stream_ptr())
+    kxp = Kp
+    wip = torch.zeros(kxp, 3 * H, device="cuda"); wip[:Kx] = wi
+    pi = torch.empty(3 * kxp * 3 * H + 8, dtype=torch.int16, device="cuda")
+    ph = torch.empty(3 * H * 3 * H + 8, dtype=torch.int16, device="cuda")
+    _lib.lib.msat_split_bf16x3(wip.data_ptr(), kxp, 3 * H, 3 * H, pi.data_ptr(), _lib.stream_ptr())
+    _lib.lib.msat_split_bf16x3(wh.data_ptr(), H, 3 * H, 3 * H, ph.data_ptr(), _lib.stream_ptr())
     for tape in (False, True):
-        for rs in ("1", "2", "t"):
-            os.environ["MARLSAT_GRU_RS"] = rs if rs != "t" else "2"
-            if rs == "t":
+        for rs in ("2", "t", "x3"):
+            os.environ["MARLSAT_GRU_RS"] = rs if rs in ("1", "2") else "2"
+            if rs == "x3":
+                f = lambda: _lib.lib.msat_gru_ln_fused_fwd_x3(*args, h.data_ptr(), H, pi.data_ptr(), kxp, bi.data_ptr(),
+                                                              ph.data_ptr(), bh.data_ptr(), sc.data_ptr(),
+                                                              lb.data_ptr(), out.data_ptr(), H,
+                                                              g4.data_ptr() if tape else 0, 4 * H, R, H,
+                                                              _lib.stream_ptr())
+            elif rs == "t":
                 f = lambda: _lib.lib.msat_gru_ln_fused_fwd_t(*args, h.data_ptr(), H, wiT.data_ptr(), bi.data_ptr(),
                                                              whT.data_ptr(), bh.data_ptr(), sc.data_ptr(),
                                                              lb.data_ptr(), out.data_ptr(), H,

@@ -80,6 +80,21 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
     args = []
     for t, off, ld, w in segs + [(None, 0, 0, 0)] * (3 - len(segs)):
         args += [t.data_ptr() + 4 * off if t is not None else 0, ld, w]
+    if layout == "x3":  # bf16x3 split kernel (H = 128): weights as split planes, Wi zero-padded to kxp
+        K = wi.shape[0]
+        kxp = (K + 15) // 16 * 16
+        wip = torch.zeros(kxp, 3 * H, device="cuda")
+        wip[:K] = wi
+        pi = torch.empty(3 * kxp * 3 * H + 8, dtype=torch.int16, device="cuda")
+        ph = torch.empty(3 * H * 3 * H + 8, dtype=torch.int16, device="cuda")
+        _lib.check(_lib.lib.msat_split_bf16x3(wip.data_ptr(), kxp, 3 * H, 3 * H, pi.data_ptr(), _lib.stream_ptr()), "split")
+        _lib.check(_lib.lib.msat_split_bf16x3(wh.data_ptr(), H, 3 * H, 3 * H, ph.data_ptr(), _lib.stream_ptr()), "split")
+        _lib.check(_lib.lib.msat_gru_ln_fused_fwd_x3(*args, h.data_ptr(), H, pi.data_ptr(), kxp, bi.data_ptr(),
+                                                     ph.data_ptr(), bh.data_ptr(), sc.data_ptr(), lb.data_ptr(),
+                                                     out.data_ptr(), H, g4.data_ptr() if g4 is not None else 0, 4 * H,
+                                                     R, H, _lib.stream_ptr()), "gru_ln_fused_fwd_x3")
+        torch.cuda.synchronize()
+        return out
     if layout == "t":  # transposed-weight kernel (k-major images, ds_read_b128 fragments)
         wiT, whT = _transposed(wi), _transposed(wh)
         assert bool((wiT[:, wi.shape[0]:] == 0).all()) and torch.equal(wiT[:, :wi.shape[0]], wi.t())
@@ -96,7 +111,7 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
     return out
 
 
-@pytest.mark.parametrize("layout", ["plain", "t"])
+@pytest.mark.parametrize("layout", ["plain", "t", "x3"])
 @pytest.mark.parametrize("R", [0, 1, 77, 1000, 70000])
 @pytest.mark.parametrize("H", [64, 128, 256])
 @pytest.mark.parametrize("kind", ["var", "clause", "var8", "clause4"])
@@ -105,6 +120,8 @@ def test_fused_forward_matches_reference(R, H, kind, layout):
         pytest.skip("large case at the production width only")
     if layout == "t" and H == 256:
         pytest.skip("transposed-weight kernel: H 64 / 128")
+    if layout == "x3" and H != 128:
+        pytest.skip("bf16x3 kernel: H 128")
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=R + H)
     g4 = torch.full((R, 4 * H), float("nan"), device="cuda")
     out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout)
