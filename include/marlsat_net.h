@@ -127,6 +127,14 @@ int msat_gru_ln_fused_fwd_x3(const float *x0, int32_t ld0, int32_t w0, const flo
  * (its prior contents are never read) instead of accumulating into it; bit 2 packs each row as
  * [dan | dar | daz | dan*r] (4H, dGh = dGi + H, lddi = lddh >= 4H): dGi is then in gate order
  * (n, r, z) and the r / z columns are written once for both. */
+/* msat_gru_ln_bwd_g4 plus (+=) the gradient of the input-matrix rows that multiply nfeat per-row
+ * features (nfeat 0, 2 or 6; feat (R, ldf)): dfeat[k][g H + j] = sum_rows feat[r][k] dG_g[r][j]
+ * (dfeat nfeat x 3H contiguous, gates r, z, n), reduced with the gate-bias partials in one pass. */
+int msat_gru_ln_bwd_g4f(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev, int32_t ldp,
+                        const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh, float *dhprev,
+                        int32_t lddp, float *dln_scale, float *dln_bias, float *dbi, float *dbh_n, const float *feat,
+                        int32_t ldf, int32_t nfeat, float *dfeat, float *partial, int32_t R, int32_t H,
+                        int32_t accumulate_ln, void *stream);
 int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
                        int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
                        float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *dbi, float *dbh_n,

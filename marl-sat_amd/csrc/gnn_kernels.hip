@@ -177,23 +177,30 @@ gru_ln_fwd_kernel(const float *__restrict__ Gi, int ldi, const float *__restrict
 // NQ = 6: the partials also carry the gate-bias gradients, part[block] =
 // [dscale | dbias | d b_ir | d b_iz | d b_in | d b_hn] (H each), so no column-sum pass
 // over dGi / dGh is needed.
-template <int PER, bool G4, int NQ = 2>
+// NF > 0: the partials also carry feature-weighted gate sums for the input-matrix rows of NF
+// per-row features (feat, ld ldf): part[block][NQ + 3k + g] = sum_rows feat[r][k] * dG_g[r]
+// (g = r, z, n gate) -- the weight gradient of those input rows without another pass over dGi.
+template <int PER, bool G4, int NQ = 2, int NF = 0>
 __global__ void __launch_bounds__(kRowThreads)
 gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
                   const float *__restrict__ scale, float *__restrict__ dGi, int lddi, float *__restrict__ dGh, int lddh,
                   float *__restrict__ dh, int lddh_prev, float *__restrict__ part, int R, int H, int dh_assign,
-                  int packed) {
-    __shared__ float s_part[4][NQ * 64 * PER];
+                  int packed, const float *__restrict__ feat, int ldf) {
+    constexpr int NQT = NQ + 3 * NF, QC = NQ;  // partial rows; LDS reduction in chunks of QC rows
+    __shared__ float s_part[4][QC * 64 * PER];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float pq[NQ][PER];
+    float pq[NQT][PER];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
+    for (int q = 0; q < NQT; ++q)
 #pragma unroll
         for (int u = 0; u < PER; ++u) pq[q][u] = 0.f;
     for (int r = blockIdx.x * 4 + w; r < R; r += gridDim.x * 4) {
         const float *gi = Gi + (size_t)r * ldi, *gh = G4 ? gi : Gh + (size_t)r * ldh, *h = hp + (size_t)r * ldp;
         const float *g = dy + (size_t)r * ldy;
+        float fw[NF > 0 ? NF : 1];
+#pragma unroll
+        for (int k = 0; k < NF; ++k) fw[k] = feat[(size_t)r * ldf + k];
         float rg[PER], zg[PER], ng[PER], hn[PER], hv[PER], ghn[PER], dyv[PER];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -266,17 +273,27 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
                 pq[4][u] += dan;
                 pq[5][u] += dan * rg[u];
             }
+#pragma unroll
+            for (int k = 0; k < NF; ++k) {
+                pq[NQ + 3 * k][u] += fw[k] * dar;
+                pq[NQ + 3 * k + 1][u] += fw[k] * daz;
+                pq[NQ + 3 * k + 2][u] += fw[k] * dan;
+            }
         }
     }
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
+    for (int q0 = 0; q0 < NQT; q0 += QC) {
+        if (q0) __syncthreads();
 #pragma unroll
-        for (int u = 0; u < PER; ++u) s_part[w][q * 64 * PER + lane + 64 * u] = pq[q][u];
-    __syncthreads();
-    for (int j = threadIdx.x; j < NQ * 64 * PER; j += kRowThreads) {
-        const float v = (s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]);
-        const int q = j / (64 * PER), jj = j - q * 64 * PER;
-        if (jj < H) part[(size_t)blockIdx.x * NQ * H + q * H + jj] = v;
+        for (int q = 0; q < QC; ++q)
+#pragma unroll
+            for (int u = 0; u < PER; ++u) s_part[w][q * 64 * PER + lane + 64 * u] = pq[q0 + q][u];
+        __syncthreads();
+        for (int j = threadIdx.x; j < QC * 64 * PER; j += kRowThreads) {
+            const float v = (s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]);
+            const int q = j / (64 * PER), jj = j - q * 64 * PER;
+            if (jj < H) part[(size_t)blockIdx.x * NQT * H + (q0 + q) * H + jj] = v;
+        }
     }
 }
 
@@ -573,8 +590,8 @@ extern "C" int msat_gru_ln_fwd(const float *Gi, int32_t ldi, const float *Gh, in
 }
 
 extern "C" size_t msat_gru_ln_bwd_partial_floats(int32_t R, int32_t H) {
-    const size_t nb = bwd_blocks(R);
-    return nb * 6 * H + (nb + kPartRows - 1) / kPartRows * 6 * H;  // block partials + reduction workspace
+    const size_t nb = bwd_blocks(R), q = 6 + 3 * 6;  // LN + gate biases + up to six feature rows
+    return nb * q * H + (nb + kPartRows - 1) / kPartRows * q * H;  // block partials + reduction workspace
 }
 
 extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, int32_t ldi, const float *Gh, int32_t ldh,
@@ -590,23 +607,26 @@ extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, in
     hipStream_t s = (hipStream_t)stream;
     const int nb = bwd_blocks(R);
     const dim3 g(nb), b(kRowThreads);
-    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0);
-    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0);
-    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0);
+    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0);
+    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0);
+    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0);
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
     return reduce_partials(partial, nb, 2 * H, dln_scale, accumulate_ln, partial + (size_t)nb * 2 * H, s);
 }
 
-extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
-                                  int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
-                                  float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *dbi,
-                                  float *dbh_n, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
-                                  void *stream) {
+extern "C" int msat_gru_ln_bwd_g4f(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
+                                   int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh,
+                                   int32_t lddh, float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias,
+                                   float *dbi, float *dbh_n, const float *feat, int32_t ldf, int32_t nfeat,
+                                   float *dfeat, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
+                                   void *stream) {
     MSAT_REQUIRE(H == 64 || H == 128 || H == 256, "gru_ln: H must be 64, 128 or 256 (got %d)", H);
     MSAT_REQUIRE(ldg >= 4 * H, "gru_ln_bwd_g4: ldg must be >= 4H");
     MSAT_REQUIRE(dln_bias == dln_scale + H, "dln_bias must follow dln_scale (contiguous [scale|bias] grads)");
     MSAT_REQUIRE((dbi == nullptr) == (dbh_n == nullptr), "gru_ln_bwd_g4: dbi and dbh_n go together");
+    MSAT_REQUIRE(nfeat == 0 || ((nfeat == 2 || nfeat == 6) && feat && dfeat && dbi && ldf >= nfeat),
+                 "gru_ln_bwd_g4f: nfeat must be 0, 2 or 6 (with feat, dfeat and the bias outputs)");
     if (R == 0) return MSAT_OK;
     MSAT_REQUIRE(dy && g4 && hprev && ln_scale && dGi && dGh && dhprev && dln_scale && partial, "NULL pointer");
     hipStream_t s = (hipStream_t)stream;
@@ -618,24 +638,26 @@ extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4,
     accumulate_ln &= 1;
     MSAT_REQUIRE(!packed || (dGh == dGi + H && lddi == lddh && lddi >= 4 * H),
                  "gru_ln_bwd_g4: packed rows need dGh = dGi + H and a shared ld >= 4H");
-    const int NQ = bias ? 6 : 2;
-#define MSAT_BWD(PER)                                                                                              \
-    if (bias)                                                                                                      \
-        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, 6>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,    \
-                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed);                \
-    else                                                                                                           \
-        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, 2>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,    \
-                           ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed);
+    const int NQ = (bias ? 6 : 2) + 3 * nfeat;
+#define MSAT_BWD1(PER, Q, F)                                                                                      \
+    hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,   \
+                       ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed, feat, ldf)
+#define MSAT_BWD(PER)                                                                                             \
+    if (!bias) MSAT_BWD1(PER, 2, 0);                                                                               \
+    else if (nfeat == 0) MSAT_BWD1(PER, 6, 0);                                                                     \
+    else if (nfeat == 2) MSAT_BWD1(PER, 6, 2);                                                                     \
+    else MSAT_BWD1(PER, 6, 6);
     if (H == 64) { MSAT_BWD(1) }
     else if (H == 128) { MSAT_BWD(2) }
     else { MSAT_BWD(4) }
 #undef MSAT_BWD
+#undef MSAT_BWD1
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
     // stage 1: 16-row float4 sums of the block partials; stage 2: fixed-order reduce of each column segment
     float *ws = partial + (size_t)nb * NQ * H;
     const int sp = (nb + kPartRows - 1) / kPartRows, width = NQ * H, W4 = width / 4;
-    MSAT_REQUIRE(a16(partial) && a16(dln_scale) && (!bias || (a16(dbi) && a16(dbh_n))),
+    MSAT_REQUIRE(a16(partial) && a16(dln_scale) && (!bias || (a16(dbi) && a16(dbh_n))) && (!nfeat || a16(dfeat)),
                  "gru_ln_bwd_g4: partial / gradient outputs must be 16-byte aligned");
     hipLaunchKernelGGL(colsum4_kernel, dim3((W4 + 15) / 16, sp), dim3(256), 0, s,
                        reinterpret_cast<const float4 *>(partial), W4, nb, W4, kPartRows, reinterpret_cast<float4 *>(ws));
@@ -650,7 +672,21 @@ extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4,
         hipLaunchKernelGGL(partial_reduce4_kernel, dim3((H / 4 + 15) / 16), dim3(256), 0, s, ws4 + 5 * H / 4, sp, H / 4,
                            W4, reinterpret_cast<float4 *>(dbh_n), 1);
     }
+    if (nfeat) {  // feature rows: nfeat x 3H contiguous (the rows of the input matrix, ld 3H), accumulated
+        const int fw4 = 3 * nfeat * H / 4;
+        hipLaunchKernelGGL(partial_reduce4_kernel, dim3((fw4 + 15) / 16), dim3(256), 0, s, ws4 + 6 * H / 4, sp, fw4, W4,
+                           reinterpret_cast<float4 *>(dfeat), 1);
+    }
     return check_launch("partial_reduce4_kernel");
+}
+
+extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
+                                  int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
+                                  float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *dbi,
+                                  float *dbh_n, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
+                                  void *stream) {
+    return msat_gru_ln_bwd_g4f(dy, ldy, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, dln_scale,
+                               dln_bias, dbi, dbh_n, nullptr, 0, 0, nullptr, partial, R, H, accumulate_ln, stream);
 }
 
 extern "C" int msat_assemble_graph_batch(

@@ -125,6 +125,7 @@ def _load():
     sig["msat_gru_ln_fused_fwd_t"] = sig["msat_gru_ln_fused_fwd"]
     sig["msat_gru_ln_fused_fwd_x3"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, I, P, P, P, P, P, P, I, P, I, I, I, P])
     sig["msat_gru_ln_bwd_g4"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, I, P])
+    sig["msat_gru_ln_bwd_g4f"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, P, P, I, I, I, P])
     sig["msat_gru_ln_bwd_partial_floats"] = (Z, [I, I])
     sig["msat_gru_ln_bwd"] = (I, [P, I, P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, I, I, I, P])
     sig["msat_colsum_workspace_floats"] = (Z, [I, I])
@@ -174,6 +175,7 @@ EXPORTED = (
     "msat_gru_ln_fwd",
     "msat_gru_ln_fused_fwd",
     "msat_gru_ln_bwd_g4",
+    "msat_gru_ln_bwd_g4f",
     "msat_gru_ln_bwd_partial_floats",
     "msat_gru_ln_bwd",
     "msat_colsum_workspace_floats",

@@ -418,11 +418,12 @@ class GNNActorCritic:
                 dgi, dgh, ldd, keep = dG_buffers(Nv)
                 dHx0 = e(Nv, H)  # written (not accumulated) by the backward kernel: flags bit 1
                 part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nv, H)))
-                _chk(L_.msat_gru_ln_bwd_g4(dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, pp(ln[k]),
-                                           dgi, ldd, dgh, ldd, dHx0.data_ptr(), H,
-                                           pp(dln[k]), pp(dln[k], H), self.g(f"enc.{cell}_bi").data_ptr(),
-                                           pp(self.g(f"enc.{cell}_bh"), 2 * H), part.data_ptr(), Nv, H, flags,
-                                           self.stream), "gru_ln_bwd_g4")
+                # dF rows H..H+5 (x, svf, n+, n-) from the same pass: feature-weighted gate sums
+                _chk(L_.msat_gru_ln_bwd_g4f(dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, pp(ln[k]),
+                                            dgi, ldd, dgh, ldd, dHx0.data_ptr(), H,
+                                            pp(dln[k]), pp(dln[k], H), self.g(f"enc.{cell}_bi").data_ptr(),
+                                            pp(self.g(f"enc.{cell}_bh"), 2 * H), b.vfeat.data_ptr(), 8, 6,
+                                            pp(gF[H]), part.data_ptr(), Nv, H, flags, self.stream), "gru_ln_bwd_g4f")
                 wh, gwh = self.p(f"enc.{cell}_wh"), self.g(f"enc.{cell}_wh")
                 sfx = cell[-2:]
                 self._dgrad(dgh, ldd, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1)
@@ -430,7 +431,6 @@ class GNNActorCritic:
                 # input path: d(gathered) and dF rows [fold | x/svf | counts]
                 self._dgrad(dgi, ldd, F, pl["Fp" if half == 0 else "Fn"], pp(dNV, half * H), 2 * H, Nv, H, W3, 0)
                 dF_wgrad(pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), Nv, H)
-                dF_wgrad(b.vfeat.data_ptr(), 8, dgi, ldd, pp(gF[H]), Nv, 8)
                 dprev[half] = dHx0
             # var gather backward: dH_c (+)= A+^T dNV+ + A-^T dNV-  (one merged clause gather)
             _chk(L_.msat_clause_gather2(dNV.data_ptr(), pp(dNV, H), 2 * H, b.slots.data_ptr(), dHc.data_ptr(), H, Nc,
@@ -439,17 +439,16 @@ class GNNActorCritic:
             dgi, dgh, ldd, keep = dG_buffers(Nc)
             dHc0 = e(Nc, H)
             part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nc, H)))
-            _chk(L_.msat_gru_ln_bwd_g4(dHc.data_ptr(), H, t.G4c.data_ptr(), 4 * H, t.Hc.data_ptr(), H, pp(ln[3 * l]),
-                                       dgi, ldd, dgh, ldd, dHc0.data_ptr(), H,
-                                       pp(dln[3 * l]), pp(dln[3 * l], H), self.g("enc.gru_c_bi").data_ptr(),
-                                       pp(self.g("enc.gru_c_bh"), 2 * H), part.data_ptr(), Nc, H, flags, self.stream),
-                 "gru_ln_bwd_g4")
+            _chk(L_.msat_gru_ln_bwd_g4f(dHc.data_ptr(), H, t.G4c.data_ptr(), 4 * H, t.Hc.data_ptr(), H,
+                                        pp(ln[3 * l]), dgi, ldd, dgh, ldd, dHc0.data_ptr(), H,
+                                        pp(dln[3 * l]), pp(dln[3 * l], H), self.g("enc.gru_c_bi").data_ptr(),
+                                        pp(self.g("enc.gru_c_bh"), 2 * H), b.cdeg.data_ptr(), 4, 2,
+                                        pp(gFc[2 * H]), part.data_ptr(), Nc, H, flags, self.stream), "gru_ln_bwd_g4f")
             self._dgrad(dgh, ldd, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1)
             self._wgrad(t.Hc.data_ptr(), H, dgh, ldd, self.g("enc.gru_c_wh").data_ptr(), W3, Nc, H, W3)
             dGIN = e(Nc, 2 * H)
             self._dgrad(dgi, ldd, Fc, pl["Fc"], dGIN.data_ptr(), 2 * H, Nc, 2 * H, W3, 0)
             dF_wgrad(t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), Nc, 2 * H)
-            dF_wgrad(b.cdeg.data_ptr(), 4, dgi, ldd, pp(gFc[2 * H]), Nc, 4)
             # clause gather backward: dH_v+/- (+)= A+/- dGIN+/-
             _chk(L_.msat_var_gather2(dGIN.data_ptr(), pp(dGIN, H), 2 * H, b.ptr.data_ptr(), b.inc.data_ptr(),
                                      dprev[0].data_ptr(), dprev[1].data_ptr(), H, Nv, H, 1, self.stream),

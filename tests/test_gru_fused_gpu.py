@@ -143,9 +143,10 @@ def test_fused_forward_matches_reference(R, H, kind, layout):
     assert bool((terr <= 2e-6 * ab + 1e-30).all()), float((terr / (ab + 1e-30)).max())
 
 
+@pytest.mark.parametrize("nfeat", [0, 2, 6])  # msat_gru_ln_bwd_g4f feature-weighted gate sums
 @pytest.mark.parametrize("assign", [False, True])  # flags bit 1: dhprev overwritten, never read
 @pytest.mark.parametrize("R,H", [(77, 64), (1000, 128), (300, 256)])
-def test_g4_backward_matches_autograd(R, H, assign):
+def test_g4_backward_matches_autograd(R, H, assign, nfeat):
     from marlsat import _lib
 
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, "var", seed=7 * R + H)
@@ -159,11 +160,14 @@ def test_g4_backward_matches_autograd(R, H, assign):
     dbi = torch.full((3 * H,), 0.5, device="cuda")  # accumulated into
     dbh = torch.full((3 * H,), 0.5, device="cuda")
     part = torch.empty(int(_lib.lib.msat_gru_ln_bwd_partial_floats(R, H)), device="cuda")
-    _lib.check(_lib.lib.msat_gru_ln_bwd_g4(dy.data_ptr(), H, g4.data_ptr(), 4 * H, h.data_ptr(), H, sc.data_ptr(),
-                                           dGi.data_ptr(), 3 * H, dGh.data_ptr(), 3 * H, dh.data_ptr(), H,
-                                           dln.data_ptr(), dln.data_ptr() + 4 * H, dbi.data_ptr(),
-                                           dbh.data_ptr() + 4 * 2 * H, part.data_ptr(), R, H, 3 if assign else 1,
-                                           _lib.stream_ptr()), "gru_ln_bwd_g4")
+    feat = torch.randn(R, 8, device="cuda", generator=torch.Generator(device="cuda").manual_seed(6))
+    dfeat = torch.full((max(nfeat, 1), 3 * H), 0.25, device="cuda")
+    _lib.check(_lib.lib.msat_gru_ln_bwd_g4f(dy.data_ptr(), H, g4.data_ptr(), 4 * H, h.data_ptr(), H, sc.data_ptr(),
+                                            dGi.data_ptr(), 3 * H, dGh.data_ptr(), 3 * H, dh.data_ptr(), H,
+                                            dln.data_ptr(), dln.data_ptr() + 4 * H, dbi.data_ptr(),
+                                            dbh.data_ptr() + 4 * 2 * H, feat.data_ptr() if nfeat else 0, 8, nfeat,
+                                            dfeat.data_ptr() if nfeat else 0, part.data_ptr(), R, H,
+                                            3 if assign else 1, _lib.stream_ptr()), "gru_ln_bwd_g4f")
     torch.cuda.synchronize()
     # autograd through the float64 reference w.r.t. gi, gh (pre-activation gate vectors), h, LN params
     d = lambda t: t.double().detach().requires_grad_(True)
@@ -185,3 +189,8 @@ def test_g4_backward_matches_autograd(R, H, assign):
         err = float((got.double() - ref).abs().max())
         assert err <= 1e-4 * scale + 1e-6, (what, err, scale)
     assert bool((dbh[:2 * H] == 0.5).all())  # b_hr / b_hz do not exist (flax): untouched
+    if nfeat:
+        ref = feat[:, :nfeat].double().t() @ gi.grad  # (nfeat, 3H): gates r, z, n
+        got = dfeat.double() - 0.25
+        scale = float(ref.abs().max())
+        assert float((got - ref).abs().max()) <= 1e-4 * scale + 1e-6
