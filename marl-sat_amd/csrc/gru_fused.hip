@@ -430,10 +430,12 @@ __global__ void transpose_pad_kernel(const float *__restrict__ W, int K, int N, 
 //   side), read as 8-row column fragments with ds_read_b64_tr_b16.
 constexpr int kXR = 128;  // rows per workgroup (x3 kernel)
 
-template <int NW>
-__global__ void __launch_bounds__(64 * NW * 4, 1)
+// RS = row groups of waves: 4 -> 16 waves x 32 rows (RT = 1); 2 -> 8 waves x 64 rows (RT = 2:
+// each weight fragment read once per two row tiles, half the transposed LDS reads per MFMA).
+template <int NW, int RS>
+__global__ void __launch_bounds__(64 * NW * RS, 1)
 gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
-    constexpr int H = 32 * NW, T = 64 * NW * 4, BW = 3 * H, RS = 4;
+    constexpr int H = 32 * NW, T = 64 * NW * RS, BW = 3 * H, RT = 4 / RS;
     static_assert(H == 128, "x3 GRU: one 128-column image per gate");
     constexpr int APL = kXR * kFK;            // bf16 per A plane (128 rows x 16 k)
     constexpr int BPL = kFK * H;              // bf16 per (plane, gate) image (16 k x 128 cols)
@@ -443,7 +445,7 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * 3 * BPL];
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wu = w % NW, wrow = (w / NW) * 32;
+    const int wu = w % NW, wrow = (w / NW) * 32 * RT;
     const int row0 = blockIdx.x * kXR;
     const int nsh = H / kFK;
     const int ns = nsh + a.kxp / kFK;
@@ -495,32 +497,40 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
         }
     };
 
-    f32x16 acc[1][4];
+    f32x16 acc[RT][4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) acc[0][g] = f32x16{};
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[i][g] = f32x16{};
     const int li = lane & 31, lk = lane >> 5, gl = (lane >> 4) & 1;
     auto slab = [&](int buf, bool hid) {
-        bf16x8 fa[3];
-        const int r = wrow + li;
+        bf16x8 fa[RT][3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-            fa[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(
-                                                   reinterpret_cast<const char *>(As[buf][q]) + r * 32 +
-                                                   16 * (lk ^ ((r >> 3) & 1))));
+        for (int i = 0; i < RT; ++i) {
+            const int r = wrow + 32 * i + li;
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                fa[i][q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(
+                                                          reinterpret_cast<const char *>(As[buf][q]) + r * 32 +
+                                                          16 * (lk ^ ((r >> 3) & 1))));
+        }
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
             bf16x8 fb[3];
 #pragma unroll
             for (int q = 0; q < 3; ++q) fb[q] = tr_frag(Bs[buf] + (q * 3 + g) * BPL, 8 * lk, (32 * wu + 16 * gl) >> 3, lane);
             const int ai = g < 2 ? g : (hid ? 3 : 2);
-            f32x16 c = acc[0][ai];
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], c, 0, 0, 0);
-            acc[0][ai] = c;
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                f32x16 c = acc[i][ai];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], c, 0, 0, 0);
+                acc[i][ai] = c;
+            }
         }
     };
 
@@ -720,7 +730,9 @@ extern "C" int msat_gru_ln_fused_fwd_x3(const float *x0, int32_t ld0, int32_t w0
     a.ldg = ldg;
     a.R = R;
     a.Kx = Kx;
-    hipLaunchKernelGGL((gru_ln_fused_fwd_x3_kernel<4>), dim3((R + kXR - 1) / kXR), dim3(1024), 0, (hipStream_t)stream,
-                       a);
+    // 16 waves x 32 rows; 8 waves x 64 rows (RS = 2, half the transposed reads per MFMA but half the
+    // waves) measured 3-12 % slower (profiles/gru_bench.py)
+    hipLaunchKernelGGL((gru_ln_fused_fwd_x3_kernel<4, 4>), dim3((R + kXR - 1) / kXR), dim3(1024), 0,
+                       (hipStream_t)stream, a);
     return check_launch("gru_ln_fused_fwd_x3_kernel");
 }
