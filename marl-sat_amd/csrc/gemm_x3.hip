@@ -56,21 +56,30 @@ __global__ void split_bf16x3_kernel(const float *__restrict__ W, int rows, int c
 }
 
 // C[M,N] (+)= A[M,K] @ W^T + bias, W planes [3][N][K] bf16.  K % 16 == 0, lda % 4 == 0, A 16-B aligned.
-__global__ void __launch_bounds__(kX3T, 3)
+// TI = 32-row MFMA tiles per wave: the workgroup tile is (64 TI) x 128 (2 x 2 waves).  TI = 4 reads
+// each weight fragment once for four row tiles (0.375 LDS fragment reads per MFMA instead of 0.5)
+// at two workgroups per CU instead of three.
+template <int TI>
+__global__ void __launch_bounds__(kX3T, TI == 2 ? 3 : 2)
 gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ Wp, float *__restrict__ C, int ldc,
                const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
-    __shared__ uint4 lds[2][6][kX3Plane];  // [buf][A planes 0..2 | W planes 3..5], 48 KiB
+    constexpr int MT = 64 * TI, APL = MT * 2, SR = TI / 2;  // tile rows; A plane uint4s; staging rows per thread
+    __shared__ uint4 lds_raw[2 * 3 * (APL + kX3Plane)];  // [buf][A planes] then [buf][W planes]
+    uint4 (*lds_a)[3][APL] = reinterpret_cast<uint4 (*)[3][APL]>(lds_raw);
+    uint4 (*lds_w)[3][kX3Plane] = reinterpret_cast<uint4 (*)[3][kX3Plane]>(lds_raw + 2 * 3 * APL);
     const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
-    const int m0 = (id / ntn) * kX3M, n0 = (id % ntn) * kX3M;
+    const int m0 = (id / ntn) * MT, n0 = (id % ntn) * kX3M;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
-    const int srow = t >> 1, shalf = t & 1;  // staging: one row-half (8 k values) per thread
-    const float *arow = A + (size_t)min(m0 + srow, M - 1) * lda + 8 * shalf;
+    const int wr = (w >> 1) * 32 * TI, wc = (w & 1) * 64;
+    const int srow = t >> 1, shalf = t & 1;  // staging: row-halves (8 k values) srow + 128 j
+    const float *arow[SR];
+#pragma unroll
+    for (int j = 0; j < SR; ++j) arow[j] = A + (size_t)min(m0 + srow + 128 * j, M - 1) * lda + 8 * shalf;
     const size_t NK = (size_t)N * K;
     const __bf16 *wrow = Wp + (size_t)min(n0 + srow, N - 1) * K + 8 * shalf;
-    f32x16v acc[2][2];
+    f32x16v acc[TI][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16v{};
     const int ns = K / kX3D;
@@ -78,33 +87,41 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
     // one slab ahead by LDS-DMA.  Per slab s: issue W(s+1), then load A(s+2) (so waiting for W(s+1)
     // never waits for A(s+2): vector-memory counts retire in issue order), multiply slab s, split
     // and store A(s+1), barrier.
-    float4 R0[2], R1[2];
-    auto loadA = [&](int s, float4 (&r)[2]) {
-        const float4 *p = reinterpret_cast<const float4 *>(arow + s * kX3D);
-        r[0] = p[0];
-        r[1] = p[1];
-    };
-    auto storeA = [&](const float4 (&r)[2], int buf) {
-        const Split8 sp = split8(r[0], r[1]);
+    float4 R0[SR][2], R1[SR][2];
+    auto loadA = [&](int s, float4 (&r)[SR][2]) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) lds[buf][q][t] = sp.p[q];
+        for (int j = 0; j < SR; ++j) {
+            const float4 *p = reinterpret_cast<const float4 *>(arow[j] + s * kX3D);
+            r[j][0] = p[0];
+            r[j][1] = p[1];
+        }
+    };
+    auto storeA = [&](const float4 (&r)[SR][2], int buf) {
+#pragma unroll
+        for (int j = 0; j < SR; ++j) {
+            const Split8 sp = split8(r[j][0], r[j][1]);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) lds_a[buf][q][t + 256 * j] = sp.p[q];
+        }
     };
     auto issueW = [&](int s, int buf) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) glds16_async(wrow + q * NK + s * kX3D, &lds[buf][3 + q][w * 64]);
+        for (int q = 0; q < 3; ++q) glds16_async(wrow + q * NK + s * kX3D, &lds_w[buf][q][w * 64]);
     };
     const int li = lane & 31, h = lane >> 5;
     auto slab = [&](int buf) {
-        bf16x8 fa[2][3], fb[2][3];
+        bf16x8 fa[TI][3], fb[2][3];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int q = 0; q < 3; ++q) {
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                fa[i][q] = __builtin_bit_cast(bf16x8, lds[buf][q][(wr + 32 * i + li) * 2 + h]);
-                fb[i][q] = __builtin_bit_cast(bf16x8, lds[buf][3 + q][(wc + 32 * i + li) * 2 + h]);
-            }
+            for (int i = 0; i < TI; ++i)
+                fa[i][q] = __builtin_bit_cast(bf16x8, lds_a[buf][q][(wr + 32 * i + li) * 2 + h]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < 2; ++j)
+                fb[j][q] = __builtin_bit_cast(bf16x8, lds_w[buf][q][(wc + 32 * j + li) * 2 + h]);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 f32x16v c = acc[i][j];
@@ -124,8 +141,9 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
     wait_vmcnt<0>();
     barrier_lds();
     if (ns > 2) loadA(2, R0);
+    constexpr int NL = 2 * SR;  // A loads per slab per thread
     // Rn holds A(s+1); Rf is free and receives A(s+2)
-    auto iter = [&](int s, float4 (&Rn)[2], float4 (&Rf)[2]) {
+    auto iter = [&](int s, float4 (&Rn)[SR][2], float4 (&Rf)[SR][2]) {
         const int buf = s & 1;
         const bool more = s + 1 < ns;
         if (more) issueW(s + 1, buf ^ 1);
@@ -135,7 +153,7 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
         if (more) storeA(Rn, buf ^ 1);
         // W(s+1) and A(s+1) landed; A(s+2) (issued after W(s+1) for s >= 1) may fly.  At s = 0,
         // A(2) precedes W(1) in issue order, so the wait drains everything.
-        if (s >= 1 && s + 2 < ns) wait_vmcnt<2>();
+        if (s >= 1 && s + 2 < ns) wait_vmcnt<NL>();
         else wait_vmcnt<0>();
         barrier_lds();
     };
@@ -143,12 +161,12 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
         iter(s, R1, R0);
         if (s + 1 < ns) iter(s + 1, R0, R1);
     }
-    float *ldsf = reinterpret_cast<float *>(&lds[0][0][0]);
+    float *ldsf = reinterpret_cast<float *>(lds_raw);  // >= 48 KiB: four 8 KiB epilogue stages
     if (vec_out) {
         // LDS-staged epilogue: each wave's 32x64 half-tile leaves as whole 256-byte rows of float4
         float *stage = ldsf + w * 32 * 64;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < TI; ++i) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -178,7 +196,7 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
         return;
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int col = n0 + wc + 32 * j + (lane & 31);
@@ -328,10 +346,19 @@ extern "C" int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, fl
     MSAT_REQUIRE(K % kX3D == 0 && lda % 4 == 0 && lda >= K && ldc >= N && a16x3(A) && a16x3(Wplanes) &&
                      (K * 2) % 16 == 0,
                  "gemm_x3: K %% 16, lda %% 4 and 16-byte aligned operands required");
-    const int ntm = (M + kX3M - 1) / kX3M, ntn = (N + kX3M - 1) / kX3M;
+    const int ntn = (N + kX3M - 1) / kX3M;
     const int vec = (N % 4 == 0 && ldc % 4 == 0 && a16x3(C) && (!bias || a16x3(bias))) ? 1 : 0;
-    hipLaunchKernelGGL(gemm_x3_kernel, dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
-                       reinterpret_cast<const __bf16 *>(Wplanes), C, ldc, bias, M, N, K, accumulate, ntn, vec);
+    const char *e = getenv("MARLSAT_GEMM_X3_TI");  // 32-row tiles per wave: 2 (128-row tile) or 4 (256)
+    const __bf16 *Wb = reinterpret_cast<const __bf16 *>(Wplanes);
+    if (e && atoi(e) == 4) {
+        const int ntm = (M + 255) / 256;
+        hipLaunchKernelGGL((gemm_x3_kernel<4>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda, Wb, C,
+                           ldc, bias, M, N, K, accumulate, ntn, vec);
+    } else {
+        const int ntm = (M + 127) / 128;
+        hipLaunchKernelGGL((gemm_x3_kernel<2>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda, Wb, C,
+                           ldc, bias, M, N, K, accumulate, ntn, vec);
+    }
     return check_launch("gemm_x3_kernel");
 }
 

@@ -37,9 +37,12 @@ for M, N, K, tb, what in GEMMS:
         planes = torch.empty(3 * N * K, dtype=torch.int16, device="cuda")
         L.msat_split_bf16x3(B.data_ptr(), N, K, K, planes.data_ptr(), s)
         f3 = lambda: L.msat_gemm_x3(A.data_ptr(), K, planes.data_ptr(), C.data_ptr(), N, 0, M, N, K, 1, s)
-        us = timeit(f3)
-        print(json.dumps({"what": "gemm_x3 " + what, "M": M, "N": N, "K": K, "us": round(us, 1),
-                          "tflops": round(2 * M * N * K / us / 1e6, 1)}))
+        for ti in ("2", "4"):
+            os.environ["MARLSAT_GEMM_X3_TI"] = ti
+            us = timeit(f3)
+            print(json.dumps({"what": f"gemm_x3 ti{ti} " + what, "M": M, "N": N, "K": K, "us": round(us, 1),
+                              "tflops": round(2 * M * N * K / us / 1e6, 1)}))
+        os.environ.pop("MARLSAT_GEMM_X3_TI")
     del A, B, C
 for M, K, N, what in WGRADS:
     A = torch.randn(M, K, device="cuda"); G = torch.randn(M, N, device="cuda"); W = torch.empty(K, N, device="cuda")

@@ -176,13 +176,15 @@ def test_colsum_deterministic(M, N, ld, off):
     assert torch.equal(res[0][:oo], out0[:oo]) and torch.equal(res[0][oo + N:], out0[oo + N:])
 
 
+@pytest.mark.parametrize("ti", ["2", "4"])  # 128- / 256-row workgroup tiles
 @pytest.mark.parametrize("M,N,K", [(1, 4, 16), (130, 132, 64), (1000, 384, 384), (5000, 128, 384), (257, 256, 128),
                                    (3, 7, 32)])
-def test_gemm_x3_fp32_accuracy(M, N, K):
+def test_gemm_x3_fp32_accuracy(M, N, K, ti, monkeypatch):
     """bf16x3 split GEMM: C = A @ W^T (+ bias, + C) at fp32 accuracy (same bound as the f32 MFMA
     kernels: 2e-6 of sum |a b|), including values spanning many binades."""
     from marlsat import _lib
 
+    monkeypatch.setenv("MARLSAT_GEMM_X3_TI", ti)
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     A = torch.randn(M, K, device="cuda", generator=g) * torch.exp2(torch.randint(-6, 7, (M, K), device="cuda",
                                                                                 generator=g).float())
