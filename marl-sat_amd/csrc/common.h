@@ -67,6 +67,18 @@ __device__ __forceinline__ void glds16_async(const void *src, const void *lds) {
         : "memory");
 }
 
+// Same, with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset (the saddr
+// form): no 64-bit per-lane address arithmetic in the issuing loop.
+__device__ __forceinline__ void glds16_async_s(const void *sbase, unsigned voff, const void *lds) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(dst)
+        : "memory");
+}
+
 // s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory operations are done.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

@@ -23,6 +23,8 @@
 // (R x 4H) that gru_ln_bwd (G4 form) consumes.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "split3.h"
 
@@ -62,6 +64,16 @@ __device__ __forceinline__ void gru_ln_epilogue(const GruFwdArgs &a, f32x16 (&ac
     const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
     const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
     float2 *red = reinterpret_cast<float2 *>(red_lds);  // [NW][64]
+    // h of every row first, all loads in flight together (clamped rows; the value of a row
+    // past R is never stored)
+    float hvs[RT][16];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = row0 + wrow + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
+            hvs[rt][reg] = a.hp[(size_t)(row < a.R ? row : a.R - 1) * a.ldp + u];
+        }
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -70,9 +82,8 @@ __device__ __forceinline__ void gru_ln_epilogue(const GruFwdArgs &a, f32x16 (&ac
             const int row = row0 + lr;
             const float rp = acc[rt][0][reg] + br, zp = acc[rt][1][reg] + bz;
             const float gi = acc[rt][2][reg] + bni, gh = acc[rt][3][reg] + bnh;
-            float hv = 0.0f;
+            const float hv = hvs[rt][reg];
             if (row < a.R) {
-                hv = a.hp[(size_t)row * a.ldp + u];
                 if (a.g4) {
                     float *q = a.g4 + (size_t)row * a.ldg + u;
                     q[0] = rp;
@@ -430,69 +441,94 @@ __global__ void transpose_pad_kernel(const float *__restrict__ W, int K, int N, 
 //   side), read as 8-row column fragments with ds_read_b64_tr_b16.
 constexpr int kXR = 128;  // rows per workgroup (x3 kernel)
 
-// RS = row groups of waves: 4 -> 16 waves x 32 rows (RT = 1); 2 -> 8 waves x 64 rows (RT = 2:
-// each weight fragment read once per two row tiles, half the transposed LDS reads per MFMA).
+// 16 waves x 32 rows (RS = 4, RT = 1).
+//
+// Pipeline: every global read of the loop is an LDS-DMA issued from asm (glds16_async*), so the
+// compiler inserts no vector-memory waits and one counted wait per slab is exact.  In step s
+// (planes buffer s & 1):
+//   issue the weight DMA of slab s + 1 (Bs[(s + 1) & 1]) and the raw fp32 activation DMA of
+//   slab s + 3 (raw ring slot (s + 3) % 3);
+//   MFMAs of slab s;
+//   split the raw activations of slab s + 1 (landed one step ago) into the bf16 planes (s + 1) & 1;
+//   wait for all but the youngest DMA (slab s + 3's activations) and barrier.
+// The hidden-state slabs and the input slabs run as two loops with the gate index of the third
+// accumulator fixed at compile time.  Raw activation rows past R are clamped (and zeroed when
+// split), k past Kx reads a valid address (zeroed when split).
 template <int NW, int RS>
 __global__ void __launch_bounds__(64 * NW * RS, 1)
 gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
     constexpr int H = 32 * NW, T = 64 * NW * RS, BW = 3 * H, RT = 4 / RS;
     static_assert(H == 128, "x3 GRU: one 128-column image per gate");
+    static_assert(T == 1024, "x3 GRU: 16 waves");
     constexpr int APL = kXR * kFK;            // bf16 per A plane (128 rows x 16 k)
     constexpr int BPL = kFK * H;              // bf16 per (plane, gate) image (16 k x 128 cols)
     constexpr int BCH = 3 * 3 * BPL / 8;      // 16-byte chunks of a B slab (2304)
-    constexpr int BN = (BCH + T - 1) / T;     // glds per thread (3, guarded)
+    constexpr int BN = (BCH + T - 1) / T;     // glds per thread (3, the last on waves 0..3)
+    constexpr int RAWW = kXR * kFK * 4 / 1024;  // waves issuing the raw A DMA (8)
     __shared__ __attribute__((aligned(16))) unsigned short As[2][3][APL];
     __shared__ __attribute__((aligned(16))) unsigned short Bs[2][3 * 3 * BPL];
+    __shared__ __attribute__((aligned(16))) float Raw[3][kXR * kFK];
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(w);  // wave index, provably uniform
     const int wu = w % NW, wrow = (w / NW) * 32 * RT;
     const int row0 = blockIdx.x * kXR;
-    const int nsh = H / kFK;
+    constexpr int nsh = H / kFK;
     const int ns = nsh + a.kxp / kFK;
 
-    // A staging: threads 0..511 -> row t >> 2, k quad t & 3
-    const bool stager = t < kXR * 4;
-    const int arow = (t >> 2) & (kXR - 1), akq = (t & 3) * 4;
-    float4 ra;
-    auto loadA = [&](int s) {
-        ra = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int r = row0 + arow;
-        if (!stager || r >= a.R) return;
-        const float *p = nullptr;
-        if (s < nsh) {
-            p = a.hp + (size_t)r * a.ldp + s * kFK + akq;
-        } else {
-            int k = (s - nsh) * kFK + akq;
-#pragma unroll
-            for (int g = 0; g < 3; ++g) {
-                if (!p && k < a.seg_w[g]) p = a.seg[g] + (size_t)r * a.seg_ld[g] + k;
-                k -= a.seg_w[g];
-            }
+    // raw A DMA: waves 0..7, lane -> row 16 wv + (lane >> 2), k quad lane & 3 (16 B each);
+    // Raw[slot] is row-major [128][16] fp32
+    const bool rawer = wv < RAWW;
+    const int rrow = (wv & (RAWW - 1)) * 16 + (lane >> 2), rk = (lane & 3) * 4;
+    const int rr = row0 + rrow;
+    const int rrc = rr < a.R ? rr : a.R - 1;
+    const int w0 = a.seg_w[0], w01 = a.seg_w[0] + a.seg_w[1], kx_end = a.Kx;
+    // segment bases / strides as scalars (a per-lane select between struct members is otherwise
+    // turned into a per-lane load of the kernel argument block)
+    const float *const hp = a.hp, *const sg0 = a.seg[0], *const sg1 = a.seg[1], *const sg2 = a.seg[2];
+    const int ldp = a.ldp, ld0 = a.seg_ld[0], ld1 = a.seg_ld[1], ld2 = a.seg_ld[2];
+    auto issueA = [&](int s) {
+        if (!rawer) return;
+        const float *p;
+        if (s < nsh) {  // uniform branch
+            p = hp + ((size_t)rrc * ldp + s * kFK + rk);
+        } else {  // per-lane segment select, branch-free
+            const int kx = (s - nsh) * kFK + rk;
+            const float *q0 = sg0 + ((size_t)rrc * ld0 + (kx < w0 ? kx : 0));
+            const float *q1 = sg1 + ((size_t)rrc * ld1 + (kx - w0));
+            const float *q2 = sg2 + ((size_t)rrc * ld2 + (kx - w01));
+            p = (kx >= w01 && kx < kx_end) ? q2 : ((kx >= w0 && kx < w01) ? q1 : q0);
         }
-        if (p) ra = *reinterpret_cast<const float4 *>(p);
+        glds16_async(p, reinterpret_cast<char *>(Raw[s % 3]) + 1024 * (wv & (RAWW - 1)));
     };
-    auto storeA = [&](int buf) {
-        if (!stager) return;
-        const Split4 sp = split4(ra);
-        const int off = arow * 32 + 16 * ((akq >> 3) ^ ((arow >> 3) & 1)) + 8 * ((akq >> 2) & 1);
+    // split: thread -> row t >> 3, k pair 2 (t & 7) of the raw slab into the three bf16 planes
+    // (32-byte rows, chunk slot h ^ ((row >> 3) & 1))
+    const int arow = t >> 3, ak = (t & 7) * 2;
+    const bool arow_ok = row0 + arow < a.R;
+    const int aoff = arow * 32 + 16 * ((ak >> 3) ^ ((arow >> 3) & 1)) + 2 * (ak & 7);
+    auto splitA = [&](int s) {
+        float2 v = *reinterpret_cast<const float2 *>(&Raw[s % 3][arow * kFK + ak]);
+        if (!arow_ok || (s >= nsh && (s - nsh) * kFK + ak >= kx_end)) v = make_float2(0.f, 0.f);
+        const Split2 sp = split2(v);
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-            *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(As[buf][q]) + off) = sp.p[q];
+            *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(As[s & 1][q]) + aoff) = sp.p[q];
     };
-    auto issueB = [&](int s, int buf) {
+    // B chunk idx = i * T + t of [plane][gate][k row][16 slots]: plane / gate are wave-uniform,
+    // the per-lane part (k row, swizzled slot) is one 32-bit offset
+    const unsigned boff = 2u * (((t >> 4) & 15) * BW + 8 * ((t & 15) ^ ((((t >> 4) & 3) << 2) | ((t >> 6) & 3))));
+    auto issueB = [&](int s) {
         const bool hid = s < nsh;
         const __bf16 *W = hid ? a.whp : a.wip;
         const int krows = hid ? H : a.kxp;
         const int kb = hid ? s * kFK : (s - nsh) * kFK;
 #pragma unroll
         for (int i = 0; i < BN; ++i) {
-            const int idx = i * T + t;  // chunk slot of [plane][gate][k row][16 slots]
-            if (idx < BCH) {
-                const int slot = idx & 15, r = (idx >> 4) & 15, pg = idx >> 8;  // pg = plane * 3 + gate
+            if (i * T + 64 * wv < BCH) {  // whole waves (BCH % 64 == 0)
+                const int pg = i * (T / 256) + (wv >> 2);  // plane * 3 + gate
                 const int q = pg / 3, g = pg - 3 * q;
-                const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
-                glds16_async(W + ((size_t)q * krows + kb + r) * BW + g * H + 8 * ch,
-                             reinterpret_cast<char *>(Bs[buf]) + 16 * (i * T + 64 * w));
+                glds16_async_s(W + ((size_t)q * krows + kb) * BW + g * H, boff,
+                               reinterpret_cast<char *>(Bs[s & 1]) + 16 * (i * T + 64 * wv));
             }
         }
     };
@@ -503,7 +539,8 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[i][g] = f32x16{};
     const int li = lane & 31, lk = lane >> 5, gl = (lane >> 4) & 1;
-    auto slab = [&](int buf, bool hid) {
+    auto slab = [&](int buf, auto hidc) {
+        constexpr bool hid = decltype(hidc)::value;
         bf16x8 fa[RT][3];
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
@@ -519,7 +556,8 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
             bf16x8 fb[3];
 #pragma unroll
             for (int q = 0; q < 3; ++q) fb[q] = tr_frag(Bs[buf] + (q * 3 + g) * BPL, 8 * lk, (32 * wu + 16 * gl) >> 3, lane);
-            const int ai = g < 2 ? g : (hid ? 3 : 2);
+            constexpr int ai3 = hid ? 3 : 2;
+            const int ai = g < 2 ? g : ai3;
 #pragma unroll
             for (int i = 0; i < RT; ++i) {
                 f32x16 c = acc[i][ai];
@@ -534,26 +572,32 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
         }
     };
 
-    issueB(0, 0);
-    loadA(0);
-    storeA(0);
+    // prologue: weights of slab 0, raw activations of slabs 0..2 (ns >= 9 > 3)
+    issueB(0);
+    issueA(0);
+    issueA(1);
+    issueA(2);
     wait_vmcnt<0>();
     barrier_lds();
-    int buf = 0;
-#pragma unroll 1
-    for (int s = 0; s < ns; ++s) {
-        const bool more = s + 1 < ns;
-        if (more) {
-            issueB(s + 1, buf ^ 1);
-            loadA(s + 1);
+    splitA(0);
+    barrier_lds();
+    auto step = [&](int s, auto hidc) {
+        if (s + 1 < ns) {
+            issueB(s + 1);
+            if (s + 3 < ns) issueA(s + 3);
         }
-        slab(buf, s < nsh);
+        slab(s & 1, hidc);
         __builtin_amdgcn_sched_barrier(0);
-        if (more) storeA(buf ^ 1);
-        wait_vmcnt<0>();
+        if (s + 1 < ns) splitA(s + 1);
+        // all but this wave's youngest DMA (slab s + 3's activations, raw waves only)
+        if (rawer && s + 3 < ns) wait_vmcnt<1>();
+        else wait_vmcnt<0>();
         barrier_lds();
-        buf ^= 1;
-    }
+    };
+#pragma unroll 1
+    for (int s = 0; s < nsh; ++s) step(s, std::true_type{});
+#pragma unroll 1
+    for (int s = nsh; s < ns; ++s) step(s, std::false_type{});
     gru_ln_epilogue<NW, RS, kXR>(a, acc, reinterpret_cast<float *>(&As[0][0][0]), row0, wu, wrow, li, lk);
 }
 

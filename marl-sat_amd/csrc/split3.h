@@ -61,6 +61,30 @@ __device__ __forceinline__ Split4 split4(const float4 &u) {
     return s;
 }
 
+struct Split2 {
+    uint32_t p[3];
+};
+
+__device__ __forceinline__ Split2 split2(const float2 &u) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const float x[2] = {u.x, u.y};
+    bf16x2 h, m, l;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const __bf16 a = (__bf16)x[j];
+        const float r = x[j] - (float)a;
+        const __bf16 b = (__bf16)r;
+        h[j] = a;
+        m[j] = b;
+        l[j] = (__bf16)(r - (float)b);
+    }
+    Split2 s;
+    s.p[0] = __builtin_bit_cast(uint32_t, h);
+    s.p[1] = __builtin_bit_cast(uint32_t, m);
+    s.p[2] = __builtin_bit_cast(uint32_t, l);
+    return s;
+}
+
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int w3off(int row, int ch) {  // byte offset of 16-byte chunk ch of row
