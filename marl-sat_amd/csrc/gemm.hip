@@ -359,10 +359,15 @@ static bool skinny_ok(const float *G, int ldg, const float *W, int ldw, int K, i
            (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0;
 }
 
-// at most 512 workgroups (2 per CU), >= ~1024 rows per split
+// at most 768 workgroups (3 per CU: the x3 weight gradient's occupancy), >= ~1024 rows per split;
+// MARLSAT_WGRAD_WG overrides the workgroup budget (A/B measurements)
 static int wgrad_splits(int M, int K, int N) {
+    static const int budget = [] {
+        const char *e = getenv("MARLSAT_WGRAD_WG");
+        return e ? std::max(1, atoi(e)) : 768;
+    }();
     const int tiles = ((K + kTM - 1) / kTM) * ((N + kTN - 1) / kTN);
-    return std::max(1, std::min(512 / std::max(tiles, 1), (M + 1023) / 1024));
+    return std::max(1, std::min(budget / std::max(tiles, 1), (M + 1023) / 1024));
 }
 
 }  // namespace msat

@@ -235,32 +235,47 @@ wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ 
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16v{};
     const int rb = sp * rows_per_split, re = min(M, rb + rows_per_split);
     const int ns = (re - rb + 15) / 16;
-    // staging: thread t -> row t >> 4 of the slab, columns 4 (t & 15) and 4 (t & 15) + 64
+    // staging: thread t -> row t >> 4 of the slab, columns 4 (t & 15) and 4 (t & 15) + 64.
+    // Loads run two slabs ahead in registers (sets R0 / R1 by slab parity) and are always issued
+    // (clamped row / columns; out-of-range values are zeroed when stored, after they landed), so
+    // hipcc's counted wait before a store leaves the next set's loads in flight.
     const int srow = t >> 4, sc = (t & 15) * 4;
-    float4 ra[2], rg[2];
-    auto load = [&](int s) {
+    struct Stage {
+        float4 a[2], g[2];
+    };
+    bool kok[2], nok[2];
+    const float *pa[2];
+    const float *pg[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int kc = k0 + sc + 64 * u, nc = n0 + sc + 64 * u;
+        kok[u] = kc < K;
+        nok[u] = nc < N;
+        pa[u] = A + (kok[u] ? kc : 0);
+        pg[u] = G + (nok[u] ? nc : 0);
+    }
+    auto load = [&](int s, Stage &r) {
         const int m = rb + s * 16 + srow;
+        const size_t mc = m < re ? m : re - 1;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int kc = k0 + sc + 64 * u, nc = n0 + sc + 64 * u;
-            ra[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            rg[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (m < re) {
-                if (kc < K) ra[u] = *reinterpret_cast<const float4 *>(A + (size_t)m * lda + kc);
-                if (nc < N) rg[u] = *reinterpret_cast<const float4 *>(G + (size_t)m * ldg + nc);
-            }
+            r.a[u] = *reinterpret_cast<const float4 *>(pa[u] + mc * lda);
+            r.g[u] = *reinterpret_cast<const float4 *>(pg[u] + mc * ldg);
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int s, Stage r, int buf) {
+        const bool mok = rb + s * 16 + srow < re;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
+            if (!(mok && kok[u])) r.a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!(mok && nok[u])) r.g[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             const int col = sc + 64 * u;
             const int off = w3off(srow, col >> 3) + 8 * ((col >> 2) & 1);
-            const Split4 pa = split4(ra[u]), pg = split4(rg[u]);
+            const Split4 xa = split4(r.a[u]), xg = split4(r.g[u]);
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
-                *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(lds[buf][q]) + off) = pa.p[q];
-                *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(lds[buf][3 + q]) + off) = pg.p[q];
+                *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(lds[buf][q]) + off) = xa.p[q];
+                *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(lds[buf][3 + q]) + off) = xg.p[q];
             }
         }
     };
@@ -289,18 +304,29 @@ wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ 
             }
     };
     if (ns > 0) {
-        load(0);
-        store(0);
+        Stage R0, R1;
+        load(0, R0);
+        load(1 < ns ? 1 : 0, R1);
+        store(0, R0, 0);
         __syncthreads();
-    }
-    for (int s = 0; s < ns; ++s) {
-        const int buf = s & 1;
-        const bool more = s + 1 < ns;
-        if (more) load(s + 1);
-        slab(buf);
-        __builtin_amdgcn_sched_barrier(0);
-        if (more) store(buf ^ 1);
-        __syncthreads();
+        // Rn holds slab s + 1, Rf receives slab s + 2 (past the end: a repeated, never stored load)
+        auto iter = [&](int s, const Stage &Rn, Stage &Rf) {
+            const int buf = s & 1;
+            load(s + 2 < ns ? s + 2 : ns - 1, Rf);
+            __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs
+            slab(buf);
+            __builtin_amdgcn_sched_barrier(0);
+            // unconditional (past the end it fills the unused buffer): a store in its own basic
+            // block lets hipcc sink the slab s + 2 loads into it, right before their use
+            store(s + 1, Rn, buf ^ 1);
+            __syncthreads();
+        };
+        int s = 0;
+        for (; s + 1 < ns; s += 2) {
+            iter(s, R1, R0);
+            iter(s + 1, R0, R1);
+        }
+        if (s < ns) iter(s, R1, R0);
     }
     float *P = part + (size_t)sp * K * N;
 #pragma unroll
