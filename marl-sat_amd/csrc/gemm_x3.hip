@@ -76,7 +76,9 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
 #pragma unroll
     for (int j = 0; j < SR; ++j) arow[j] = A + (size_t)min(m0 + srow + 128 * j, M - 1) * lda + 8 * shalf;
     const size_t NK = (size_t)N * K;
-    const __bf16 *wrow = Wp + (size_t)min(n0 + srow, N - 1) * K + 8 * shalf;
+    // LDS images: row r's 16-byte k-halves h at uint4 2 r + (h ^ ((r >> 3) & 1)) -- the XOR makes the
+    // ds_read_b128 fragment reads (32-byte row stride) conflict-free in every 16-lane group
+    const __bf16 *wrow = Wp + (size_t)min(n0 + srow, N - 1) * K + 8 * (shalf ^ ((srow >> 3) & 1));
     f32x16v acc[TI][2];
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -101,7 +103,7 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
         for (int j = 0; j < SR; ++j) {
             const Split8 sp = split8(r[j][0], r[j][1]);
 #pragma unroll
-            for (int q = 0; q < 3; ++q) lds_a[buf][q][t + 256 * j] = sp.p[q];
+            for (int q = 0; q < 3; ++q) lds_a[buf][q][2 * (srow + 128 * j) + (shalf ^ ((srow >> 3) & 1))] = sp.p[q];
         }
     };
     auto issueW = [&](int s, int buf) {
@@ -115,10 +117,10 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
         for (int q = 0; q < 3; ++q) {
 #pragma unroll
             for (int i = 0; i < TI; ++i)
-                fa[i][q] = __builtin_bit_cast(bf16x8, lds_a[buf][q][(wr + 32 * i + li) * 2 + h]);
+                fa[i][q] = __builtin_bit_cast(bf16x8, lds_a[buf][q][(wr + 32 * i + li) * 2 + (h ^ ((li >> 3) & 1))]);
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                fb[j][q] = __builtin_bit_cast(bf16x8, lds_w[buf][q][(wc + 32 * j + li) * 2 + h]);
+                fb[j][q] = __builtin_bit_cast(bf16x8, lds_w[buf][q][(wc + 32 * j + li) * 2 + (h ^ ((li >> 3) & 1))]);
         }
 #pragma unroll
         for (int i = 0; i < TI; ++i)
