@@ -430,6 +430,74 @@ __global__ void transpose_pad_kernel(const float *__restrict__ W, int K, int N, 
     }
 }
 
+// Fast gate nonlinearities for the x3 epilogue: v_exp + v_rcp (<= 2 ulp each), no IEEE division.
+__device__ __forceinline__ float fsig_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float ftanh_fast(float x) {  // 2 sigma(2x) - 1, saturates cleanly at +-1
+    return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
+}
+
+// x3 epilogue (128-row tile, 16 waves, wave = 32 rows x 32 units of all four gates): the gate
+// algebra per accumulator, h' staged to LDS as [row][unit] (row stride 132 floats: conflict-free
+// for both the column writes and the row reads), then one row per 8 threads: 16 units each,
+// LayerNorm sums over 8 lanes, float4 output rows.  hv = h of each accumulator's (row, unit).
+template <int NW>
+__device__ __forceinline__ void gru_ln_epilogue_x3(const GruFwdArgs &a, f32x16 (&acc)[1][4], const float (&hv)[16],
+                                                   float *stage, int row0, int wu, int wrow, int li, int lk, int t) {
+    constexpr int H = 32 * NW, HP = H + 4;
+    const int u = 32 * wu + li;
+    const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
+    const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int lr = wrow + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
+        const int row = row0 + lr;
+        const float rp = acc[0][0][reg] + br, zp = acc[0][1][reg] + bz;
+        const float gi = acc[0][2][reg] + bni, gh = acc[0][3][reg] + bnh;
+        if (a.g4 && row < a.R) {
+            float *q = a.g4 + (size_t)row * a.ldg + u;
+            q[0] = rp;
+            q[H] = zp;
+            q[2 * H] = gi;
+            q[3 * H] = gh;
+        }
+        const float rg = fsig_fast(rp), zg = fsig_fast(zp);
+        const float ng = ftanh_fast(gi + rg * gh);
+        stage[lr * HP + u] = (1.0f - zg) * ng + zg * hv[reg];
+    }
+    __syncthreads();
+    const int r = t >> 3, c0 = (t & 7) * (H / 8);
+    float4 v[H / 32];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < H / 32; ++j) {
+        v[j] = *reinterpret_cast<const float4 *>(stage + r * HP + c0 + 4 * j);
+        s1 += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+        s2 += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+        s1 += __shfl_xor(s1, o, 8);
+        s2 += __shfl_xor(s2, o, 8);
+    }
+    const float mean = s1 / (float)H;
+    const float var = fmaxf(s2 / (float)H - mean * mean, 0.0f);
+    const float rs = rsqrtf(var + 1e-6f);
+    const int row = row0 + r;
+    if (row < a.R) {
+#pragma unroll
+        for (int j = 0; j < H / 32; ++j) {
+            const float4 sc = *reinterpret_cast<const float4 *>(a.ln_scale + c0 + 4 * j);
+            const float4 lb = *reinterpret_cast<const float4 *>(a.ln_bias + c0 + 4 * j);
+            float4 o;
+            o.x = (v[j].x - mean) * (rs * sc.x) + lb.x;
+            o.y = (v[j].y - mean) * (rs * sc.y) + lb.y;
+            o.z = (v[j].z - mean) * (rs * sc.z) + lb.z;
+            o.w = (v[j].w - mean) * (rs * sc.w) + lb.w;
+            *reinterpret_cast<float4 *>(a.out + (size_t)row * a.ldo + c0 + 4 * j) = o;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // bf16x3 form (msat_gru_ln_fused_fwd_x3, H = 128): the same cell on the bf16 matrix cores with the
 // exact three-way operand split of gemm_x3.hip (six bf16 MFMAs per 16-deep k step, fp32-accurate).
@@ -597,8 +665,17 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
 #pragma unroll 1
     for (int s = 0; s < nsh; ++s) step(s, std::true_type{});
 #pragma unroll 1
-    for (int s = nsh; s < ns; ++s) step(s, std::false_type{});
-    gru_ln_epilogue<NW, RS, kXR>(a, acc, reinterpret_cast<float *>(&As[0][0][0]), row0, wu, wrow, li, lk);
+    for (int s = nsh; s < ns - 1; ++s) step(s, std::false_type{});
+    // last slab: nothing left to fetch; the epilogue's h values load under its MFMAs
+    float hv[16];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int row = row0 + wrow + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
+        hv[reg] = hp[(size_t)(row < a.R ? row : a.R - 1) * ldp + 32 * wu + li];
+    }
+    slab((ns - 1) & 1, std::false_type{});
+    barrier_lds();  // every wave is done with the slab buffers before the epilogue reuses them
+    gru_ln_epilogue_x3<NW>(a, acc, hv, reinterpret_cast<float *>(&Bs[0][0]), row0, wu, wrow, li, lk, t);
 }
 
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -753,6 +830,8 @@ extern "C" int msat_gru_ln_fused_fwd_x3(const float *x0, int32_t ld0, int32_t w0
     MSAT_REQUIRE(kxp % kFK == 0 && kxp >= Kx, "gru_ln_fused_fwd_x3: kxp must be >= Kx and a multiple of 16");
     MSAT_REQUIRE(aligned16(hprev) && ldp % 4 == 0 && aligned16(wi_planes) && aligned16(wh_planes),
                  "gru_ln_fused_fwd_x3: hprev / weight planes must be 16-byte aligned");
+    MSAT_REQUIRE(aligned16(out) && ldo % 4 == 0 && aligned16(ln_scale) && aligned16(ln_bias),
+                 "gru_ln_fused_fwd_x3: out (ld %% 4 == 0) and the LayerNorm rows must be 16-byte aligned");
     GruFwdArgs a = {};
     for (int g = 0; g < 3; ++g) {
         a.seg[g] = ws[g] ? seg[g] : nullptr;
