@@ -26,6 +26,13 @@ namespace msat {
 
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 
+// diagnostic ablations of gemm_x3_kernel (timing only, wrong results; never set in the product
+// build): bit 0 no weight DMA after slab 0, 1 no activation loads after the prologue, 2 no split
+// store after the prologue, 3 no MFMAs
+#ifndef MSAT_GEMM_ABL
+#define MSAT_GEMM_ABL 0
+#endif
+
 constexpr int kX3T = 256;
 constexpr int kX3M = 128;  // tile rows / cols
 constexpr int kX3D = 16;   // slab depth (one bf16 MFMA k step)
@@ -148,11 +155,11 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
     auto iter = [&](int s, float4 (&Rn)[SR][2], float4 (&Rf)[SR][2]) {
         const int buf = s & 1;
         const bool more = s + 1 < ns;
-        if (more) issueW(s + 1, buf ^ 1);
-        if (s >= 1 && s + 2 < ns) loadA(s + 2, Rf);  // s = 0: A(2) was issued in the prologue
-        slab(buf);
+        if (!(MSAT_GEMM_ABL & 1) && more) issueW(s + 1, buf ^ 1);
+        if (!(MSAT_GEMM_ABL & 2) && s >= 1 && s + 2 < ns) loadA(s + 2, Rf);  // s = 0: A(2) was issued in the prologue
+        if (!(MSAT_GEMM_ABL & 8)) slab(buf);
         __builtin_amdgcn_sched_barrier(0);
-        if (more) storeA(Rn, buf ^ 1);
+        if (!(MSAT_GEMM_ABL & 4) && more) storeA(Rn, buf ^ 1);
         // W(s+1) and A(s+1) landed; A(s+2) (issued after W(s+1) for s >= 1) may fly.  At s = 0,
         // A(2) precedes W(1) in issue order, so the wait drains everything.
         if (s >= 1 && s + 2 < ns) wait_vmcnt<NL>();

@@ -508,6 +508,12 @@ __device__ __forceinline__ void gru_ln_epilogue_x3(const GruFwdArgs &a, f32x16 (
 //   [plane][gate][16 k][128 cols] images (256-byte rows, w3off swizzle applied on the source
 //   side), read as 8-row column fragments with ds_read_b64_tr_b16.
 constexpr int kXR = 128;  // rows per workgroup (x3 kernel)
+// diagnostic ablations of the x3 kernel's pipeline (timing only, wrong results; never set in the
+// product build): bit 0 no weight DMA after slab 0, 1 no activation DMA after the prologue,
+// 2 no split after the prologue, 3 no MFMAs, 4 no epilogue
+#ifndef MSAT_GRU_ABL
+#define MSAT_GRU_ABL 0
+#endif
 
 // 16 waves x 32 rows (RS = 4, RT = 1).
 //
@@ -651,12 +657,12 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
     barrier_lds();
     auto step = [&](int s, auto hidc) {
         if (s + 1 < ns) {
-            issueB(s + 1);
-            if (s + 3 < ns) issueA(s + 3);
+            if (!(MSAT_GRU_ABL & 1)) issueB(s + 1);
+            if (!(MSAT_GRU_ABL & 2) && s + 3 < ns) issueA(s + 3);
         }
-        slab(s & 1, hidc);
+        if (!(MSAT_GRU_ABL & 8)) slab(s & 1, hidc);
         __builtin_amdgcn_sched_barrier(0);
-        if (s + 1 < ns) splitA(s + 1);
+        if (!(MSAT_GRU_ABL & 4) && s + 1 < ns) splitA(s + 1);
         // all but this wave's youngest DMA (slab s + 3's activations, raw waves only)
         if (rawer && s + 3 < ns) wait_vmcnt<1>();
         else wait_vmcnt<0>();
@@ -673,8 +679,12 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
         const int row = row0 + wrow + (reg & 3) + 8 * (reg >> 2) + 4 * lk;
         hv[reg] = hp[(size_t)(row < a.R ? row : a.R - 1) * ldp + 32 * wu + li];
     }
-    slab((ns - 1) & 1, std::false_type{});
+    if (!(MSAT_GRU_ABL & 8)) slab((ns - 1) & 1, std::false_type{});
     barrier_lds();  // every wave is done with the slab buffers before the epilogue reuses them
+    if (MSAT_GRU_ABL & 16) {  // keep the accumulators live, store one value per lane
+        if (row0 + wrow + li < a.R) a.out[(size_t)(row0 + wrow + li) * a.ldo + 32 * wu + lk] = acc[0][0][0] + acc[0][1][1] + acc[0][2][2] + acc[0][3][3] + hv[0];
+        return;
+    }
     gru_ln_epilogue_x3<NW>(a, acc, hv, reinterpret_cast<float *>(&Bs[0][0]), row0, wu, wrow, li, lk, t);
 }
 
