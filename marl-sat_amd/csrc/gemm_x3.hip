@@ -25,6 +25,7 @@
 namespace msat {
 
 typedef float f32x16v __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // diagnostic ablations of gemm_x3_kernel (timing only, wrong results; never set in the product
 // build): bit 0 no weight DMA after slab 0, 1 no activation loads after the prologue, 2 no split
@@ -223,6 +224,336 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Register-A form of the same product (K % 32 == 0).  Each wave owns 32 TI rows x all 128 columns
+// of the workgroup tile, so no other wave needs its activation rows: they go global -> registers
+// -> split -> MFMA operands and never touch LDS.  For the 32x32x16 MFMA lane (r, h) holds
+// A[r][8h + j] of a 16-deep step, i.e. 32 contiguous bytes per lane: two float4 loads per row
+// tile and step, straight from the row.  Only the weight planes, shared by the four waves, are
+// staged: 32-deep double slabs by LDS-DMA into [plane][128 rows][4 chunks of 8 k] images (64-B
+// rows, chunk XOR (row >> 2) & 3: conflict-free ds_read_b128 fragments), one barrier per 32 k.
+// The MFMA sequence per (row tile, column tile, k step) is the register-staged kernel's, so the
+// results are bitwise those of gemm_x3_kernel.
+template <int TI, int PF>
+__global__ void __launch_bounds__(kX3T, TI == 1 && PF == 1 ? 3 : 2)
+gemm_x3r_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ Wp, float *__restrict__ C, int ldc,
+                const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
+    constexpr int MT = 128 * TI;       // tile rows (4 waves x 32 TI)
+    constexpr int WPL = kX3M * 4;      // uint4 per weight plane image: 128 rows x 4 chunks = 8 KiB
+    __shared__ uint4 lds_w[2][3][WPL];  // 48 KiB
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    const int m0 = (id / ntn) * MT, n0 = (id % ntn) * kX3M;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63, li = lane & 31, h = lane >> 5;
+    const int wr = w * 32 * TI;
+    const float *arow[TI];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) arow[i] = A + (size_t)min(m0 + wr + 32 * i + li, M - 1) * lda + 8 * h;
+    // weight DMA: 24 wave-instructions (1 KiB = 16 rows x 4 chunks each) per double slab, 6 per wave.
+    // Instruction e of wave w fills plane q = (6w + e) / 8, rows 16 p .. 16 p + 15 (p = (6w + e) % 8);
+    // lane -> row 16 p + (lane >> 2), LDS chunk lane & 3 holding source chunk (lane & 3) ^ ((row >> 2) & 3).
+    // weight DMA: 24 wave-instructions (1 KiB = 16 rows x 4 chunks each) per double slab, 6 per wave.
+    // Instruction e of wave w fills plane q = (6w + e) / 8, rows 16 p .. 16 p + 15 (p = (6w + e) % 8);
+    // lane -> row 16 p + (lane >> 2), LDS chunk lane & 3 holding source chunk (lane & 3) ^ ((row >> 2) & 3).
+    unsigned voff[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+        const int x = 6 * w + e, q = x >> 3, p = x & 7, row = 16 * p + (lane >> 2);
+        const int ch = (lane & 3) ^ ((row >> 2) & 3);
+        voff[e] = (unsigned)(((size_t)q * N * K + (size_t)min(n0 + row, N - 1) * K + 8 * ch) * 2);
+    }
+    auto issueW = [&](int d, int buf) {
+        const char *base = reinterpret_cast<const char *>(Wp) + (size_t)d * 64;
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+            const int x = 6 * w + e;
+            glds16_async_s(base, voff[e], &lds_w[buf][x >> 3][64 * (x & 7)]);
+        }
+    };
+    f32x16v acc[TI][4];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x16v{};
+    // raw A of one double slab per register set: [tile][2 step + half]; PF sets, A(d) in set d % PF
+    float4 ra[PF][TI][4];
+    auto loadA = [&](int d, float4 (&r)[TI][4]) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                r[i][e] = *reinterpret_cast<const float4 *>(arow[i] + 32 * d + 16 * (e >> 1) + 4 * (e & 1));
+    };
+    const int sw = (li >> 2) & 3;
+    const int nd = K / 32;
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        if (p < nd) loadA(p, ra[p]);
+    issueW(0, 0);
+    wait_vmcnt<0>();
+    barrier_lds();
+    // per double slab d: split A(d), issue W(d+1) and A(d+PF) (into A(d)'s set), MFMAs of d, wait
+    // for W(d+1) (vector-memory counts retire in issue order, so A(d+PF) may still fly), barrier
+    auto iter = [&](int d, float4 (&r)[TI][4]) {
+        const int buf = d & 1;
+        bf16x8 fa[TI][2][3];
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const Split8 sp = split8(r[i][2 * u], r[i][2 * u + 1]);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) fa[i][u][q] = __builtin_bit_cast(bf16x8, sp.p[q]);
+            }
+        __builtin_amdgcn_sched_barrier(0);
+        const bool more = d + 1 < nd, fill = d + PF < nd;
+        if (!(MSAT_GEMM_ABL & 1) && more) issueW(d + 1, buf ^ 1);
+        if (!(MSAT_GEMM_ABL & 2) && fill) loadA(d + PF, r);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(MSAT_GEMM_ABL & 8)) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bf16x8 fb[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        fb[q] = __builtin_bit_cast(bf16x8, lds_w[buf][q][(32 * j + li) * 4 + ((2 * u + h) ^ sw)]);
+#pragma unroll
+                    for (int i = 0; i < TI; ++i) {
+                        f32x16v c = acc[i][j];
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][2], fb[0], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][1], fb[1], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][0], fb[2], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][1], fb[0], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][0], fb[1], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][0], fb[0], c, 0, 0, 0);
+                        acc[i][j] = c;
+                    }
+                }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (fill && !(MSAT_GEMM_ABL & 2)) wait_vmcnt<4 * TI>();
+        else wait_vmcnt<0>();
+        barrier_lds();
+    };
+    if constexpr (PF == 1) {
+        for (int d = 0; d < nd; ++d) iter(d, ra[0]);
+    } else {
+        int d = 0;
+        for (; d + 1 < nd; d += 2) {
+            iter(d, ra[0]);
+            iter(d + 1, ra[1]);
+        }
+        if (d < nd) iter(d, ra[0]);
+    }
+    float *ldsf = reinterpret_cast<float *>(&lds_w[0][0][0]);  // 48 KiB: four 8 KiB wave stages
+    if (vec_out) {
+        float *stage = ldsf + w * 32 * 64;
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int hc = 0; hc < 2; ++hc) {  // columns 64 hc .. 64 hc + 63 of the wave's 32 rows
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg)
+                        stage[((reg & 3) + 8 * (reg >> 2) + 4 * h) * 64 + 32 * jj + li] = acc[i][2 * hc + jj][reg];
+                __syncthreads();
+                const int col = n0 + 64 * hc + (lane & 15) * 4;
+                float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (bias && col < N) bv = *reinterpret_cast<const float4 *>(bias + col);
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int r = it * 4 + (lane >> 4);
+                    const int row = m0 + wr + 32 * i + r;
+                    float4 v = *reinterpret_cast<const float4 *>(stage + r * 64 + (lane & 15) * 4);
+                    v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+                    if (row < M && col < N) {
+                        float4 *c = reinterpret_cast<float4 *>(C + (size_t)row * ldc + col);
+                        if (accumulate) {
+                            const float4 o = *c;
+                            v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
+                        }
+                        *c = v;
+                    }
+                }
+                __syncthreads();
+            }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = n0 + 32 * j + li;
+            if (col >= N) continue;
+            const float bv = bias ? bias[col] : 0.0f;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = m0 + wr + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                if (row >= M) continue;
+                float *c = C + (size_t)row * ldc + col;
+                const float v = acc[i][j][reg] + bv;
+                *c = accumulate ? *c + v : v;
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The register-A kernel on v_mfma_f32_16x16x32_bf16: one MFMA k step covers the whole 32-deep
+// double slab (lane l holds A[l & 15][8 (l >> 4) + j], i.e. 32 contiguous bytes of its row), the
+// wave tile is 2 x 8 tiles of 16 x 16.  Same MFMA work and LDS reads as the 32x32x16 form; the
+// 16x16 loop holds a higher clock under load (MI355X_MICROARCH.md, DVFS item 7).  Weight chunk c of
+// row n sits at slot c ^ f((n >> 2) & 3), f = {0, 2, 3, 1}: conflict-free for this lane map.
+__device__ __forceinline__ int x3swz16(int b) { return (0x1E >> (2 * b)) & 3; }  // {0, 2, 3, 1}
+
+template <int PF>
+__global__ void __launch_bounds__(kX3T, PF == 1 ? 3 : 2)
+gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ Wp, float *__restrict__ C, int ldc,
+                  const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
+    constexpr int WPL = kX3M * 4;
+    __shared__ uint4 lds_w[2][3][WPL];  // 48 KiB
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    const int m0 = (id / ntn) * 128, n0 = (id % ntn) * kX3M;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63, l16 = lane & 15, g = lane >> 4;
+    const int wr = w * 32;
+    const float *arow[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) arow[i] = A + (size_t)min(m0 + wr + 16 * i + l16, M - 1) * lda + 8 * g;
+    unsigned voff[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+        const int x = 6 * w + e, q = x >> 3, p = x & 7, row = 16 * p + (lane >> 2);
+        const int ch = (lane & 3) ^ x3swz16((row >> 2) & 3);
+        voff[e] = (unsigned)(((size_t)q * N * K + (size_t)min(n0 + row, N - 1) * K + 8 * ch) * 2);
+    }
+    auto issueW = [&](int d, int buf) {
+        const char *base = reinterpret_cast<const char *>(Wp) + (size_t)d * 64;
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+            const int x = 6 * w + e;
+            glds16_async_s(base, voff[e], &lds_w[buf][x >> 3][64 * (x & 7)]);
+        }
+    };
+    f32x4 acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
+    float4 ra[PF][2][2];  // [set][row tile][half]
+    auto loadA = [&](int d, float4 (&r)[2][2]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) r[i][e] = *reinterpret_cast<const float4 *>(arow[i] + 32 * d + 4 * e);
+    };
+    const int slot = g ^ x3swz16((l16 >> 2) & 3);
+    const int nd = K / 32;
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        if (p < nd) loadA(p, ra[p]);
+    issueW(0, 0);
+    wait_vmcnt<0>();
+    barrier_lds();
+    auto iter = [&](int d, float4 (&r)[2][2]) {
+        const int buf = d & 1;
+        bf16x8 fa[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const Split8 sp = split8(r[i][0], r[i][1]);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) fa[i][q] = __builtin_bit_cast(bf16x8, sp.p[q]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bool more = d + 1 < nd, fill = d + PF < nd;
+        if (more) issueW(d + 1, buf ^ 1);
+        if (fill) loadA(d + PF, r);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            bf16x8 fb[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) fb[q] = __builtin_bit_cast(bf16x8, lds_w[buf][q][(16 * j + l16) * 4 + slot]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                f32x4 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[0], c, 0, 0, 0);
+                acc[i][j] = c;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (fill) wait_vmcnt<4>();
+        else wait_vmcnt<0>();
+        barrier_lds();
+    };
+    if constexpr (PF == 1) {
+        for (int d = 0; d < nd; ++d) iter(d, ra[0]);
+    } else {
+        int d = 0;
+        for (; d + 1 < nd; d += 2) {
+            iter(d, ra[0]);
+            iter(d + 1, ra[1]);
+        }
+        if (d < nd) iter(d, ra[0]);
+    }
+    // C/D map: col = lane & 15, row = 4 (lane >> 4) + reg
+    float *stage = reinterpret_cast<float *>(&lds_w[0][0][0]) + w * 32 * 64;
+    if (vec_out) {
+#pragma unroll
+        for (int hc = 0; hc < 2; ++hc) {  // columns 64 hc .. 64 hc + 63 of the wave's 32 rows
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg)
+                        stage[(16 * i + 4 * g + reg) * 64 + 16 * jj + l16] = acc[i][4 * hc + jj][reg];
+            __syncthreads();
+            const int col = n0 + 64 * hc + l16 * 4;
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (bias && col < N) bv = *reinterpret_cast<const float4 *>(bias + col);
+#pragma unroll
+            for (int it = 0; it < 8; ++it) {
+                const int rr = it * 4 + g;
+                const int row = m0 + wr + rr;
+                float4 v = *reinterpret_cast<const float4 *>(stage + rr * 64 + l16 * 4);
+                v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+                if (row < M && col < N) {
+                    float4 *c = reinterpret_cast<float4 *>(C + (size_t)row * ldc + col);
+                    if (accumulate) {
+                        const float4 o = *c;
+                        v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
+                    }
+                    *c = v;
+                }
+            }
+            __syncthreads();
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int col = n0 + 16 * j + l16;
+            if (col >= N) continue;
+            const float bv = bias ? bias[col] : 0.0f;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int row = m0 + wr + 16 * i + 4 * g + reg;
+                if (row >= M) continue;
+                float *c = C + (size_t)row * ldc + col;
+                const float v = acc[i][j][reg] + bv;
+                *c = accumulate ? *c + v : v;
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Weight gradient on the same split: part[s][k][n] = sum_{m in split s} A[m][k] G[m][n].
 // The MFMA reduction runs over the rows m, so both fragments are 8-row column strips.  Both
 // operands are staged row-major as three bf16 planes [16 rows][128 cols] (256-byte rows, chunks
@@ -385,6 +716,19 @@ extern "C" int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, fl
     const int vec = (N % 4 == 0 && ldc % 4 == 0 && a16x3(C) && (!bias || a16x3(bias))) ? 1 : 0;
     const char *e = getenv("MARLSAT_GEMM_X3_TI");  // 32-row tiles per wave: 2 (128-row tile) or 4 (256)
     const __bf16 *Wb = reinterpret_cast<const __bf16 *>(Wplanes);
+    // register-A kernels (K % 32 == 0): 16 = 16x16x32 MFMA (default), 1 = 32x32x16, 0 = off
+    const char *r = getenv("MARLSAT_GEMM_X3_R");
+    const int rv = r ? atoi(r) : 16;
+    if ((rv == 1 || rv == 16) && K % 32 == 0) {
+        const int ntm = (M + 127) / 128;
+        if (rv == 16)
+            hipLaunchKernelGGL((gemm_x3r16_kernel<1>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
+                               Wb, C, ldc, bias, M, N, K, accumulate, ntn, vec);
+        else
+            hipLaunchKernelGGL((gemm_x3r_kernel<1, 1>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
+                               Wb, C, ldc, bias, M, N, K, accumulate, ntn, vec);
+        return check_launch("gemm_x3r_kernel");
+    }
     if (e && atoi(e) == 4) {
         const int ntm = (M + 255) / 256;
         hipLaunchKernelGGL((gemm_x3_kernel<4>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda, Wb, C,

@@ -176,7 +176,7 @@ def test_colsum_deterministic(M, N, ld, off):
     assert torch.equal(res[0][:oo], out0[:oo]) and torch.equal(res[0][oo + N:], out0[oo + N:])
 
 
-@pytest.mark.parametrize("ti", ["2", "4"])  # 128- / 256-row workgroup tiles
+@pytest.mark.parametrize("ti", ["2", "4", "r1", "r16"])  # 128- / 256-row tiles; register-A kernels 32x32x16 / 16x16x32
 @pytest.mark.parametrize("M,N,K", [(1, 4, 16), (130, 132, 64), (1000, 384, 384), (5000, 128, 384), (257, 256, 128),
                                    (3, 7, 32)])
 def test_gemm_x3_fp32_accuracy(M, N, K, ti, monkeypatch):
@@ -184,7 +184,11 @@ def test_gemm_x3_fp32_accuracy(M, N, K, ti, monkeypatch):
     kernels: 2e-6 of sum |a b|), including values spanning many binades."""
     from marlsat import _lib
 
-    monkeypatch.setenv("MARLSAT_GEMM_X3_TI", ti)
+    if ti.startswith("r"):
+        monkeypatch.setenv("MARLSAT_GEMM_X3_R", ti[1:])
+    else:
+        monkeypatch.setenv("MARLSAT_GEMM_X3_R", "0")
+        monkeypatch.setenv("MARLSAT_GEMM_X3_TI", ti)
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     A = torch.randn(M, K, device="cuda", generator=g) * torch.exp2(torch.randint(-6, 7, (M, K), device="cuda",
                                                                                 generator=g).float())
@@ -204,3 +208,35 @@ def test_gemm_x3_fp32_accuracy(M, N, K, ti, monkeypatch):
         ref = A.double() @ W.double().t() + bias.double() + (C0.double() if acc else 0)
         absprod = A.double().abs() @ W.double().abs().t() + bias.double().abs() + (C0.double().abs() if acc else 0)
         _ref_close(C, ref, absprod)
+
+
+@pytest.mark.parametrize("M,N,K,lda", [(5000, 128, 384, 512), (1001, 256, 384, 384), (77, 100, 64, 68)])
+def test_gemm_x3_register_a_bitwise(M, N, K, lda, monkeypatch):
+    """The 32x32x16 register-A kernel issues the register-staged kernel's MFMA sequence per output
+    tile, so its results are bitwise equal (strided A rows, both accumulate modes); the 16x16x32
+    form meets the fp32 bound on the same strided operands."""
+    from marlsat import _lib
+
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    A = torch.randn(M, lda, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g)
+    C0 = torch.randn(M, N, device="cuda", generator=g)
+    planes = torch.empty(3 * N * K + 8, dtype=torch.int16, device="cuda")
+    s = _lib.stream_ptr()
+    _lib.check(_lib.lib.msat_split_bf16x3(W.data_ptr(), N, K, K, planes.data_ptr(), s), "split")
+    for acc in (0, 1):
+        out = []
+        for r in ("0", "1"):
+            monkeypatch.setenv("MARLSAT_GEMM_X3_R", r)
+            C = C0.clone()
+            _lib.check(_lib.lib.msat_gemm_x3(A.data_ptr(), lda, planes.data_ptr(), C.data_ptr(), N, None, M, N, K,
+                                             acc, s), "gemm_x3")
+            out.append(C)
+        assert all(torch.equal(out[0], o) for o in out[1:])
+        monkeypatch.setenv("MARLSAT_GEMM_X3_R", "16")  # 16x16x32 form: same bound, another summation order
+        C = C0.clone()
+        _lib.check(_lib.lib.msat_gemm_x3(A.data_ptr(), lda, planes.data_ptr(), C.data_ptr(), N, None, M, N, K, acc, s),
+                   "gemm_x3")
+        Ak = A[:, :K].double()
+        _ref_close(C, Ak @ W.double().t() + (C0.double() if acc else 0),
+                   Ak.abs() @ W.double().abs().t() + (C0.double().abs() if acc else 0))

@@ -111,17 +111,17 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
     return out
 
 
-@pytest.mark.parametrize("layout", ["plain", "t", "x3"])
-@pytest.mark.parametrize("R", [0, 1, 77, 1000, 70000])
-@pytest.mark.parametrize("H", [64, 128, 256])
+def _fwd_cases():
+    """(layout, H, R): the plain kernel at H 64 / 128 / 256, the transposed-weight kernel at H 64 /
+    128, the bf16x3 kernel at H 128; the 70,000-row case at the production width H = 128 only."""
+    widths = {"plain": (64, 128, 256), "t": (64, 128), "x3": (128,)}
+    return [(lay, H, R) for lay, hs in widths.items() for H in hs for R in (0, 1, 77, 1000, 70000)
+            if R != 70000 or H == 128]
+
+
+@pytest.mark.parametrize("layout,H,R", _fwd_cases())
 @pytest.mark.parametrize("kind", ["var", "clause", "var8", "clause4"])
 def test_fused_forward_matches_reference(R, H, kind, layout):
-    if R == 70000 and H != 128:
-        pytest.skip("large case at the production width only")
-    if layout == "t" and H == 256:
-        pytest.skip("transposed-weight kernel: H 64 / 128")
-    if layout == "x3" and H != 128:
-        pytest.skip("bf16x3 kernel: H 128")
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=R + H)
     g4 = torch.full((R, 4 * H), float("nan"), device="cuda")
     out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout)
