@@ -406,19 +406,19 @@ gemm_x3r_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__
 // row n sits at slot c ^ f((n >> 2) & 3), f = {0, 2, 3, 1}: conflict-free for this lane map.
 __device__ __forceinline__ int x3swz16(int b) { return (0x1E >> (2 * b)) & 3; }  // {0, 2, 3, 1}
 
-template <int PF>
-__global__ void __launch_bounds__(kX3T, PF == 1 ? 3 : 2)
+template <int RT>  // 16-row tiles per wave: the workgroup tile is 64 RT rows x 128 columns
+__global__ void __launch_bounds__(kX3T, RT == 2 ? 3 : 2)
 gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ Wp, float *__restrict__ C, int ldc,
                   const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
     constexpr int WPL = kX3M * 4;
     __shared__ uint4 lds_w[2][3][WPL];  // 48 KiB
     const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
-    const int m0 = (id / ntn) * 128, n0 = (id % ntn) * kX3M;
+    const int m0 = (id / ntn) * 64 * RT, n0 = (id % ntn) * kX3M;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63, l16 = lane & 15, g = lane >> 4;
-    const int wr = w * 32;
-    const float *arow[2];
+    const int wr = w * 16 * RT;
+    const float *arow[RT];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) arow[i] = A + (size_t)min(m0 + wr + 16 * i + l16, M - 1) * lda + 8 * g;
+    for (int i = 0; i < RT; ++i) arow[i] = A + (size_t)min(m0 + wr + 16 * i + l16, M - 1) * lda + 8 * g;
     unsigned voff[6];
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
@@ -434,109 +434,104 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
             glds16_async_s(base, voff[e], &lds_w[buf][x >> 3][64 * (x & 7)]);
         }
     };
-    f32x4 acc[2][8];
+    f32x4 acc[RT][8];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
-    float4 ra[PF][2][2];  // [set][row tile][half]
-    auto loadA = [&](int d, float4 (&r)[2][2]) {
+    float4 ra[RT][2];  // the next double slab's raw A: [row tile][half]
+    auto loadA = [&](int d) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < RT; ++i)
 #pragma unroll
-            for (int e = 0; e < 2; ++e) r[i][e] = *reinterpret_cast<const float4 *>(arow[i] + 32 * d + 4 * e);
+            for (int e = 0; e < 2; ++e) ra[i][e] = *reinterpret_cast<const float4 *>(arow[i] + 32 * d + 4 * e);
     };
     const int slot = g ^ x3swz16((l16 >> 2) & 3);
     const int nd = K / 32;
-#pragma unroll
-    for (int p = 0; p < PF; ++p)
-        if (p < nd) loadA(p, ra[p]);
+    loadA(0);
     issueW(0, 0);
     wait_vmcnt<0>();
     barrier_lds();
-    auto iter = [&](int d, float4 (&r)[2][2]) {
+    // per double slab d: split A(d), issue W(d+1) and A(d+1), MFMAs of d, wait for W(d+1) (vector-
+    // memory counts retire in issue order, so A(d+1) may still fly), barrier
+    for (int d = 0; d < nd; ++d) {
         const int buf = d & 1;
-        bf16x8 fa[2][3];
+        bf16x8 fa[RT][3];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const Split8 sp = split8(r[i][0], r[i][1]);
+        for (int i = 0; i < RT; ++i) {
+            const Split8 sp = split8(ra[i][0], ra[i][1]);
 #pragma unroll
             for (int q = 0; q < 3; ++q) fa[i][q] = __builtin_bit_cast(bf16x8, sp.p[q]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        const bool more = d + 1 < nd, fill = d + PF < nd;
-        if (more) issueW(d + 1, buf ^ 1);
-        if (fill) loadA(d + PF, r);
+        const bool more = d + 1 < nd;
+        if (!(MSAT_GEMM_ABL & 1) && more) issueW(d + 1, buf ^ 1);
+        if (!(MSAT_GEMM_ABL & 2) && more) loadA(d + 1);
         __builtin_amdgcn_sched_barrier(0);
+        if (!(MSAT_GEMM_ABL & 8)) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            bf16x8 fb[3];
+            for (int j = 0; j < 8; ++j) {
+                bf16x8 fb[3];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) fb[q] = __builtin_bit_cast(bf16x8, lds_w[buf][q][(16 * j + l16) * 4 + slot]);
+                for (int q = 0; q < 3; ++q)
+                    fb[q] = __builtin_bit_cast(bf16x8, lds_w[buf][q][(16 * j + l16) * 4 + slot]);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                f32x4 c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[2], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[0], c, 0, 0, 0);
-                acc[i][j] = c;
+                for (int i = 0; i < RT; ++i) {
+                    f32x4 c = acc[i][j];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[0], c, 0, 0, 0);
+                    acc[i][j] = c;
+                }
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (fill) wait_vmcnt<4>();
+        if (more && !(MSAT_GEMM_ABL & 2)) wait_vmcnt<2 * RT>();
         else wait_vmcnt<0>();
         barrier_lds();
-    };
-    if constexpr (PF == 1) {
-        for (int d = 0; d < nd; ++d) iter(d, ra[0]);
-    } else {
-        int d = 0;
-        for (; d + 1 < nd; d += 2) {
-            iter(d, ra[0]);
-            iter(d + 1, ra[1]);
-        }
-        if (d < nd) iter(d, ra[0]);
     }
     // C/D map: col = lane & 15, row = 4 (lane >> 4) + reg
     float *stage = reinterpret_cast<float *>(&lds_w[0][0][0]) + w * 32 * 64;
     if (vec_out) {
 #pragma unroll
-        for (int hc = 0; hc < 2; ++hc) {  // columns 64 hc .. 64 hc + 63 of the wave's 32 rows
+        for (int i0 = 0; i0 < RT; i0 += 2)  // 32 rows at a time
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int hc = 0; hc < 2; ++hc) {  // columns 64 hc .. 64 hc + 63
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj)
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int reg = 0; reg < 4; ++reg)
-                        stage[(16 * i + 4 * g + reg) * 64 + 16 * jj + l16] = acc[i][4 * hc + jj][reg];
-            __syncthreads();
-            const int col = n0 + 64 * hc + l16 * 4;
-            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (bias && col < N) bv = *reinterpret_cast<const float4 *>(bias + col);
+                    for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-            for (int it = 0; it < 8; ++it) {
-                const int rr = it * 4 + g;
-                const int row = m0 + wr + rr;
-                float4 v = *reinterpret_cast<const float4 *>(stage + rr * 64 + l16 * 4);
-                v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-                if (row < M && col < N) {
-                    float4 *c = reinterpret_cast<float4 *>(C + (size_t)row * ldc + col);
-                    if (accumulate) {
-                        const float4 o = *c;
-                        v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
+                        for (int reg = 0; reg < 4; ++reg)
+                            stage[(16 * i + 4 * g + reg) * 64 + 16 * jj + l16] = acc[i0 + i][4 * hc + jj][reg];
+                __syncthreads();
+                const int col = n0 + 64 * hc + l16 * 4;
+                float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (bias && col < N) bv = *reinterpret_cast<const float4 *>(bias + col);
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int rr = it * 4 + g;
+                    const int row = m0 + wr + 16 * i0 + rr;
+                    float4 v = *reinterpret_cast<const float4 *>(stage + rr * 64 + l16 * 4);
+                    v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+                    if (row < M && col < N) {
+                        float4 *c = reinterpret_cast<float4 *>(C + (size_t)row * ldc + col);
+                        if (accumulate) {
+                            const float4 o = *c;
+                            v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
+                        }
+                        *c = v;
                     }
-                    *c = v;
                 }
+                __syncthreads();
             }
-            __syncthreads();
-        }
         return;
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int col = n0 + 16 * j + l16;
@@ -716,13 +711,17 @@ extern "C" int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, fl
     const int vec = (N % 4 == 0 && ldc % 4 == 0 && a16x3(C) && (!bias || a16x3(bias))) ? 1 : 0;
     const char *e = getenv("MARLSAT_GEMM_X3_TI");  // 32-row tiles per wave: 2 (128-row tile) or 4 (256)
     const __bf16 *Wb = reinterpret_cast<const __bf16 *>(Wplanes);
-    // register-A kernels (K % 32 == 0): 16 = 16x16x32 MFMA (default), 1 = 32x32x16, 0 = off
+    // register-A kernels (K % 32 == 0): 16 = 16x16x32 MFMA, 128-row tiles (default); 32 = the same
+    // with 256-row tiles; 1 = 32x32x16; 0 = off
     const char *r = getenv("MARLSAT_GEMM_X3_R");
     const int rv = r ? atoi(r) : 16;
-    if ((rv == 1 || rv == 16) && K % 32 == 0) {
-        const int ntm = (M + 127) / 128;
+    if ((rv == 1 || rv == 16 || rv == 32) && K % 32 == 0) {
+        const int rows = rv == 32 ? 256 : 128, ntm = (M + rows - 1) / rows;
         if (rv == 16)
-            hipLaunchKernelGGL((gemm_x3r16_kernel<1>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
+            hipLaunchKernelGGL((gemm_x3r16_kernel<2>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
+                               Wb, C, ldc, bias, M, N, K, accumulate, ntn, vec);
+        else if (rv == 32)
+            hipLaunchKernelGGL((gemm_x3r16_kernel<4>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
                                Wb, C, ldc, bias, M, N, K, accumulate, ntn, vec);
         else
             hipLaunchKernelGGL((gemm_x3r_kernel<1, 1>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,

@@ -176,7 +176,7 @@ def test_colsum_deterministic(M, N, ld, off):
     assert torch.equal(res[0][:oo], out0[:oo]) and torch.equal(res[0][oo + N:], out0[oo + N:])
 
 
-@pytest.mark.parametrize("ti", ["2", "4", "r1", "r16"])  # 128- / 256-row tiles; register-A kernels 32x32x16 / 16x16x32
+@pytest.mark.parametrize("ti", ["2", "4", "r1", "r16", "r32"])  # 128- / 256-row tiles; register-A 32x32x16, 16x16x32 (128 / 256 rows)
 @pytest.mark.parametrize("M,N,K", [(1, 4, 16), (130, 132, 64), (1000, 384, 384), (5000, 128, 384), (257, 256, 128),
                                    (3, 7, 32)])
 def test_gemm_x3_fp32_accuracy(M, N, K, ti, monkeypatch):
