@@ -120,6 +120,17 @@ int msat_gru_ln_fused_fwd_x3(const float *x0, int32_t ld0, int32_t w0, const flo
                              const void *wi_planes, int32_t kxp, const float *bi, const void *wh_planes,
                              const float *bh, const float *ln_scale, const float *ln_bias, float *out, int32_t ldo,
                              float *g4, int32_t ldg, int32_t R, int32_t H, void *stream);
+/* Register-A form of msat_gru_ln_fused_fwd_x3 (16x16x32 bf16 MFMAs; activations read straight into
+ * registers, only the weights staged): weights given as msat_split_bf16x3_t planes of Wi^T zero-padded
+ * to kxp columns (kxp >= Kx, multiple of 32) and of Wh^T (kxp = H).  g4 rows 16-byte aligned. */
+int msat_gru_ln_fused_fwd_x3r(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
+                              const float *x2, int32_t ld2, int32_t w2, const float *hprev, int32_t ldp,
+                              const void *wiT_planes, int32_t kxp, const float *bi, const void *whT_planes,
+                              const float *bh, const float *ln_scale, const float *ln_bias, float *out, int32_t ldo,
+                              float *g4, int32_t ldg, int32_t R, int32_t H, void *stream);
+/* planes[q][n][k] = bf16x3 part q of (k < K ? W[k][n] : 0) for n < N, k < Kp: the transposed,
+ * zero-padded split of a (K, N) weight (row stride ldw) for msat_gru_ln_fused_fwd_x3r. */
+int msat_split_bf16x3_t(const float *W, int32_t K, int32_t N, int32_t ldw, int32_t Kp, void *planes, void *stream);
 /* msat_gru_ln_bwd from the fused forward's g4 tape (same outputs).  dbi (3H) / dbh_n (H), both
  * or neither, receive (+=) the gate-bias gradients sum_rows dGi and sum_rows dGh[:, 2H:3H]
  * (b_ir|b_iz|b_in and b_hn) from the same pass.  partial >= msat_gru_ln_bwd_partial_floats.

@@ -514,6 +514,11 @@ constexpr int kXR = 128;  // rows per workgroup (x3 kernel)
 #ifndef MSAT_GRU_ABL
 #define MSAT_GRU_ABL 0
 #endif
+// x3r kernel: 1 = tape stored straight from the accumulators (measured 0-4 % faster), 0 = float4
+// rows staged through LDS
+#ifndef MSAT_GRU_TAPE_DIRECT
+#define MSAT_GRU_TAPE_DIRECT 1
+#endif
 
 // 16 waves x 32 rows (RS = 4, RT = 1).
 //
@@ -686,6 +691,276 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
         return;
     }
     gru_ln_epilogue_x3<NW>(a, acc, hv, reinterpret_cast<float *>(&Bs[0][0]), row0, wu, wrow, li, lk, t);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Register-A bf16x3 form on v_mfma_f32_16x16x32_bf16 (msat_gru_ln_fused_fwd_x3r, H = 128).
+// 128-row tile, 8 waves; wave w owns rows 16 w .. 16 w + 15 and ALL 128 units of all four gates
+// (acc[gate][8 column tiles of 16], 128 accumulator registers), so its activation rows are private:
+// lane l needs A[l & 15][k0 + 8 (l >> 4) + j] of a 32-deep k step, two float4 loads straight from
+// the row into registers, split in registers.  Only the weights go through LDS: transposed planes
+// W^T [3 planes][3H][Kp] (msat_split_bf16x3_t, Kp % 32 == 0) arrive by LDS-DMA as per-(plane, gate)
+// images [128 units][4 chunks of 8 k] (64-byte rows, chunk c at slot c ^ f((u >> 2) & 3),
+// f = {0, 2, 3, 1}: conflict-free ds_read_b128 for this lane map), 72 KiB per step, double-buffered.
+// One barrier per 32 k.  The gate algebra is lane-local; LayerNorm row sums reduce over the 8
+// column tiles in-lane and the 16 lanes of a row group by shuffles; the tape and h' leave as
+// float4 rows staged per wave in LDS.
+__device__ __forceinline__ int gswz16(int b) { return (0x1E >> (2 * b)) & 3; }  // {0, 2, 3, 1}
+
+struct GruX3rArgs {
+    const float *seg[3];
+    int seg_ld[3];
+    int seg_w[3];
+    const float *hp;
+    int ldp;
+    const float *bi, *bh, *ln_scale, *ln_bias;
+    const __bf16 *wiT, *whT;  // [3][3H][kxp] / [3][3H][H]
+    int kxp;                  // multiple of 32
+    float *out;
+    int ldo;
+    float *g4;
+    int ldg;
+    int R, Kx;
+};
+
+typedef float f32x4g __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs a) {
+    constexpr int H = 128, IMG = H * 4;  // uint4 per (plane, gate) image: 128 units x 4 chunks = 8 KiB
+    __shared__ uint4 Bs[2][9][IMG];      // [buf][plane * 3 + gate], 144 KiB
+    const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int row0 = blockIdx.x * 128, wr = 16 * w;
+    const int arow = row0 + wr + l16, arc = arow < a.R ? arow : a.R - 1;
+    constexpr int nsh = H / 32;
+    const int ns = nsh + a.kxp / 32;
+    const float *const hp = a.hp, *const sg0 = a.seg[0], *const sg1 = a.seg[1], *const sg2 = a.seg[2];
+    const int w0 = a.seg_w[0], w01 = a.seg_w[0] + a.seg_w[1], kx_end = a.Kx;
+    const unsigned ro0 = (unsigned)arc * (unsigned)a.seg_ld[0], ro1 = (unsigned)arc * (unsigned)a.seg_ld[1],
+                   ro2 = (unsigned)arc * (unsigned)a.seg_ld[2];
+    const float *const hrow = hp + (size_t)arc * a.ldp + 8 * g;
+    // raw A of step s: two float4 (k = k0 + 8 g + 4 e); input steps select the segment per float4
+    float4 ra[2];
+    auto loadA = [&](int s) {
+        if (s < nsh) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) ra[e] = *reinterpret_cast<const float4 *>(hrow + 32 * s + 4 * e);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int kx = (s - nsh) * 32 + 8 * g + 4 * e;
+                const float *q0 = sg0 + (ro0 + (unsigned)(kx < w0 ? kx : 0));
+                const float *q1 = sg1 + (ro1 + (unsigned)(kx - w0));
+                const float *q2 = sg2 + (ro2 + (unsigned)(kx - w01));
+                const float *pp = (kx >= w01 && kx < kx_end) ? q2 : ((kx >= w0 && kx < w01) ? q1 : q0);
+                ra[e] = *reinterpret_cast<const float4 *>(pp);
+            }
+        }
+    };
+    // weight DMA: 72 wave-instructions (1 KiB = 16 units x 4 chunks) per step, 9 per wave; instruction
+    // e of wave w fills image x = (9 w + e) / 8 (plane * 3 + gate), units 16 p .. 16 p + 15 (p = (9 w + e) % 8).
+    // Lane -> unit 16 p + (lane >> 2), LDS chunk lane & 3 = source chunk (lane & 3) ^ f((lane >> 4) & 3).
+    const unsigned lpart = (unsigned)(lane >> 2) * 2u, chb = 16u * ((lane & 3) ^ gswz16((lane >> 4) & 3));
+    auto issueW = [&](int s, int buf) {
+        const bool hid = s < nsh;
+        const __bf16 *W = hid ? a.whT : a.wiT;
+        const int Kp = hid ? H : a.kxp;
+        const int k0 = hid ? 32 * s : 32 * (s - nsh);
+        const unsigned voff = lpart * (unsigned)Kp + chb;
+#pragma unroll
+        for (int e = 0; e < 9; ++e) {
+            const int x = 9 * w + e, img = x >> 3, p = x & 7, q = img / 3, gt = img - 3 * q;
+            const __bf16 *base = W + ((size_t)q * 3 * H + gt * H + 16 * p) * Kp + k0;
+            glds16_async_s(base, voff, &Bs[buf][img][64 * p]);
+        }
+    };
+    f32x4g acc[4][8];
+#pragma unroll
+    for (int G = 0; G < 4; ++G)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[G][j] = f32x4g{};
+    const int slot = g ^ gswz16((l16 >> 2) & 3);
+    auto step = [&](int s, auto hidc) {
+        constexpr bool hid = decltype(hidc)::value;
+        const int buf = s & 1;
+        float4 v0 = ra[0], v1 = ra[1];
+        if (!hid) {  // zero k >= Kx (padded weight rows are zero, the activations there are not)
+            const int kx = (s - nsh) * 32 + 8 * g;
+            if (kx >= kx_end) v0 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (kx + 4 >= kx_end) v1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        bf16x8 fa[3];
+        {
+            const Split8 sp = split8(v0, v1);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) fa[q] = __builtin_bit_cast(bf16x8, sp.p[q]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bool more = s + 1 < ns;
+        if (more) {
+            if (!(MSAT_GRU_ABL & 1)) issueW(s + 1, buf ^ 1);
+            if (!(MSAT_GRU_ABL & 2)) loadA(s + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int gt = 0; gt < (MSAT_GRU_ABL & 8 ? 0 : 3); ++gt) {
+            const int G = gt < 2 ? gt : (hid ? 3 : 2);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                bf16x8 fb[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    fb[q] = __builtin_bit_cast(bf16x8, Bs[buf][q * 3 + gt][(16 * j + l16) * 4 + slot]);
+                f32x4g c = acc[G][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[0], c, 0, 0, 0);
+                acc[G][j] = c;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (more && !(MSAT_GRU_ABL & 2)) wait_vmcnt<2>();  // W(s+1) landed; A(s+1), issued after it, may fly
+        else wait_vmcnt<0>();
+        barrier_lds();
+    };
+    loadA(0);
+    issueW(0, 0);
+    wait_vmcnt<0>();
+    barrier_lds();
+#pragma unroll 1
+    for (int s = 0; s < nsh; ++s) step(s, std::true_type{});
+#pragma unroll 1
+    for (int s = nsh; s < ns; ++s) step(s, std::false_type{});
+
+    if (MSAT_GRU_ABL & 16) {  // keep the accumulators live, store one value per lane
+        float v = 0.f;
+#pragma unroll
+        for (int G = 0; G < 4; ++G)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v += acc[G][j][j & 3];
+        if (arow < a.R) a.out[(size_t)arow * a.ldo + lane] = v;
+        return;
+    }
+    // ---- epilogue.  C/D map: unit u = 16 j + l16, row wr + 4 g + reg.
+    float *stage = reinterpret_cast<float *>(&Bs[0][0][0]) + w * 16 * 132;  // [16 rows][132] per wave
+    const bool tape = a.g4 != nullptr;
+    // h of each accumulator's (row, unit), loaded before the tape stores (vector-memory counts retire
+    // in issue order, so a load issued after them would wait for them)
+    float hv[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = row0 + wr + 4 * g + r;
+            hv[j][r] = hp[(size_t)(row < a.R ? row : a.R - 1) * a.ldp + 16 * j + l16];
+        }
+
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int u = 16 * j + l16;
+        const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
+        const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            acc[0][j][r] += br;
+            acc[1][j][r] += bz;
+            acc[2][j][r] += bni;
+            acc[3][j][r] += bnh;
+        }
+    }
+    // float4 rows of the wave's [16][128] stage -> dst (row stride ld), rows < R only.  LDS-only
+    // barriers: the global stores stay in flight (a __syncthreads release fence would drain them)
+    auto flush = [&](float *dst, int ld) {
+        barrier_lds();
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int rr = 2 * it + (lane >> 5), c4 = lane & 31;
+            const float4 v = *reinterpret_cast<const float4 *>(stage + rr * 132 + 4 * c4);
+            const int row = row0 + wr + rr;
+            if (row < a.R) *reinterpret_cast<float4 *>(dst + (size_t)row * ld + 4 * c4) = v;
+        }
+        barrier_lds();
+    };
+    if (tape) {
+#if MSAT_GRU_TAPE_DIRECT
+        // pre-activations straight from the accumulators (16 lanes x 4 B per row segment)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = row0 + wr + 4 * g + r;
+            if (row < a.R) {
+                float *q = a.g4 + (size_t)row * a.ldg + l16;
+#pragma unroll
+                for (int G = 0; G < 4; ++G)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) q[G * H + 16 * j] = acc[G][j][r];
+            }
+        }
+#else
+#pragma unroll
+        for (int G = 0; G < 4; ++G) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) stage[(4 * g + r) * 132 + 16 * j + l16] = acc[G][j][r];
+            flush(a.g4 + (size_t)G * H, a.ldg);
+        }
+#endif
+    }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float rg = fsig_fast(acc[0][j][r]), zg = fsig_fast(acc[1][j][r]);
+            const float ng = ftanh_fast(acc[2][j][r] + rg * acc[3][j][r]);
+            const float hn = (1.0f - zg) * ng + zg * hv[j][r];
+            acc[0][j][r] = hn;
+            s1[r] += hn;
+            s2[r] += hn * hn;
+        }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            s1[r] += __shfl_xor(s1[r], o, 16);
+            s2[r] += __shfl_xor(s2[r], o, 16);
+        }
+    float mean[4], rs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        mean[r] = s1[r] / (float)H;
+        const float var = fmaxf(s2[r] / (float)H - mean[r] * mean[r], 0.0f);
+        rs[r] = rsqrtf(var + 1e-6f);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int u = 16 * j + l16;
+        const float sc = a.ln_scale[u], lb = a.ln_bias[u];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            stage[(4 * g + r) * 132 + u] = (acc[0][j][r] - mean[r]) * (rs[r] * sc) + lb;
+    }
+    flush(a.out, a.ldo);
+}
+
+// planes[q][n][k] = part q of (k < K ? W[k][n] : 0), n < N, k < Kp: the transposed, zero-padded
+// bf16x3 split of a [K][N] weight (the x3r GRU kernel's W^T planes)
+__global__ void split_bf16x3_t_kernel(const float *__restrict__ W, int K, int N, int ldw, int Kp,
+                                      __bf16 *__restrict__ out) {
+    const size_t n = (size_t)N * Kp;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t c = i / Kp, k = i - c * Kp;
+        const float x = k < (size_t)K ? W[k * ldw + c] : 0.0f;
+        const __bf16 p = (__bf16)x;
+        const float res = x - (float)p;
+        const __bf16 m = (__bf16)res;
+        out[i] = p;
+        out[n + i] = m;
+        out[2 * n + i] = (__bf16)(res - (float)m);
+    }
 }
 
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -868,4 +1143,68 @@ extern "C" int msat_gru_ln_fused_fwd_x3(const float *x0, int32_t ld0, int32_t w0
     hipLaunchKernelGGL((gru_ln_fused_fwd_x3_kernel<4, 4>), dim3((R + kXR - 1) / kXR), dim3(1024), 0,
                        (hipStream_t)stream, a);
     return check_launch("gru_ln_fused_fwd_x3_kernel");
+}
+
+extern "C" int msat_split_bf16x3_t(const float *W, int32_t K, int32_t N, int32_t ldw, int32_t Kp, void *planes,
+                                   void *stream) {
+    if (K == 0 || N == 0) return MSAT_OK;
+    MSAT_REQUIRE(W && planes && K > 0 && N > 0 && ldw >= N && Kp >= K, "bad split_bf16x3_t args");
+    const size_t n = (size_t)N * Kp;
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(split_bf16x3_t_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, W, K, N, ldw, Kp,
+                       reinterpret_cast<__bf16 *>(planes));
+    return check_launch("split_bf16x3_t_kernel");
+}
+
+extern "C" int msat_gru_ln_fused_fwd_x3r(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1,
+                                         int32_t w1, const float *x2, int32_t ld2, int32_t w2, const float *hprev,
+                                         int32_t ldp, const void *wiT_planes, int32_t kxp, const float *bi,
+                                         const void *whT_planes, const float *bh, const float *ln_scale,
+                                         const float *ln_bias, float *out, int32_t ldo, float *g4, int32_t ldg,
+                                         int32_t R, int32_t H, void *stream) {
+    MSAT_REQUIRE(H == 128, "gru_ln_fused_fwd_x3r: H must be 128 (got %d)", H);
+    MSAT_REQUIRE(R >= 0, "gru_ln_fused_fwd_x3r: R < 0");
+    if (R == 0) return MSAT_OK;
+    MSAT_REQUIRE(x0 && hprev && wiT_planes && bi && whT_planes && bh && ln_scale && ln_bias && out, "NULL pointer");
+    MSAT_REQUIRE(ldo >= H && ldp >= H && (!g4 || ldg >= 4 * H), "gru_ln_fused_fwd_x3r: bad dims");
+    const float *seg[3] = {x0, x1, x2};
+    const int lds_[3] = {ld0, ld1, ld2}, ws[3] = {w0, w1, w2};
+    int Kx = 0;
+    for (int g = 0; g < 3; ++g) {
+        MSAT_REQUIRE(ws[g] >= 0 && ws[g] % 4 == 0, "gru_ln_fused_fwd_x3r: segment %d width %d must be a multiple of 4",
+                     g, ws[g]);
+        if (ws[g] == 0) continue;
+        MSAT_REQUIRE(seg[g] && aligned16(seg[g]) && lds_[g] % 4 == 0 && lds_[g] >= ws[g],
+                     "gru_ln_fused_fwd_x3r: segment %d must be 16-byte aligned with ld %% 4 == 0", g);
+        Kx += ws[g];
+    }
+    MSAT_REQUIRE(Kx > 0 && w0 > 0, "gru_ln_fused_fwd_x3r: empty input");
+    MSAT_REQUIRE(kxp % 32 == 0 && kxp >= Kx, "gru_ln_fused_fwd_x3r: kxp must be >= Kx and a multiple of 32");
+    MSAT_REQUIRE(aligned16(hprev) && ldp % 4 == 0 && aligned16(wiT_planes) && aligned16(whT_planes),
+                 "gru_ln_fused_fwd_x3r: hprev / weight planes must be 16-byte aligned");
+    MSAT_REQUIRE(aligned16(out) && ldo % 4 == 0 && (!g4 || (aligned16(g4) && ldg % 4 == 0)),
+                 "gru_ln_fused_fwd_x3r: out / g4 rows must be 16-byte aligned");
+    GruX3rArgs a = {};
+    for (int g = 0; g < 3; ++g) {
+        a.seg[g] = ws[g] ? seg[g] : nullptr;
+        a.seg_ld[g] = lds_[g];
+        a.seg_w[g] = ws[g];
+    }
+    a.hp = hprev;
+    a.ldp = ldp;
+    a.wiT = reinterpret_cast<const __bf16 *>(wiT_planes);
+    a.whT = reinterpret_cast<const __bf16 *>(whT_planes);
+    a.kxp = kxp;
+    a.bi = bi;
+    a.bh = bh;
+    a.ln_scale = ln_scale;
+    a.ln_bias = ln_bias;
+    a.out = out;
+    a.ldo = ldo;
+    a.g4 = g4;
+    a.ldg = ldg;
+    a.R = R;
+    a.Kx = Kx;
+    hipLaunchKernelGGL(gru_ln_fused_fwd_x3r_kernel, dim3((R + 127) / 128), dim3(512), 0, (hipStream_t)stream, a);
+    return check_launch("gru_ln_fused_fwd_x3r_kernel");
 }

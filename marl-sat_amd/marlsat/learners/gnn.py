@@ -169,6 +169,23 @@ class GNNActorCritic:
     # bf16x3 split GRU kernel (fp32-accurate, bf16 matrix cores) for the fused encoder at H = 128
     use_gru_x3 = os.environ.get("MARLSAT_GRU_X3", "1") != "0"
 
+    # register-A bf16x3 GRU kernel on 16x16x32 MFMAs (gru_fused.hip x3r): 5-8 % faster than the x3
+    # kernel without the tape (rollout), equal with it (training); opt-in (MARLSAT_GRU_X3R=1)
+    use_gru_x3r = os.environ.get("MARLSAT_GRU_X3R", "0") == "1"
+
+    def _split_weights_t(self, mats):
+        """{key: (K, 3H) matrix} -> {key: (W^T bf16x3 planes (3, 3H, Kp), Kp)}, Kp = K rounded up to 32
+        (msat_split_bf16x3_t: transposed, zero-padded, split in one pass; once per forward)."""
+        out = {}
+        for key, Wm in mats.items():
+            K, N = Wm.shape
+            Kp = (K + 31) // 32 * 32
+            buf = torch.empty(3 * N * Kp + 8, dtype=torch.int16, device=self.device)
+            _chk(L_.msat_split_bf16x3_t(Wm.data_ptr(), K, N, Wm.stride(0), Kp, buf.data_ptr(), self.stream),
+                 "split_bf16x3_t")
+            out[key] = (buf, Kp)
+        return out
+
     # transposed-weight GRU kernel (k-major images, ds_read_b128 fragments): measured equal to the
     # [K][3H] form (profiles/gru_bench.py: 855-3060 vs 888-3049 us) plus the per-forward transposes,
     # so it is opt-in (MARLSAT_GRU_T=1)
@@ -184,6 +201,15 @@ class GNNActorCritic:
         kx = sum(w for _, _, w in segs)
         GNNActorCritic.flops += 2 * R * 3 * H * (H + (kx + 15) // 16 * 16)
         (p0, l0, w0), (p1, l1, w1), (p2, l2, w2) = segs
+        if isinstance(wt, dict) and wt.get("x3r"):  # register-A kernel: W^T planes {"wi": (planes, kxp), "wh"}
+            _chk(L_.msat_gru_ln_fused_fwd_x3r(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
+                                              wt["wi"][0].data_ptr(), wt["wi"][1],
+                                              self.p(f"enc.{cell}_bi").data_ptr(), wt["wh"].data_ptr(),
+                                              self.p(f"enc.{cell}_bh").data_ptr(), self._ptr(ln_row),
+                                              self._ptr(ln_row, H), out.data_ptr(), H,
+                                              g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
+                 "msat_gru_ln_fused_fwd_x3r")
+            return
         if isinstance(wt, dict):  # bf16x3 planes {"wi": (planes, kxp), "wh": planes}
             _chk(L_.msat_gru_ln_fused_fwd_x3(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
                                              wt["wi"][0].data_ptr(), wt["wi"][1],
@@ -335,7 +361,12 @@ class GNNActorCritic:
         self._fold_weights()
         (Fc, Fp, Fn), _ = self._fold_views()
         wt = {"gru_c": None, "gru_vp": None, "gru_vn": None}
-        if self.use_gru_x3 and H == 128:
+        if self.use_gru_x3r and H == 128:
+            pl = self._split_weights_t({"c": Fc, "vp": Fp, "vn": Fn, "hc": self.p("enc.gru_c_wh"),
+                                        "hvp": self.p("enc.gru_vp_wh"), "hvn": self.p("enc.gru_vn_wh")})
+            wt = {c: {"x3r": True, "wi": pl[k], "wh": pl[hk][0]}
+                  for c, k, hk in (("gru_c", "c", "hc"), ("gru_vp", "vp", "hvp"), ("gru_vn", "vn", "hvn"))}
+        elif self.use_gru_x3 and H == 128:
             (Pc, Pp, Pn), _ = self._fold_views(padded=True)
             pl = self._split_weights({"c": (Pc, 0), "vp": (Pp, 0), "vn": (Pn, 0), "hc": (self.p("enc.gru_c_wh"), 0),
                                       "hvp": (self.p("enc.gru_vp_wh"), 0), "hvn": (self.p("enc.gru_vn_wh"), 0)})

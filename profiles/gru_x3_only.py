@@ -30,10 +30,18 @@ for kind in cells:
     args += [0, 0, 0] * (3 - len(segs_w))
     pi = torch.empty(3 * kxp * 3 * H + 8, dtype=torch.int16, device="cuda")
     ph = torch.empty(3 * H * 3 * H + 8, dtype=torch.int16, device="cuda")
-    _lib.lib.msat_split_bf16x3(wip.data_ptr(), kxp, 3 * H, 3 * H, pi.data_ptr(), _lib.stream_ptr())
-    _lib.lib.msat_split_bf16x3(wh.data_ptr(), H, 3 * H, 3 * H, ph.data_ptr(), _lib.stream_ptr())
+    fn = _lib.lib.msat_gru_ln_fused_fwd_x3
+    if os.environ.get("MARLSAT_GRU_LAYOUT") == "x3r":  # register-A kernel: W^T planes, K padded to 32
+        kxp = (Kx + 31) // 32 * 32
+        pi = torch.empty(3 * kxp * 3 * H + 8, dtype=torch.int16, device="cuda")
+        _lib.lib.msat_split_bf16x3_t(wip.data_ptr(), Kx, 3 * H, 3 * H, kxp, pi.data_ptr(), _lib.stream_ptr())
+        _lib.lib.msat_split_bf16x3_t(wh.data_ptr(), H, 3 * H, 3 * H, H, ph.data_ptr(), _lib.stream_ptr())
+        fn = _lib.lib.msat_gru_ln_fused_fwd_x3r
+    else:
+        _lib.lib.msat_split_bf16x3(wip.data_ptr(), kxp, 3 * H, 3 * H, pi.data_ptr(), _lib.stream_ptr())
+        _lib.lib.msat_split_bf16x3(wh.data_ptr(), H, 3 * H, 3 * H, ph.data_ptr(), _lib.stream_ptr())
     for tape in (False, True):
-        f = lambda: _lib.lib.msat_gru_ln_fused_fwd_x3(*args, h.data_ptr(), H, pi.data_ptr(), kxp, bi.data_ptr(),
+        f = lambda: fn(*args, h.data_ptr(), H, pi.data_ptr(), kxp, bi.data_ptr(),
                                                       ph.data_ptr(), bh.data_ptr(), sc.data_ptr(), lb.data_ptr(),
                                                       out.data_ptr(), H, g4.data_ptr() if tape else 0, 4 * H, R, H,
                                                       _lib.stream_ptr())

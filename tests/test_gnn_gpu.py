@@ -72,17 +72,18 @@ def _close_norm(dev, ref, rtol, what):
     _close(dev, ref, 0.0, rtol * max(np.abs(ref[fin]).max(), 1e-12), what)
 
 
-@pytest.mark.parametrize("fuse,x3", [(True, True), (True, False), (False, True)])
+@pytest.mark.parametrize("fuse,x3", [(True, True), (True, False), (False, True), (True, "r")])
 @pytest.mark.parametrize("V,C,vpa,H,L,S,mode", CASES)
 def test_forward_backward_match_oracle(V, C, vpa, H, L, S, mode, fuse, x3, monkeypatch):
     """fuse: phi folded into the GRU input matrices (else reference order); x3: bf16x3 data
     gradients with packed backward rows and the bf16x3 GRU forward at H = 128 (else fp32 MFMA
-    GEMMs / GRU, separate dGi / dGh)."""
+    GEMMs / GRU, separate dGi / dGh); "r": the same with the register-A GRU forward (x3r)."""
     from marlsat.learners.gnn import GNNActorCritic
 
     monkeypatch.setattr(GNNActorCritic, "fuse_phi", fuse)
-    monkeypatch.setattr(GNNActorCritic, "use_x3", x3)
-    monkeypatch.setattr(GNNActorCritic, "use_gru_x3", x3)
+    monkeypatch.setattr(GNNActorCritic, "use_x3", bool(x3))
+    monkeypatch.setattr(GNNActorCritic, "use_gru_x3", bool(x3))
+    monkeypatch.setattr(GNNActorCritic, "use_gru_x3r", x3 == "r")
     net, b, P, batch, av, am, A, M = _setup(V, C, vpa, H, L, S, mode)
     logits, value, state = net.forward(b, save=True)
     ref_logits = onet.actor_logits(P, L, batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"], av,

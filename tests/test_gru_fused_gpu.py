@@ -95,6 +95,20 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
                                                      R, H, _lib.stream_ptr()), "gru_ln_fused_fwd_x3")
         torch.cuda.synchronize()
         return out
+    if layout == "x3r":  # register-A bf16x3 kernel (16x16x32): transposed planes W^T, K padded to 32
+        K = wi.shape[0]
+        kxp = (K + 31) // 32 * 32
+        pi = torch.empty(3 * 3 * H * kxp + 8, dtype=torch.int16, device="cuda")
+        ph = torch.empty(3 * 3 * H * H + 8, dtype=torch.int16, device="cuda")
+        s = _lib.stream_ptr()
+        _lib.check(_lib.lib.msat_split_bf16x3_t(wi.data_ptr(), K, 3 * H, 3 * H, kxp, pi.data_ptr(), s), "split_t")
+        _lib.check(_lib.lib.msat_split_bf16x3_t(wh.data_ptr(), H, 3 * H, 3 * H, H, ph.data_ptr(), s), "split_t")
+        _lib.check(_lib.lib.msat_gru_ln_fused_fwd_x3r(*args, h.data_ptr(), H, pi.data_ptr(), kxp, bi.data_ptr(),
+                                                      ph.data_ptr(), bh.data_ptr(), sc.data_ptr(), lb.data_ptr(),
+                                                      out.data_ptr(), H, g4.data_ptr() if g4 is not None else 0,
+                                                      4 * H, R, H, s), "gru_ln_fused_fwd_x3r")
+        torch.cuda.synchronize()
+        return out
     if layout == "t":  # transposed-weight kernel (k-major images, ds_read_b128 fragments)
         wiT, whT = _transposed(wi), _transposed(wh)
         assert bool((wiT[:, wi.shape[0]:] == 0).all()) and torch.equal(wiT[:, :wi.shape[0]], wi.t())
@@ -113,8 +127,9 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
 
 def _fwd_cases():
     """(layout, H, R): the plain kernel at H 64 / 128 / 256, the transposed-weight kernel at H 64 /
-    128, the bf16x3 kernel at H 128; the 70,000-row case at the production width H = 128 only."""
-    widths = {"plain": (64, 128, 256), "t": (64, 128), "x3": (128,)}
+    128, the bf16x3 kernels (LDS-staged, register-A) at H 128; the 70,000-row case at the
+    production width H = 128 only."""
+    widths = {"plain": (64, 128, 256), "t": (64, 128), "x3": (128,), "x3r": (128,)}
     return [(lay, H, R) for lay, hs in widths.items() for H in hs for R in (0, 1, 77, 1000, 70000)
             if R != 70000 or H == 128]
 
