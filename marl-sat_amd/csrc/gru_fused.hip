@@ -516,6 +516,10 @@ constexpr int kXR = 128;  // rows per workgroup (x3 kernel)
 #endif
 // x3r kernel: 1 = tape stored straight from the accumulators (measured 0-4 % faster), 0 = float4
 // rows staged through LDS
+// x3r kernel: 1 = activations loaded two steps ahead by asm, split among the previous step's MFMAs
+#ifndef MSAT_GRU_X3R_PIPE
+#define MSAT_GRU_X3R_PIPE 1
+#endif
 #ifndef MSAT_GRU_TAPE_DIRECT
 #define MSAT_GRU_TAPE_DIRECT 1
 #endif
@@ -826,6 +830,91 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
         else wait_vmcnt<0>();
         barrier_lds();
     };
+#if MSAT_GRU_X3R_PIPE
+    // Pipelined form: activation loads by asm (invisible to hipcc's wait insertion) two steps
+    // ahead into alternating register sets; the split of step s + 1 runs among step s's MFMAs;
+    // one vmcnt(0) + barrier per step (the weights of s + 1 and the activations of s + 2, both
+    // issued at the start of step s, have landed).  The wait names the set just loaded as an
+    // in/out operand, so no use of it is scheduled above the wait.
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v ras[2][2];  // [set = step & 1][half]
+    auto aptr = [&](int st, int e) -> const float * {
+        if (st < nsh) return hrow + 32 * st + 4 * e;
+        const int kx = (st - nsh) * 32 + 8 * g + 4 * e;
+        const float *q0 = sg0 + (ro0 + (unsigned)(kx < w0 ? kx : 0));
+        const float *q1 = sg1 + (ro1 + (unsigned)(kx - w0));
+        const float *q2 = sg2 + (ro2 + (unsigned)(kx - w01));
+        return (kx >= w01 && kx < kx_end) ? q2 : ((kx >= w0 && kx < w01) ? q1 : q0);
+    };
+    auto aload = [&](int st, f4v (&r)[2]) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[e]) : "v"(aptr(st, e)) : "memory");
+    };
+    auto await0 = [&](f4v (&r)[2]) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]) :: "memory"); };
+    auto asplit = [&](int st, const f4v (&r)[2], bf16x8 (&f)[3]) {  // branch-free (selects)
+        const int kx = (st - nsh) * 32 + 8 * g;
+        const bool z0 = st >= nsh && kx >= kx_end, z1 = st >= nsh && kx + 4 >= kx_end;
+        const f4v zero = {0.f, 0.f, 0.f, 0.f};
+        const float4 v0 = __builtin_bit_cast(float4, z0 ? zero : r[0]);
+        const float4 v1 = __builtin_bit_cast(float4, z1 ? zero : r[1]);
+        const Split8 sp = split8(v0, v1);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) f[q] = __builtin_bit_cast(bf16x8, sp.p[q]);
+    };
+    bf16x8 fas[2][3];  // split activations of step s in fas[s & 1]
+    aload(0, ras[0]);
+    if (ns > 1) aload(1, ras[1]);
+    issueW(0, 0);
+    await0(ras[0]);
+    await0(ras[1]);
+    asplit(0, ras[0], fas[0]);
+    barrier_lds();
+    auto pstep = [&](int st, auto hidc, auto parc) {
+        constexpr bool hid = decltype(hidc)::value;
+        constexpr int P = decltype(parc)::value;  // st & 1
+        const int buf = P;
+        if (st + 1 < ns) issueW(st + 1, buf ^ 1);
+        if (st + 2 < ns) aload(st + 2, ras[P]);
+#pragma unroll
+        for (int gt = 0; gt < 3; ++gt) {
+            const int G = gt < 2 ? gt : (hid ? 3 : 2);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                bf16x8 fb[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    fb[q] = __builtin_bit_cast(bf16x8, Bs[buf][q * 3 + gt][(16 * j + l16) * 4 + slot]);
+                f32x4g c = acc[G][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][2], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][1], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][0], fb[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][1], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][0], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][0], fb[0], c, 0, 0, 0);
+                acc[G][j] = c;
+            }
+            // among the MFMAs; unconditional (after the last step it splits stale registers, unused)
+            if (gt == 0) asplit(st + 1, ras[P ^ 1], fas[P ^ 1]);
+        }
+        await0(ras[P]);
+        barrier_lds();
+    };
+    {
+        int st = 0;
+#pragma unroll 1
+        for (; st + 1 < nsh; st += 2) {
+            pstep(st, std::true_type{}, std::integral_constant<int, 0>{});
+            pstep(st + 1, std::true_type{}, std::integral_constant<int, 1>{});
+        }
+        // nsh = 4 is even: the input steps start at parity 0
+#pragma unroll 1
+        for (; st + 1 < ns; st += 2) {
+            pstep(st, std::false_type{}, std::integral_constant<int, 0>{});
+            pstep(st + 1, std::false_type{}, std::integral_constant<int, 1>{});
+        }
+        if (st < ns) pstep(st, std::false_type{}, std::integral_constant<int, 0>{});
+    }
+#else
     loadA(0);
     issueW(0, 0);
     wait_vmcnt<0>();
@@ -834,6 +923,7 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
     for (int s = 0; s < nsh; ++s) step(s, std::true_type{});
 #pragma unroll 1
     for (int s = nsh; s < ns; ++s) step(s, std::false_type{});
+#endif
 
     if (MSAT_GRU_ABL & 16) {  // keep the accumulators live, store one value per lane
         float v = 0.f;
