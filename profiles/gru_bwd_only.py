@@ -1,0 +1,36 @@
+"""GRU + LayerNorm backward from the tape (msat_gru_ln_bwd_g4f, packed rows, dh assigned, gate-bias and
+feature partials) on the uf50 training shapes, HIP-event timed, with its HBM rate.
+usage: gru_bwd_only.py [reps]
+Measured: var 507 us (4.5 TB/s), clause 1067 us (5.5 TB/s); more blocks, or two rows per wave with
+all loads first (3 / 2 waves per SIMD instead of 5 / 4), measured slower."""
+import json, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "marl-sat_amd")]
+import torch
+from marlsat import _lib
+
+L = _lib.lib
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+H = 128
+s = _lib.stream_ptr()
+for what, R, nf, ldf in [("var", 407000, 6, 8), ("clause", 1036000, 2, 4)]:
+    r = lambda *sh: torch.randn(*sh, device="cuda")
+    dy, g4, hp, feat = r(R, H), r(R, 4 * H), r(R, H), r(R, ldf)
+    sc, dln = r(H), torch.zeros(2 * H, device="cuda")
+    dG, dh = torch.empty(R, 4 * H, device="cuda"), torch.empty(R, H, device="cuda")
+    dbi, dbh, dfeat = torch.zeros(3 * H, device="cuda"), torch.zeros(H, device="cuda"), torch.zeros(nf * 3 * H, device="cuda")
+    part = torch.empty(int(L.msat_gru_ln_bwd_partial_floats(R, H)), device="cuda")
+    f = lambda: L.msat_gru_ln_bwd_g4f(dy.data_ptr(), H, g4.data_ptr(), 4 * H, hp.data_ptr(), H, sc.data_ptr(),
+                                      dG.data_ptr(), 4 * H, dG.data_ptr() + 4 * H, 4 * H, dh.data_ptr(), H,
+                                      dln.data_ptr(), dln.data_ptr() + 4 * H, dbi.data_ptr(), dbh.data_ptr(),
+                                      feat.data_ptr(), ldf, nf, dfeat.data_ptr(), part.data_ptr(), R, H, 0b111, s)
+    assert f() == 0
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        f()
+    b.record(); torch.cuda.synchronize()
+    us = a.elapsed_time(b) / reps * 1e3
+    nbytes = R * 4 * (H + 4 * H + H + nf + 4 * H + H)  # dy, tape, h, feat in; packed dG, dh out
+    print(json.dumps({"what": what, "R": R, "us": round(us, 1), "GBps": round(nbytes / us / 1e3, 1)}))
