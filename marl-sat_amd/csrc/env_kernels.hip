@@ -1,6 +1,6 @@
 // Batched multi-agent SAT environment on gfx950.
 //
-// One workgroup (kThreads lanes) owns one environment for the whole call:
+// One workgroup (256 lanes; 64 for small instances, env_threads) owns one environment for the whole call:
 //   1. assignment -> LDS bit words (one ballot per 64 vars), agents' flips as
 //      LDS atomic XORs;
 //   2. every clause evaluated once from the L2/MALL-resident packed pool
@@ -85,16 +85,17 @@ __device__ __forceinline__ EnvLds carve(uint32_t *smem, const EnvParams &p) {
 __device__ __forceinline__ uint32_t bit(const uint32_t *w, int i) { return (w[i >> 5] >> (i & 31)) & 1u; }
 
 // Assignment bytes -> LDS bit words, one ballot per 64 vars.
+template <int T>
 __device__ __forceinline__ void load_x_bits(const EnvParams &p, const EnvLds &l, const uint8_t *__restrict__ xg) {
     const int lane = threadIdx.x & 63;
-    for (int v0 = threadIdx.x & ~63; v0 < p.WV * 32; v0 += kThreads) {
+    for (int v0 = threadIdx.x & ~63; v0 < p.WV * 32; v0 += T) {
         const int v = v0 + lane;
         const uint64_t m = __ballot(v < p.V && (xg[v] & 1u));
         if (lane < 2) l.x[(v0 >> 5) + lane] = (uint32_t)(m >> (32 * lane));
     }
 }
 
-// Prefetch depth (per lane) of the step path: pool-row words (covers C <= kPfClause*kThreads
+// Prefetch depth (per lane) of the step path: pool-row words (covers C <= kPfClause*T
 // clauses) and agent-table words, all issued right after problem_idx is known so the
 // preamble costs ~2 dependent memory round trips instead of ~4.
 constexpr int kPfClause = 4;
@@ -130,7 +131,7 @@ __device__ __forceinline__ void clause_slice(const EnvParams &p, const EnvLds &l
 // Evaluate every clause of pool row `pidx` against l.x: clause bits -> l.sat,
 // bytes -> sat_g / ntrue_g, unsat count (and PBRS newly-satisfied) -> red[0] / red[1].
 // The first NPF slices use the lane's prefetched pool words pw[].
-template <bool kPbrs, int NPF>
+template <int T, bool kPbrs, int NPF>
 __device__ __forceinline__ void eval_clauses(const EnvParams &p, const EnvLds &l, const uint16_t *__restrict__ lits,
                                              int pidx, uint8_t *__restrict__ sat_g, uint8_t *__restrict__ ntrue_g,
                                              const uint64_t (&pw)[kPfClause]) {
@@ -140,10 +141,10 @@ __device__ __forceinline__ void eval_clauses(const EnvParams &p, const EnvLds &l
     const int cend = p.WC * 32;
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
-        const int c0 = (threadIdx.x & ~63) + j * kThreads;
+        const int c0 = (threadIdx.x & ~63) + j * T;
         if (c0 < cend) clause_slice<kPbrs>(p, l, c0, pw[j], sat_g, ntrue_g, unsat, newly);
     }
-    for (int c0 = (threadIdx.x & ~63) + NPF * kThreads; c0 < cend; c0 += kThreads) {
+    for (int c0 = (threadIdx.x & ~63) + NPF * T; c0 < cend; c0 += T) {
         const int c = c0 + lane;
         const uint64_t w = c < p.C ? prow[c] : 0ull;  // pool rows are shared by many envs: keep them cached
         clause_slice<kPbrs>(p, l, c0, w, sat_g, ntrue_g, unsat, newly);
@@ -175,10 +176,11 @@ __device__ __forceinline__ void or_bits(uint32_t *img, int dst, uint32_t bits) {
     }
 }
 
+template <int T>
 __device__ __forceinline__ void build_obs_images(const EnvParams &p, const EnvLds &l) {
     const int nwV = (p.V + 31) >> 5, nwC = (p.C + 31) >> 5;
     const int U = 2 * nwV + nwC;  // source words per row
-    for (int t = threadIdx.x; t < p.A * U; t += kThreads) {
+    for (int t = threadIdx.x; t < p.A * U; t += T) {
         const int i = t / U;
         int s = t - i * U;
         int len, off;
@@ -248,20 +250,20 @@ struct ObsVec<int8_t> {
 };
 
 // Stream the env's (A, D) observation block from the bit images: unaligned head, 16 B body, tail.
-template <typename ObsT>
+template <int T, typename ObsT>
 __device__ __forceinline__ void write_obs(const EnvParams &p, const EnvLds &l, ObsT *__restrict__ o) {
     constexpr int VEC = ObsVec<ObsT>::N;
     const int total = p.A * p.D;
     int head = (int)((reinterpret_cast<uintptr_t>(o) / sizeof(ObsT)) % VEC);
     head = head ? VEC - head : 0;
     head = min(head, total);
-    for (int e = threadIdx.x; e < head; e += kThreads) o[e] = (ObsT)elem_val(bits_at(l.fm, e), bits_at(l.fx, e), 0);
+    for (int e = threadIdx.x; e < head; e += T) o[e] = (ObsT)elem_val(bits_at(l.fm, e), bits_at(l.fx, e), 0);
     const int nchunks = (total - head) / VEC;
-    for (int q = threadIdx.x; q < nchunks; q += kThreads) {
+    for (int q = threadIdx.x; q < nchunks; q += T) {
         const int e = head + q * VEC;
         ObsVec<ObsT>::store(o + e, bits_at(l.fm, e), bits_at(l.fx, e));
     }
-    for (int e = head + nchunks * VEC + threadIdx.x; e < total; e += kThreads)
+    for (int e = head + nchunks * VEC + threadIdx.x; e < total; e += T)
         o[e] = (ObsT)elem_val(bits_at(l.fm, e), bits_at(l.fx, e), 0);
 }
 
@@ -280,7 +282,7 @@ __device__ __forceinline__ int xcd_major(int blk, int n, bool off) {
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // One environment (index b of its batch) advanced / reset / observed by one workgroup.
-template <int MODE, typename ObsT>
+template <int MODE, typename ObsT, int T>
 __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &pool, const msat_env_state &st,
                                         const int32_t *__restrict__ actions, const uint8_t *__restrict__ reset_mask,
                                         const int32_t *__restrict__ new_pidx, const uint8_t *__restrict__ new_assign,
@@ -307,17 +309,17 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         const uint32_t *nbr_g = pool.nbr + (size_t)pidx * p.A * p.WV;
 #pragma unroll
         for (int j = 0; j < kPfClause; ++j) {
-            const int c = tid + j * kThreads;
+            const int c = tid + j * T;
             pw[j] = c < p.C ? prow[c] : 0ull;
         }
 #pragma unroll
         for (int j = 0; j < kPfRel; ++j) {
-            const int t = tid + j * kThreads;
+            const int t = tid + j * T;
             prel[j] = t < p.A * p.WC ? rel_g[t] : 0u;
         }
 #pragma unroll
         for (int j = 0; j < kPfNbr; ++j) {
-            const int t = tid + j * kThreads;
+            const int t = tid + j * T;
             pnbr[j] = t < p.A * p.WV ? nbr_g[t] : 0u;
         }
         // step-0 / unsat-0 and this lane's first action, loaded with the prefetch
@@ -326,12 +328,12 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         int a0 = 0;
         if (MODE != kModeObs && p.action_mode == 0 && tid < p.A) a0 = actions[(size_t)b * p.A + tid];
         // ---- assignment + the agents' flips (env:230-250) --------------------
-        load_x_bits(p, l, xg);
+        load_x_bits<T>(p, l, xg);
         lds_barrier();
         if (MODE == kModeObs) {
             // get_obs only: no flips, no state update
         } else if (p.action_mode == 0) {
-            for (int i = tid; i < p.A; i += kThreads) {
+            for (int i = tid; i < p.A; i += T) {
                 const int a = i == tid ? a0 : actions[(size_t)b * p.A + i];
                 const int n = agent_size(p, i);
                 if (a >= n) continue;  // no-op index (and every action of a var-less agent)
@@ -349,7 +351,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
                 }
             }
         } else {
-            for (int t = tid; t < p.A * p.M; t += kThreads) {
+            for (int t = tid; t < p.A * p.M; t += T) {
                 const int i = t / p.M, j = t - (t / p.M) * p.M;
                 if (j < agent_size(p, i) && (actions[(size_t)b * p.A * p.M + t] & 1)) {
                     const int v = agent_lo(p, i) + j;
@@ -360,9 +362,9 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         lds_barrier();
         // ---- clause scan of the stepped assignment (env:252-254) ------------
         if (MODE != kModeObs && p.reward_mode == MSAT_REWARD_PBRS)
-            eval_clauses<true, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
+            eval_clauses<T, true, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
         else
-            eval_clauses<false, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
+            eval_clauses<T, false, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
         lds_barrier();
         if (MODE != kModeObs && tid == 0) {
             const int u_new = l.red[0];
@@ -411,10 +413,10 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
             pidx = (int)(((uint64_t)r.x * (uint64_t)p.N) >> 32);
         }
         if (new_assign != nullptr) {
-            load_x_bits(p, l, new_assign + (size_t)b * p.V);
+            load_x_bits<T>(p, l, new_assign + (size_t)b * p.V);
         } else {
             // word t of the assignment = lane t%4 of the Philox block 1 + t/4 (128 vars per block)
-            for (int t = tid; t < p.WV; t += kThreads) {
+            for (int t = tid; t < p.WV; t += T) {
                 const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 1u + (uint32_t)(t >> 2));
                 const int lane = t & 3;
                 uint32_t w = lane == 0 ? r.x : lane == 1 ? r.y : lane == 2 ? r.z : r.w;
@@ -425,7 +427,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         }
         if (tid < 2) l.red[tid] = 0;  // red[2] (reset broadcast) may still be read by slower waves
         lds_barrier();
-        eval_clauses<false, 0>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
+        eval_clauses<T, false, 0>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
         lds_barrier();
         if (tid == 0) {
             st.num_unsat[b] = l.red[0];
@@ -435,7 +437,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         }
     }
     if (MODE != kModeObs)
-        for (int v = tid; v < p.V; v += kThreads) xg[v] = (uint8_t)bit(l.x, v);
+        for (int v = tid; v < p.V; v += T) xg[v] = (uint8_t)bit(l.x, v);
     if ((p.ablate & 3) == 2 || obs == nullptr) return;  // NULL obs: state-only step (single-agent SatEnv)
     // ---- stage the instance's agent tables (built once per pool instance) --
     {
@@ -446,44 +448,44 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         if (pf) {
 #pragma unroll
             for (int j = 0; j < kPfRel; ++j)
-                if (tid + j * kThreads < p.A * p.WC) l.rel[tid + j * kThreads] = prel[j];
+                if (tid + j * T < p.A * p.WC) l.rel[tid + j * T] = prel[j];
 #pragma unroll
             for (int j = 0; j < kPfNbr; ++j)
-                if (tid + j * kThreads < p.A * p.WV) l.nbr[tid + j * kThreads] = pnbr[j];
-            t0r = kPfRel * kThreads;
-            t0n = kPfNbr * kThreads;
+                if (tid + j * T < p.A * p.WV) l.nbr[tid + j * T] = pnbr[j];
+            t0r = kPfRel * T;
+            t0n = kPfNbr * T;
         }
-        for (int t = t0r + tid; t < p.A * p.WC; t += kThreads) l.rel[t] = rel_g[t];
-        for (int t = t0n + tid; t < p.A * p.WV; t += kThreads) l.nbr[t] = nbr_g[t];
-        for (int t = tid; t < 2 * obs_image_words(p); t += kThreads) l.fm[t] = 0u;  // fm, fx contiguous
+        for (int t = t0r + tid; t < p.A * p.WC; t += T) l.rel[t] = rel_g[t];
+        for (int t = t0n + tid; t < p.A * p.WV; t += T) l.nbr[t] = nbr_g[t];
+        for (int t = tid; t < 2 * obs_image_words(p); t += T) l.fm[t] = 0u;  // fm, fx contiguous
     }
     lds_barrier();
     ObsT *o = obs + (size_t)b * p.A * p.D;
     if ((p.ablate & 3) == 0) {
-        build_obs_images(p, l);
+        build_obs_images<T>(p, l);
         lds_barrier();
-        write_obs<ObsT>(p, l, o);
+        write_obs<T, ObsT>(p, l, o);
     } else {
         constexpr int VEC = ObsVec<ObsT>::N;
         const int n = (p.A * p.D) / VEC;
-        for (int q = tid; q < n; q += kThreads) ObsVec<ObsT>::store(o + q * VEC, 0u, 0u);
+        for (int q = tid; q < n; q += T) ObsVec<ObsT>::store(o + q * VEC, 0u, 0u);
     }
 }
 
-template <int MODE, typename ObsT>
-__global__ void __launch_bounds__(kThreads)
+template <int MODE, typename ObsT, int T>
+__global__ void __launch_bounds__(T)
 env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__restrict__ actions,
            const uint8_t *__restrict__ reset_mask, const int32_t *__restrict__ new_pidx,
            const uint8_t *__restrict__ new_assign, uint64_t seed, uint64_t ctr, msat_step_out out,
            ObsT *__restrict__ obs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int b = xcd_major(blockIdx.x, p.B, p.ablate & 4);
-    env_run<MODE, ObsT>(p, pool, st, actions, reset_mask, new_pidx, new_assign, seed, ctr, out, obs, b, smem);
+    env_run<MODE, ObsT, T>(p, pool, st, actions, reset_mask, new_pidx, new_assign, seed, ctr, out, obs, b, smem);
 }
 
 // Ragged batches (BASELINE config 5): several size classes, each its own (V, C, A) batch with its own
-// pool / state / obs, advanced by ONE launch.  Blocks map to (class, env) in class order after the
-// XCD-major permutation of the whole grid.  Class g draws its resets from seed ^ group_seed(g), so it
+// pool / state / obs, advanced by ONE launch (256-lane workgroups).  Blocks map to (class, env) with
+// the classes laid out most expensive first (launch_groups).  Class g draws its resets from seed ^ group_seed(g), so it
 // replays exactly as a single-class launch with that seed (group_seed(0) = 0).
 struct EnvGroup {
     EnvParams p;
@@ -515,7 +517,7 @@ env_group_kernel(EnvGroups gs, uint64_t seed, uint64_t ctr) {
     for (int k = 1; k < MSAT_MAX_GROUPS; ++k)
         if (k < gs.G && gb >= gs.g[k].begin) g = k;
     const EnvGroup &e = gs.g[g];
-    env_run<MODE, ObsT>(e.p, e.pool, e.st, e.actions, nullptr, nullptr, nullptr, seed ^ group_seed(e.gid), ctr, e.out,
+    env_run<MODE, ObsT, kThreads>(e.p, e.pool, e.st, e.actions, nullptr, nullptr, nullptr, seed ^ group_seed(e.gid), ctr, e.out,
                         reinterpret_cast<ObsT *>(e.obs), gb - e.begin, smem);
 }
 
@@ -790,6 +792,20 @@ static int check_pool(const msat_pool *pool) {
     return MSAT_OK;
 }
 
+// Workgroup size of the single-class env kernel: one wave per env for small instances (more envs
+// resident per CU: the per-env chain of dependent memory round trips, not bandwidth, bounds them),
+// 256 lanes otherwise.  MARLSAT_ENV_THREADS (64 / 128 / 256) overrides.
+static int env_threads(const EnvParams &p) {
+    static const int forced = [] {
+        const char *e = getenv("MARLSAT_ENV_THREADS");
+        const int v = e ? atoi(e) : 0;
+        return v == 64 || v == 128 || v == 256 ? v : 0;
+    }();
+    if (forced) return forced;
+    // uf50 x 4096: 13.4 us at 64 lanes vs 20.0 at 256; uf100 equal; uf200 x 4096: 113 vs 142 us
+    return (long)p.A * p.D <= 4096 ? 64 : 256;
+}
+
 template <int MODE>
 static int launch_env(const EnvParams &p, const msat_env_desc *d, const msat_pool *pool,
                       const msat_env_state *st, const int32_t *actions, const uint8_t *mask,
@@ -800,12 +816,22 @@ static int launch_env(const EnvParams &p, const msat_env_desc *d, const msat_poo
     msat_step_out o{};
     if (out) o = *out;
     if (p.B == 0) return MSAT_OK;
-    if (d->obs_dtype == MSAT_OBS_I32)
-        hipLaunchKernelGGL((env_kernel<MODE, int32_t>), dim3(p.B), dim3(kThreads), lds, s, p, *pool, *st, actions,
-                           mask, npidx, nassign, seed, ctr, o, (int32_t *)obs);
-    else
-        hipLaunchKernelGGL((env_kernel<MODE, int8_t>), dim3(p.B), dim3(kThreads), lds, s, p, *pool, *st, actions,
+    const int T = env_threads(p);
+#define MSAT_ENV_LAUNCH(TT)                                                                                        \
+    if (d->obs_dtype == MSAT_OBS_I32)                                                                              \
+        hipLaunchKernelGGL((env_kernel<MODE, int32_t, TT>), dim3(p.B), dim3(TT), lds, s, p, *pool, *st, actions,    \
+                           mask, npidx, nassign, seed, ctr, o, (int32_t *)obs);                                    \
+    else                                                                                                           \
+        hipLaunchKernelGGL((env_kernel<MODE, int8_t, TT>), dim3(p.B), dim3(TT), lds, s, p, *pool, *st, actions,     \
                            mask, npidx, nassign, seed, ctr, o, (int8_t *)obs);
+    if (T == 64) {
+        MSAT_ENV_LAUNCH(64)
+    } else if (T == 128) {
+        MSAT_ENV_LAUNCH(128)
+    } else {
+        MSAT_ENV_LAUNCH(256)
+    }
+#undef MSAT_ENV_LAUNCH
     return check_launch("env_kernel");
 }
 
