@@ -45,6 +45,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
 
 
+
+def env_lanes(A: int, D: int) -> int:
+    """Workgroup size the env step launches with (env_kernels.hip env_threads): for the kernel label."""
+    n = A * D
+    return 64 if n <= 4096 else (512 if n >= 16384 else 256)
+
 def step_bytes(V: int, C: int, A: int) -> int:
     """Algorithmic bytes of one env-step (reference API dtypes)."""
     D = 2 * V + C
@@ -288,28 +294,42 @@ def env_leg(args, rank, world, dist):
         obs, states, outs = [o], [st], [classes[0]._step_out(sizes[0])]
         sstep = classes[0].stepper(st, o, outs[0], autoreset=True, seed=seed)
         step = lambda i, c: sstep(acts[0][i % ring], c)
-        kernel = "env_kernel<2,int>"
+        e0 = classes[0]
+        lanes = int(os.environ.get("MARLSAT_ENV_THREADS", "0")) or env_lanes(e0.num_agents, 2 * e0.num_vars + e0.num_clauses)
+        kernel = f"env_kernel<2,{'int' if obs_dtype == torch.int32 else 'signed char'},{lanes}>"
     counter = 1
     for i in range(args.warmup):
         step(i, counter)
         counter += 1
     torch.cuda.synchronize()
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    # HIP events on the kernel's stream (torch's current stream) bracket the whole timed region:
+    # the launches run back to back, so span / K is the mean launch duration.  (An event pair
+    # around every launch put a marker between consecutive launches and cost ~15 us per step.)
+    per_launch = os.environ.get("MARLSAT_BENCH_PER_LAUNCH_EVENTS") == "1"
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K if per_launch else 1)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(K):
-        ev[i][0].record()
-        step(i, counter)
-        ev[i][1].record()
-        counter += 1
+    if per_launch:
+        for i in range(K):
+            ev[i][0].record()
+            step(i, counter)
+            ev[i][1].record()
+            counter += 1
+    else:
+        ev[0][0].record()
+        for i in range(K):
+            step(i, counter)
+            counter += 1
+        ev[0][1].record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K  # launch duration on the kernel's stream
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K  # mean launch duration on the kernel's stream
     if dist is not None:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
