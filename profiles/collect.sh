@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof
 TAG=${1:-r01}
 shift || true
-ARGS=${@:-"--steps 30 --warmup 5 --cpu-budget 0 --mappo-T 0"}
+ARGS=${@:-"--steps 200 --warmup 20 --cpu-budget 0 --mappo-T 0"}  # the default bench's env leg
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $R/bench.py $ARGS > $OUT/trace_bench.log 2>&1
