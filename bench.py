@@ -366,7 +366,7 @@ def main():
     ap.add_argument("--mappo-workload", default="uf50-218", choices=sorted(WORKLOADS))
     ap.add_argument("--mappo-envs", type=int, default=1024, help="envs per GPU in the MAPPO leg")
     ap.add_argument("--mappo-T", type=int, default=32, help="NUM_STEPS of the MAPPO leg (0: skip the leg)")
-    ap.add_argument("--mappo-micro-gb", type=float, default=160.0, help="activation budget per PPO micro-batch")
+    ap.add_argument("--mappo-micro-gb", type=float, default=240.0, help="activation budget per PPO micro-batch")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -157,7 +157,7 @@ class MAPPOLearner:
         # G4 tapes = 12H, clause rows Hc, GIN, G4 = 7H (bounded by 12H), plus ~24H of transients
         per_sample_train = 4.0 * L * rows * 12 * H + 4.0 * rows * 24 * H
         per_sample_infer = 4.0 * rows * 24 * H
-        budget = micro_bytes if micro_bytes is not None else float(config.get("MICROBATCH_BYTES", 160e9))
+        budget = micro_bytes if micro_bytes is not None else float(config.get("MICROBATCH_BYTES", 240e9))
         cap = max(1, min(self.MB, int(budget // per_sample_train)))
         self.micro = -(-self.MB // -(-self.MB // cap))  # equal micro-batches, none above the budget
         self.chunk = max(1, min(self.B, int(budget // per_sample_infer)))
