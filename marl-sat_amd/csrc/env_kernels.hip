@@ -1,6 +1,6 @@
 // Batched multi-agent SAT environment on gfx950.
 //
-// One workgroup (256 lanes; 64 for small instances, env_threads) owns one environment for the whole call:
+// One workgroup (64 / 256 / 512 lanes by instance size, env_threads) owns one environment for the whole call:
 //   1. assignment -> LDS bit words (one ballot per 64 vars), agents' flips as
 //      LDS atomic XORs;
 //   2. every clause evaluated once from the L2/MALL-resident packed pool
@@ -794,16 +794,18 @@ static int check_pool(const msat_pool *pool) {
 
 // Workgroup size of the single-class env kernel: one wave per env for small instances (more envs
 // resident per CU: the per-env chain of dependent memory round trips, not bandwidth, bounds them),
-// 256 lanes otherwise.  MARLSAT_ENV_THREADS (64 / 128 / 256) overrides.
+// 512 lanes for large ones (A * D >= 16384: uf200), 256 otherwise.  MARLSAT_ENV_THREADS (64 / 128 / 256 / 512) overrides.
 static int env_threads(const EnvParams &p) {
     static const int forced = [] {
         const char *e = getenv("MARLSAT_ENV_THREADS");
         const int v = e ? atoi(e) : 0;
-        return v == 64 || v == 128 || v == 256 ? v : 0;
+        return v == 64 || v == 128 || v == 256 || v == 512 ? v : 0;
     }();
     if (forced) return forced;
-    // uf50 x 4096: 13.4 us at 64 lanes vs 20.0 at 256; uf100 equal; uf200 x 4096: 113 vs 142 us
-    return (long)p.A * p.D <= 4096 ? 64 : 256;
+    // uf50 x 4096: 13.4 us at 64 lanes vs 20.0 at 256; uf100 x 4096: 27.6 us at 256, 34.9 at 512;
+    // uf200 x 4096: 111 us at 512, 113 at 256, 142 at 64
+    const long n = (long)p.A * p.D;
+    return n <= 4096 ? 64 : (n >= 16384 ? 512 : 256);
 }
 
 template <int MODE>
@@ -828,6 +830,8 @@ static int launch_env(const EnvParams &p, const msat_env_desc *d, const msat_poo
         MSAT_ENV_LAUNCH(64)
     } else if (T == 128) {
         MSAT_ENV_LAUNCH(128)
+    } else if (T == 512) {
+        MSAT_ENV_LAUNCH(512)
     } else {
         MSAT_ENV_LAUNCH(256)
     }
