@@ -288,7 +288,8 @@ def env_leg(args, rank, world, dist):
         outs = menv.alloc_outs(states)
         gstep = menv.stepper(states, obs, outs, autoreset=True, seed=seed)
         step = lambda i, c: gstep([a[i % ring] for a in acts], c)
-        kernel = "env_group_kernel<2,int>"
+        glanes = int(os.environ.get("MARLSAT_ENV_GROUP_THREADS", "0")) or (512 if sum(sizes) <= 2048 else 256)
+        kernel = f"env_group_kernel<2,{'int' if obs_dtype == torch.int32 else 'signed char'},{glanes}>"
     else:
         o, st = classes[0].reset_from_pool(pools[0], sizes[0], Key(seed, 0))
         obs, states, outs = [o], [st], [classes[0]._step_out(sizes[0])]

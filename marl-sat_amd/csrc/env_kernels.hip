@@ -505,8 +505,8 @@ struct EnvGroups {
 
 __host__ __device__ __forceinline__ uint64_t group_seed(int g) { return (uint64_t)g * 0x9E3779B97F4A7C15ull; }
 
-template <int MODE, typename ObsT>
-__global__ void __launch_bounds__(kThreads)
+template <int MODE, typename ObsT, int T>
+__global__ void __launch_bounds__(T)
 env_group_kernel(EnvGroups gs, uint64_t seed, uint64_t ctr) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     // Blocks in dispatch order, the classes laid out most expensive first (launch_groups): no XCD-major
@@ -517,7 +517,7 @@ env_group_kernel(EnvGroups gs, uint64_t seed, uint64_t ctr) {
     for (int k = 1; k < MSAT_MAX_GROUPS; ++k)
         if (k < gs.G && gb >= gs.g[k].begin) g = k;
     const EnvGroup &e = gs.g[g];
-    env_run<MODE, ObsT, kThreads>(e.p, e.pool, e.st, e.actions, nullptr, nullptr, nullptr, seed ^ group_seed(e.gid), ctr, e.out,
+    env_run<MODE, ObsT, T>(e.p, e.pool, e.st, e.actions, nullptr, nullptr, nullptr, seed ^ group_seed(e.gid), ctr, e.out,
                         reinterpret_cast<ObsT *>(e.obs), gb - e.begin, smem);
 }
 
@@ -885,10 +885,28 @@ static int launch_groups(int G, const msat_env_desc *descs, const msat_pool *poo
     MSAT_REQUIRE(lds <= 160 * 1024, "env needs %zu B of LDS (> 160 KiB)", lds);
     gs.total = total;
     if (total == 0) return MSAT_OK;
-    if (descs[0].obs_dtype == MSAT_OBS_I32)
-        hipLaunchKernelGGL((env_group_kernel<MODE, int32_t>), dim3(total), dim3(kThreads), lds, s, gs, seed, ctr);
-    else
-        hipLaunchKernelGGL((env_group_kernel<MODE, int8_t>), dim3(total), dim3(kThreads), lds, s, gs, seed, ctr);
+    // workgroup size: 512 lanes for small batches (<= 2048 envs: the launch is bound by one large env's
+    // latency; mixed 1024: 15.7 vs 16.9 us), 256 otherwise (mixed 8192: 91.5-96.9 vs 105.5 us on
+    // 512); MARLSAT_ENV_GROUP_THREADS (256 / 512 / 1024) overrides
+    static const int forced = [] {
+        const char *e = getenv("MARLSAT_ENV_GROUP_THREADS");
+        const int v = e ? atoi(e) : 0;
+        return v == 256 || v == 512 || v == 1024 ? v : 0;
+    }();
+    const int gT = forced ? forced : (total <= 2048 ? 512 : 256);
+#define MSAT_GROUP_LAUNCH(TT)                                                                                      \
+    if (descs[0].obs_dtype == MSAT_OBS_I32)                                                                        \
+        hipLaunchKernelGGL((env_group_kernel<MODE, int32_t, TT>), dim3(total), dim3(TT), lds, s, gs, seed, ctr);   \
+    else                                                                                                           \
+        hipLaunchKernelGGL((env_group_kernel<MODE, int8_t, TT>), dim3(total), dim3(TT), lds, s, gs, seed, ctr);
+    if (gT == 1024) {
+        MSAT_GROUP_LAUNCH(1024)
+    } else if (gT == 512) {
+        MSAT_GROUP_LAUNCH(512)
+    } else {
+        MSAT_GROUP_LAUNCH(256)
+    }
+#undef MSAT_GROUP_LAUNCH
     return check_launch("env_group_kernel");
 }
 
