@@ -963,8 +963,10 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
     }
     // float4 rows of the wave's [16][128] stage -> dst (row stride ld), rows < R only.  LDS-only
     // barriers: the global stores stay in flight (a __syncthreads release fence would drain them)
+    // The stage is wave-private: a wave's LDS operations complete in issue order, so waiting for its
+    // own stage writes (lgkmcnt) is the only ordering needed -- no workgroup barrier.
     auto flush = [&](float *dst, int ld) {
-        barrier_lds();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
             const int rr = 2 * it + (lane >> 5), c4 = lane & 31;
@@ -972,7 +974,7 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
             const int row = row0 + wr + rr;
             if (row < a.R) *reinterpret_cast<float4 *>(dst + (size_t)row * ld + 4 * c4) = v;
         }
-        barrier_lds();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
     if (tape) {
 #if MSAT_GRU_TAPE_DIRECT
