@@ -493,11 +493,33 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
         else wait_vmcnt<0>();
         barrier_lds();
     }
-    // C/D map: col = lane & 15, row = 4 (lane >> 4) + reg
+    // C/D map: col = lane & 15, row = 4 (lane >> 4) + reg.  The stage is wave-private (32 rows x 64
+    // columns per wave).
     float *stage = reinterpret_cast<float *>(&lds_w[0][0][0]) + w * 32 * 64;
     if (vec_out) {
+        // (the main loop's last barrier already ordered every wave's weight reads before the stage)
+        // accumulating calls order only the wave's own LDS operations (a workgroup barrier's release
+        // fence would drain the stores issued so far, and with them the next rows' old-C loads);
+        // overwriting calls measured faster with the barrier (275 vs 290 us, var dh)
+        auto stage_sync = [&] {
+            if (accumulate) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            else __syncthreads();
+        };
 #pragma unroll
-        for (int i0 = 0; i0 < RT; i0 += 2)  // 32 rows at a time
+        for (int i0 = 0; i0 < RT; i0 += 2) {  // 32 rows at a time
+            // accumulate: the old C values of these 32 rows are all loaded before any of their stores
+            // (a load issued after a store waits for it: vector-memory counts retire in issue order)
+            float4 o[2][8];
+#pragma unroll
+            for (int hc = 0; hc < 2; ++hc) {
+                const int col = n0 + 64 * hc + l16 * 4;
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int row = m0 + wr + 16 * i0 + it * 4 + g;
+                    if (accumulate && row < M && col < N)
+                        o[hc][it] = *reinterpret_cast<const float4 *>(C + (size_t)row * ldc + col);
+                }
+            }
 #pragma unroll
             for (int hc = 0; hc < 2; ++hc) {  // columns 64 hc .. 64 hc + 63
 #pragma unroll
@@ -507,7 +529,7 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
 #pragma unroll
                         for (int reg = 0; reg < 4; ++reg)
                             stage[(16 * i + 4 * g + reg) * 64 + 16 * jj + l16] = acc[i0 + i][4 * hc + jj][reg];
-                __syncthreads();
+                stage_sync();
                 const int col = n0 + 64 * hc + l16 * 4;
                 float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (bias && col < N) bv = *reinterpret_cast<const float4 *>(bias + col);
@@ -517,17 +539,15 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
                     const int row = m0 + wr + 16 * i0 + rr;
                     float4 v = *reinterpret_cast<const float4 *>(stage + rr * 64 + l16 * 4);
                     v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-                    if (row < M && col < N) {
-                        float4 *c = reinterpret_cast<float4 *>(C + (size_t)row * ldc + col);
-                        if (accumulate) {
-                            const float4 o = *c;
-                            v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
-                        }
-                        *c = v;
+                    if (accumulate) {
+                        const float4 &ov = o[hc][it];
+                        v.x = ov.x + v.x; v.y = ov.y + v.y; v.z = ov.z + v.z; v.w = ov.w + v.w;
                     }
+                    if (row < M && col < N) *reinterpret_cast<float4 *>(C + (size_t)row * ldc + col) = v;
                 }
-                __syncthreads();
+                stage_sync();
             }
+        }
         return;
     }
 #pragma unroll

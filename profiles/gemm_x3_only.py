@@ -14,7 +14,8 @@ for M, N, K, what in [(Nv, H, 3 * H, "var dh"), (Nc, H, 3 * H, "clause dh"), (Nc
     A = torch.randn(M, K, device="cuda"); B = torch.randn(N, K, device="cuda"); C = torch.randn(M, N, device="cuda")
     planes = torch.empty(3 * N * K, dtype=torch.int16, device="cuda")
     L.msat_split_bf16x3(B.data_ptr(), N, K, K, planes.data_ptr(), s)
-    f = lambda: L.msat_gemm_x3(A.data_ptr(), K, planes.data_ptr(), C.data_ptr(), N, 0, M, N, K, 0, s)
+    acc = int(os.environ.get("GEMM_ACC", "0"))  # 1: C += A @ W^T (the backward's accumulating products)
+    f = lambda: L.msat_gemm_x3(A.data_ptr(), K, planes.data_ptr(), C.data_ptr(), N, 0, M, N, K, acc, s)
     f(); torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
