@@ -1,8 +1,9 @@
 """GRU + LayerNorm backward from the tape (msat_gru_ln_bwd_g4f, packed rows, dh assigned, gate-bias and
 feature partials) on the uf50 training shapes, HIP-event timed, with its HBM rate.
 usage: gru_bwd_only.py [reps]
-Measured: var 507 us (4.5 TB/s), clause 1067 us (5.5 TB/s); more blocks, or two rows per wave with
-all loads first (3 / 2 waves per SIMD instead of 5 / 4), measured slower."""
+Measured: var 507 us (4.5 TB/s), clause 1067 us (5.5 TB/s); more blocks, two rows per wave with
+all loads first (3 / 2 waves per SIMD instead of 5 / 4), or the next row's loads issued before this
+row's stores (4 / 3 waves per SIMD: 567 / 1249 vs 526 / 1141 us) measured slower."""
 import json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "marl-sat_amd")]
