@@ -20,9 +20,16 @@ Hp, Hn = torch.randn(Nv, H, device="cuda", generator=g), torch.randn(Nv, H, devi
 base = torch.randint(0, Nv - 64, (Nc, 1), device="cuda", generator=g)
 slots = ((base + torch.randint(0, 64, (Nc, 3), device="cuda", generator=g)) << 1 |
          torch.randint(0, 2, (Nc, 3), device="cuda", generator=g)).int().contiguous()
-out = torch.empty(Nc, 2 * H, device="cuda")
-f = lambda: L.msat_clause_gather2(Hp.data_ptr(), Hn.data_ptr(), H, slots.data_ptr(), out.data_ptr(), 2 * H, Nc, H,
-                                  0, 0, s)
+bwd = os.environ.get("GATHER_MODE") == "bwd"  # the backward's merged, accumulating form (dH_c += ...)
+if bwd:
+    Hp = torch.randn(Nv, 2 * H, device="cuda", generator=g)
+    out = torch.zeros(Nc, H, device="cuda")
+    f = lambda: L.msat_clause_gather2(Hp.data_ptr(), Hp.data_ptr() + 4 * H, 2 * H, slots.data_ptr(), out.data_ptr(),
+                                      H, Nc, H, 1, 1, s)
+else:
+    out = torch.empty(Nc, 2 * H, device="cuda")
+    f = lambda: L.msat_clause_gather2(Hp.data_ptr(), Hn.data_ptr(), H, slots.data_ptr(), out.data_ptr(), 2 * H, Nc,
+                                      H, 0, 0, s)
 assert f() == 0
 torch.cuda.synchronize()
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -31,6 +38,7 @@ for _ in range(reps):
     f()
 b.record(); torch.cuda.synchronize()
 us = a.elapsed_time(b) / reps * 1e3
-nbytes = Nc * (12 + 3 * 4 * H + 8 * H)  # slots, 3 source rows of H floats read, one 2H row written
-print(json.dumps({"what": "clause_gather2", "Nc": Nc, "us": round(us, 1), "GBps": round(nbytes / us / 1e3, 1),
+# slots, 3 source rows of H floats read, one output row written (bwd: H wide, read and written)
+nbytes = Nc * (12 + 3 * 4 * H + (8 * H if bwd else 8 * H))
+print(json.dumps({"what": "clause_gather2" + (" bwd" if bwd else ""), "Nc": Nc, "us": round(us, 1), "GBps": round(nbytes / us / 1e3, 1),
                   "checksum": float(out.double().sum())}))
