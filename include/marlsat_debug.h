@@ -11,6 +11,11 @@ extern "C" {
 int msat_debug_fill(void *dst, size_t bytes, int32_t value, int32_t nontemporal, int32_t grid, void *stream);
 /* Same bytes, but block g writes one contiguous chunk [g*bytes/grid, (g+1)*bytes/grid). */
 int msat_debug_fill_chunked(void *dst, size_t bytes, int32_t value, int32_t nontemporal, int32_t grid, void *stream);
+/* Expand compact bit images into int32 obs [E][A][D] (D % 4 == 0): element (e, a, d) is
+ * bit d of vimg[e] if bit d of mimg[inst[e]][a] is set, else -1 (two-phase env-step probe).
+ * grid > 0: one lane per 16 B quad, grid-stride; grid < 0: -grid blocks, one wave per row. */
+int msat_debug_obs_expand(void *dst, int32_t E, int32_t A, int32_t D, const int32_t *inst, const uint32_t *vimg,
+                          const uint32_t *mimg, int32_t grid, void *stream);
 #ifdef __cplusplus
 }
 #endif

@@ -29,7 +29,76 @@ __global__ void __launch_bounds__(256) fill_chunk_kernel(int4 *__restrict__ dst,
             *reinterpret_cast<v4i *>(dst + i) = v;
     }
 }
+// pattern 2: obs expansion from compact bit images (two-phase env-step prototype).
+// Quad q covers obs elements 4q..4q+3 of the flat [E][A][D] array (D % 4 == 0, so a quad
+// stays in one row and one 32-bit image word). vimg[e][Dw]: bit d = value of element d;
+// mimg[inst][a][Dw]: bit d = element visible to agent a (else -1).
+__global__ void __launch_bounds__(256) obs_expand_kernel(int4 *__restrict__ dst, uint32_t nq, uint32_t D,
+                                                         uint32_t A, uint32_t Dw, const int *__restrict__ inst,
+                                                         const uint32_t *__restrict__ vimg,
+                                                         const uint32_t *__restrict__ mimg) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < nq; q += gridDim.x * 256) {
+        const uint32_t i = q * 4, row = i / D, d = i - row * D, e = row / A, a = row - e * A;
+        const uint32_t w = d >> 5, sh = d & 31;
+        const uint32_t vb = vimg[(size_t)e * Dw + w] >> sh;
+        const uint32_t mb = mimg[((size_t)inst[e] * A + a) * Dw + w] >> sh;
+        v4i o;
+        o.x = (mb & 1) ? (int)(vb & 1) : -1;
+        o.y = (mb & 2) ? (int)((vb >> 1) & 1) : -1;
+        o.z = (mb & 4) ? (int)((vb >> 2) & 1) : -1;
+        o.w = (mb & 8) ? (int)((vb >> 3) & 1) : -1;
+        *reinterpret_cast<v4i *>(dst + q) = o;
+    }
+}
+// Same expansion, one wave per obs row (e, a): the row's image words sit one per lane
+// (Dw <= 64) and each quad takes its word by lane shuffle, so the loop is stores only.
+__global__ void __launch_bounds__(256) obs_expand_rows_kernel(int4 *__restrict__ dst, uint32_t rows, uint32_t D,
+                                                              uint32_t A, uint32_t Dw,
+                                                              const int *__restrict__ inst,
+                                                              const uint32_t *__restrict__ vimg,
+                                                              const uint32_t *__restrict__ mimg) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const uint32_t lane = threadIdx.x & 63, nq = D / 4, nw = gridDim.x * 4;
+    for (uint32_t r = (blockIdx.x * 256 + threadIdx.x) >> 6; r < rows; r += nw) {
+        const uint32_t e = r / A, a = r - e * A;
+        uint32_t vw = 0, mw = 0;
+        if (lane < Dw) {
+            vw = vimg[(size_t)e * Dw + lane];
+            mw = mimg[((size_t)inst[e] * A + a) * Dw + lane];
+        }
+        int4 *o = dst + (size_t)r * nq;
+        for (uint32_t q = lane; q < nq; q += 64) {
+            const uint32_t d = q * 4, w = d >> 5, sh = d & 31;
+            const uint32_t vb = (uint32_t)__shfl((int)vw, (int)w) >> sh, mb = (uint32_t)__shfl((int)mw, (int)w) >> sh;
+            v4i v;
+            v.x = (mb & 1) ? (int)(vb & 1) : -1;
+            v.y = (mb & 2) ? (int)((vb >> 1) & 1) : -1;
+            v.z = (mb & 4) ? (int)((vb >> 2) & 1) : -1;
+            v.w = (mb & 8) ? (int)((vb >> 3) & 1) : -1;
+            *reinterpret_cast<v4i *>(o + q) = v;
+        }
+    }
+}
 }  // namespace msat
+
+extern "C" int msat_debug_obs_expand(void *dst, int32_t E, int32_t A, int32_t D, const int32_t *inst,
+                                     const uint32_t *vimg, const uint32_t *mimg, int32_t grid, void *stream) {
+    MSAT_REQUIRE(dst && inst && vimg && mimg && E > 0 && A > 0 && D > 0 && D % 4 == 0 && grid != 0,
+                 "bad expand args");
+    const uint64_t nq = (uint64_t)E * A * D / 4;
+    MSAT_REQUIRE(nq * 4 < (1ull << 32), "expand: too many elements");
+    if (grid < 0) {  // one wave per row
+        MSAT_REQUIRE((D + 31) / 32 <= 64, "expand rows: D too large");
+        hipLaunchKernelGGL(msat::obs_expand_rows_kernel, dim3(-grid), dim3(256), 0, (hipStream_t)stream,
+                           (int4 *)dst, (uint32_t)(E * A), (uint32_t)D, (uint32_t)A, (uint32_t)((D + 31) / 32),
+                           inst, vimg, mimg);
+        return msat::check_launch("obs_expand_rows_kernel");
+    }
+    hipLaunchKernelGGL(msat::obs_expand_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (int4 *)dst,
+                       (uint32_t)nq, (uint32_t)D, (uint32_t)A, (uint32_t)((D + 31) / 32), inst, vimg, mimg);
+    return msat::check_launch("obs_expand_kernel");
+}
 
 extern "C" int msat_debug_fill_chunked(void *dst, size_t bytes, int32_t value, int32_t nontemporal, int32_t grid,
                                        void *stream) {

@@ -150,6 +150,7 @@ def _load():
     sig["msat_standardize"] = (I, [P, Z, F, F, P])
     sig["msat_debug_fill"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])  # marlsat_debug.h
     sig["msat_debug_fill_chunked"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])
+    sig["msat_debug_obs_expand"] = (c_int32, [P, c_int32, c_int32, c_int32, P, P, P, c_int32, P])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
@@ -203,6 +204,7 @@ EXPORTED = (
     "msat_gemm_wgrad",
     "msat_debug_fill",
     "msat_debug_fill_chunked",
+    "msat_debug_obs_expand",
     "msat_last_error",
     "msat_version",
     "msat_pool_pack",
