@@ -517,6 +517,9 @@ constexpr int kXR = 128;  // rows per workgroup (x3 kernel)
 // x3r kernel: 1 = tape stored straight from the accumulators (measured 0-4 % faster), 0 = float4
 // rows staged through LDS
 // x3r kernel: 1 = activations loaded two steps ahead by asm, split among the previous step's MFMAs
+#ifndef MSAT_GRU_X3R_BPIPE
+#define MSAT_GRU_X3R_BPIPE 1
+#endif
 #ifndef MSAT_GRU_X3R_PIPE
 #define MSAT_GRU_X3R_PIPE 1
 #endif
@@ -875,6 +878,35 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
         const int buf = P;
         if (st + 1 < ns) issueW(st + 1, buf ^ 1);
         if (st + 2 < ns) aload(st + 2, ras[P]);
+#if MSAT_GRU_X3R_BPIPE
+        // weight fragments carried across the 24 (gate, column tile) blocks: each plane is re-read
+        // for the next block as soon as its last MFMA here has issued (w3 after the 1st, w2 after
+        // the 3rd, w1 after the 6th), so the reads fly under the MFMAs instead of each block
+        // waiting for its own three reads.  Term order a1w3, a2w2, a1w2, a3w1, a2w1, a1w1.
+        auto bfrag = [&](int n, int q) {
+            const int gt = n >> 3, j = n & 7;
+            return __builtin_bit_cast(bf16x8, Bs[buf][q * 3 + gt][(16 * j + l16) * 4 + slot]);
+        };
+        bf16x8 b0 = bfrag(0, 0), b1 = bfrag(0, 1), b2 = bfrag(0, 2);
+#pragma unroll
+        for (int n = 0; n < 24; ++n) {
+            const int gt = n >> 3, j = n & 7;
+            const int G = gt < 2 ? gt : (hid ? 3 : 2);
+            f32x4g c = acc[G][j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][0], b2, c, 0, 0, 0);
+            if (n + 1 < 24) b2 = bfrag(n + 1, 2);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][1], b1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][0], b1, c, 0, 0, 0);
+            if (n + 1 < 24) b1 = bfrag(n + 1, 1);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][2], b0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][1], b0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fas[P][0], b0, c, 0, 0, 0);
+            if (n + 1 < 24) b0 = bfrag(n + 1, 0);
+            acc[G][j] = c;
+            if (n == 7) asplit(st + 1, ras[P ^ 1], fas[P ^ 1]);
+            __builtin_amdgcn_sched_barrier(0);  // keep the blocks in order (the reads lead by one)
+        }
+#else
 #pragma unroll
         for (int gt = 0; gt < 3; ++gt) {
             const int G = gt < 2 ? gt : (hid ? 3 : 2);
@@ -896,6 +928,7 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
             // among the MFMAs; unconditional (after the last step it splits stale registers, unused)
             if (gt == 0) asplit(st + 1, ras[P ^ 1], fas[P ^ 1]);
         }
+#endif
         await0(ras[P]);
         barrier_lds();
     };
