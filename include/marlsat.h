@@ -138,7 +138,9 @@ int msat_env_reset(const msat_env_desc *desc, const msat_pool *pool,
                    uint64_t seed, uint64_t rng_counter, void *obs, void *stream);
 
 /* One batched SATEnv.step_env.  actions: (B,A) int32 (mode 0) or (B,A,M) int32
- * (mode 1).  autoreset=0: pure step_env (state/obs are the stepped ones).
+ * (mode 1, values 0/1: MultiDiscrete([2]*m); the state keeps one bit per variable, so bit 0
+ * is applied — the reference's integer XOR with other values (env:246-250) leaves non-binary
+ * assignments, and the Python facade rejects such actions before the call).  autoreset=0: pure step_env (state/obs are the stepped ones).
  * autoreset=1: the rollout's auto-reset — envs whose step is done are reset
  * (problem index / assignment from the explicit arrays or the RNG, exactly as
  * msat_env_reset) and state/obs hold the post-reset values, while `out` holds

@@ -7,6 +7,7 @@
 #include <stdio.h>
 
 #include "marlsat.h"
+#include "marlsat_net.h"  // every extern "C" definition is checked against its declaration
 
 namespace msat {
 

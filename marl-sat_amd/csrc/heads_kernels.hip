@@ -275,7 +275,9 @@ sample_kernel(const float *__restrict__ logits, int R, int W, int greedy, uint64
         }
         if (lane == 0) {
             action[r] = bi;
-            logp[r] = lg[bi] - lse;
+            // a row with no finite logit (mode-1 padded variable slot) stores log-prob 0: distrax gives
+            // NaN there (-inf - logsumexp(-inf)), which would poison the PPO ratio
+            logp[r] = mx > -INFINITY ? lg[bi] - lse : 0.f;
         }
     }
 }
@@ -375,12 +377,13 @@ ppo_loss_multi_kernel(const float *__restrict__ logits, int R, int A, int M, int
     float lp_new = 0.f, lp_old = 0.f, hsum = 0.f;
     for (int j = 0; j < M; ++j) {
         const float *lg = logits + ((size_t)r * M + j) * 2;
-        lp_old += old_logp[(size_t)r * M + j];
         if (j >= n) {
-            // all -inf: distrax log_prob = -inf - logsumexp(-inf) = nan in JAX; padded slots are never
-            // sampled with a finite probability, callers store 0 there and we treat them as 0.
+            // padded slot, both logits -inf: distrax log_prob / entropy are NaN there in JAX, which
+            // would turn the joint ratio and every gradient into NaN.  The slot contributes 0 to the
+            // joint log-probs (new and old, whatever the caller stored) and to the entropy.
             continue;
         }
+        lp_old += old_logp[(size_t)r * M + j];
         const float m = fmaxf(lg[0], lg[1]);
         const float lse = m + __logf(__expf(lg[0] - m) + __expf(lg[1] - m));
         const int a = action[(size_t)r * M + j] & 1;

@@ -148,9 +148,6 @@ def _load():
     sig["msat_adam"] = (I, [P, P, P, P, Z, F, F, F, F, I, F, P])
     sig["msat_moments"] = (I, [P, Z, P, P, P])
     sig["msat_standardize"] = (I, [P, Z, F, F, P])
-    sig["msat_debug_fill"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])  # marlsat_debug.h
-    sig["msat_debug_fill_chunked"] = (c_int32, [P, c_size_t, c_int32, c_int32, c_int32, P])
-    sig["msat_debug_obs_expand"] = (c_int32, [P, c_int32, c_int32, c_int32, P, P, P, c_int32, P])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
@@ -159,6 +156,23 @@ def _load():
 
 
 lib = _load()
+
+_debug = None
+
+
+def debug_lib():
+    """libmarlsat_debug.so: diagnostic entry points (csrc/marlsat_debug.h) for profiles/*.py only."""
+    global _debug
+    if _debug is None:
+        d = ctypes.CDLL(os.path.join(os.path.dirname(LIB_PATH), "libmarlsat_debug.so"))
+        P = c_void_p
+        for name, args in (("msat_debug_fill", [P, c_size_t, c_int32, c_int32, c_int32, P]),
+                           ("msat_debug_fill_chunked", [P, c_size_t, c_int32, c_int32, c_int32, P]),
+                           ("msat_debug_obs_expand", [P, c_int32, c_int32, c_int32, P, P, P, c_int32, P])):
+            fn = getattr(d, name)
+            fn.restype, fn.argtypes = c_int32, args
+        _debug = d
+    return _debug
 
 # Every symbol include/marlsat*.h declares (checked by tests/test_capi.py).
 EXPORTED = (
@@ -202,9 +216,6 @@ EXPORTED = (
     "msat_gemm",
     "msat_gemm_wgrad_workspace_bytes",
     "msat_gemm_wgrad",
-    "msat_debug_fill",
-    "msat_debug_fill_chunked",
-    "msat_debug_obs_expand",
     "msat_last_error",
     "msat_version",
     "msat_pool_pack",

@@ -294,6 +294,16 @@ class SATEnv:
             raise ValueError(f"actions must have shape {want}, got {tuple(a.shape)}")
         return a
 
+    def _refuse_nonbinary(self, actions, B: int) -> torch.Tensor:
+        """env:246-250 XORs the raw integer: a mode-1 action of 2 or -1 leaves a non-binary assignment
+        (both polarities false in the clause scan).  MultiDiscrete([2]*m) never samples one, and the device
+        state keeps one bit per variable, so the reference-API entry points refuse such actions (one
+        device reduction + sync; the raw ``step_raw`` / ``stepper`` paths apply bit 0 unchecked)."""
+        a = self._actions_tensor(actions, B)
+        if self.action_mode == 1 and a.numel() and bool(((a != 0) & (a != 1)).any()):
+            raise ValueError("action_mode 1 actions must be 0 or 1 (MultiDiscrete([2] * max_vars_per_agent))")
+        return a
+
     # ------------------------------------------------------------ reset ----
     def reset_from_pool(self, pool: ProblemPool, num_envs: int, key=None, *, problem_idx=None, assignments=None,
                         state: Optional[SATState] = None, reset_mask=None, obs: Optional[torch.Tensor] = None,
@@ -398,6 +408,7 @@ class SATEnv:
 
     def step_env(self, key, state: SATState, actions, *, inplace: bool = False):
         """env:225-284 -> (obs, next_state, rewards, dones, infos). Functional unless ``inplace``."""
+        actions = self._refuse_nonbinary(actions, state.num_envs)
         nxt = state if inplace else state.clone()
         obs, out = self.step_raw(nxt, actions, autoreset=False, key=key)
         done = out["done"].bool()
@@ -411,6 +422,7 @@ class SATEnv:
     def step(self, key, state: SATState, actions, *, inplace: bool = False, problem_idx=None, assignments=None):
         """jaxmarl ``MultiAgentEnv.step``: step_env + auto-reset of done envs onto random pool rows."""
         nxt = state if inplace else state.clone()
+        actions = self._refuse_nonbinary(actions, state.num_envs)
         obs, out = self.step_raw(nxt, actions, autoreset=True, key=key, problem_idx=problem_idx,
                                  assignments=assignments)
         done = out["done"].bool()

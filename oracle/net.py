@@ -203,7 +203,11 @@ def ppo_loss(P, L, batch, cfg, agent_vars, action_mask, action_mode=0, ent_coef=
     if action_mode == 0:
         ratio = torch.exp(lp - batch["log_prob"])
     else:
-        ratio = torch.exp(lp.sum(-1) - batch["log_prob"].sum(-1))
+        # padded variable slots (both logits -inf) give NaN log-probs / entropy in distrax, which turns
+        # the reference's joint ratio into NaN; the build counts them as 0, so does this
+        valid = action_mask[None].expand_as(lp)
+        zero = torch.zeros((), dtype=lp.dtype)
+        ratio = torch.exp(torch.where(valid, lp, zero).sum(-1) - torch.where(valid, batch["log_prob"], zero).sum(-1))
     eps = cfg["CLIP_EPS"]
     loss_actor = -torch.minimum(ratio * gae, torch.clamp(ratio, 1.0 - eps, 1.0 + eps) * gae).mean()
     ent = entropy(logits).mean()

@@ -97,3 +97,22 @@ def test_product_path_does_not_import_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f
+
+
+def test_ctypes_argtypes_match_header_prototypes():
+    """Every ctypes binding in marlsat/_lib.py passes as many arguments as its include/*.h prototype
+    declares (the compiler checks the prototypes against the extern "C" definitions: csrc/common.h
+    includes both headers)."""
+    import glob
+
+    from marlsat import _lib
+
+    text = "".join(open(f).read() for f in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    protos = dict(re.findall(r"\b(msat_[a-z_0-9]+)\s*\(([^)]*)\)\s*;", text))
+    assert sorted(protos) == _header_symbols()
+    for name, params in protos.items():
+        params = params.strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        argtypes = getattr(_lib.lib, name).argtypes
+        assert argtypes is not None and len(argtypes) == n, (name, n, argtypes)

@@ -192,6 +192,28 @@ def test_negative_and_out_of_range_actions():
     _check_state(env, st, ost)
 
 
+def test_mode1_actions_outside_0_1_are_refused():
+    """env:246-250 XORs the raw action integer, so 2 or -1 would leave a non-binary assignment
+    (tests/test_oracle.py pins that behaviour on the oracle).  The facade refuses such actions;
+    {0, 1} (everything MultiDiscrete([2]*m) samples) match the oracle bit-exact."""
+    env, ora = _mk(23, 97, 10, action_mode=1)  # 3 agents of 8, 8, 7 vars: one padded slot
+    pool = _pool(23, 97, 2)
+    x = np.random.default_rng(8).integers(0, 2, (2, 23)).astype(np.uint8)
+    obs, st = env.reset(pool, assignments=x)
+    _, ost = ora.reset(pool, x.astype(np.int32))
+    A, M = env.num_agents, env.max_vars_per_agent
+    for bad in (2, -1):
+        a = np.zeros((2, A, M), np.int32)
+        a[1, 0, 3] = bad
+        with pytest.raises(ValueError, match="must be 0 or 1"):
+            env.step_env(None, st, torch.from_numpy(a).cuda())
+    a = np.random.default_rng(9).integers(0, 2, (2, A, M)).astype(np.int32)
+    obs2, st2, rewards, dones, infos = env.step_env(None, st, torch.from_numpy(a).cuda())
+    oobs, ost2, r, d, _ = ora.step(ost, a)
+    np.testing.assert_array_equal(_np(obs2.tensor), oobs)
+    _check_state(env, st2, ost2, "mode 1 {0,1}")
+
+
 def test_rng_reset_replays_on_host():
     from marlsat.random import Key
 

@@ -99,6 +99,19 @@ def test_oracle_flip_decode_edge_cases():
     assert env.decode_flips(x, np.array([[-1, -1]])).tolist() == [[0, 0, 1, 0, 0]]
 
 
+def test_oracle_mode1_integer_xor_semantics():
+    """env:246-250: mode 1 XORs the raw action integer into the int32 assignment; env:135-144: a
+    literal is true only for x == 1 (positive) or x == 0 (negative).  An action of 2 or -1 therefore
+    leaves a value for which both polarities are false (the device facade refuses such actions)."""
+    env = OracleSATEnv(4, 2, max_steps=10, vars_per_agent=2, action_mode=1)  # agents [0,1], [2,3]
+    x = np.array([[0, 1, 1, 0]], np.int32)
+    new = env.decode_flips(x, np.array([[[2, 1], [-1, 0]]]))
+    assert new.tolist() == [[2, 0, -2, 0]]
+    cl = np.array([[[1, -1, 3], [-3, 2, 4]]], np.int32)
+    status, nun = OracleSATEnv.satisfaction(new, cl)
+    assert status.tolist() == [[False, False]] and nun.tolist() == [2]
+
+
 def test_oracle_pbrs_reward():
     env = OracleSATEnv(6, 4, max_steps=5, vars_per_agent=3, reward_mode=1, r_clause=0.25, r_sat=2.0, gamma=0.5)
     cl = np.array([[[1, -2, 3], [-1, 4, 5], [-4, -5, -6], [2, 6, -3]]], np.int32)
