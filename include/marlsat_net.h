@@ -24,6 +24,14 @@ int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ldb, int32_t 
               int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, int32_t accumulate,
               void *stream);
 
+/* C[M,N] (+)= op(A)[M,K] @ op(B)[K,N], fp32 operands, fp64 accumulation, one rounding per
+ * element; op(A) = A[M,K] (transA=0) or A[K,M]^T, op(B) = B[K,N] (transB=0) or B[N,K]^T.
+ * For the small folded-weight products of the phi folding (F = W Wi per forward, dW = dF Wi^T and
+ * dWi = W^T dF per backward) that stand in for the reference's separate Dense layers
+ * (src/learners/mappo_gnn_sat_learner.py:66-79). */
+int msat_gemm_f64acc(const float *A, int32_t lda, int32_t transA, const float *B, int32_t ldb, int32_t transB,
+                     float *C, int32_t ldc, int32_t M, int32_t N, int32_t K, int32_t accumulate, void *stream);
+
 /* fp32 GEMM on the bf16 matrix cores (gemm_x3.hip): operands split exactly into three bf16
  * parts, six bf16 MFMAs per 16-deep k step keep every product term above fp32 rounding.
  * msat_split_bf16x3: planes (3 x rows x cols bf16, contiguous) of W (rows x cols, ldw).

@@ -396,6 +396,38 @@ static bool legacy_gemm() {
     return e && e[0] == '1';
 }
 
+// Small fp32 products accumulated in fp64 and rounded once (gnn.py phi folding: F = W Wi and its
+// unfolding dW = dF Wi^T, dWi = W^T dF).  F multiplies every row of every message step, so a
+// plain fp32 GEMM's rounding of F is a systematic weight perturbation that the 16 GRU + LayerNorm
+// steps accumulate coherently (critic values ~4x the reference order's error at L = 16,
+// tests/probe_value_error.py); rounded once from fp64, F is as accurate as the weights themselves.
+// One thread per output element; the operands are at most a few hundred rows (microseconds).
+__global__ void __launch_bounds__(256)
+gemm_f64acc_kernel(const float *__restrict__ A, int lda, int transA, const float *__restrict__ B, int ldb, int transB,
+                   float *__restrict__ C, int ldc, int M, int N, int K, int accumulate) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x, m = blockIdx.y;
+    if (n >= N) return;
+    double acc = accumulate ? (double)C[(size_t)m * ldc + n] : 0.0;
+    for (int k = 0; k < K; ++k) {
+        const double a = transA ? A[(size_t)k * lda + m] : A[(size_t)m * lda + k];
+        const double b = transB ? B[(size_t)n * ldb + k] : B[(size_t)k * ldb + n];
+        acc = fma(a, b, acc);
+    }
+    C[(size_t)m * ldc + n] = (float)acc;
+}
+
+extern "C" int msat_gemm_f64acc(const float *A, int32_t lda, int32_t transA, const float *B, int32_t ldb,
+                                int32_t transB, float *C, int32_t ldc, int32_t M, int32_t N, int32_t K,
+                                int32_t accumulate, void *stream) {
+    MSAT_REQUIRE(A && B && C, "NULL operand");
+    MSAT_REQUIRE(M >= 0 && M <= 65535 && N >= 1 && K >= 0, "bad dims M=%d N=%d K=%d", M, N, K);
+    MSAT_REQUIRE(lda >= (transA ? M : K) && ldb >= (transB ? K : N) && ldc >= N, "leading dims too small");
+    if (M == 0) return MSAT_OK;
+    hipLaunchKernelGGL(gemm_f64acc_kernel, dim3((N + 255) / 256, M), dim3(256), 0, (hipStream_t)stream, A, lda,
+                       transA, B, ldb, transB, C, ldc, M, N, K, accumulate);
+    return check_launch("gemm_f64acc_kernel");
+}
+
 extern "C" int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ldb, int32_t transB, float *C,
                          int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, int32_t accumulate,
                          void *stream) {

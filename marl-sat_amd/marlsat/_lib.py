@@ -145,6 +145,7 @@ def _load():
     sig["msat_split_dlogits"] = (I, [P, I, I, P, P, P])
     sig["msat_sample_actions"] = (I, [P, I, I, I, U, U, P, P, P])
     sig["msat_ppo_loss"] = (I, [P, I, I, I, I, I, I, P, P, P, P, P, P, F, F, F, F, I, P, P, P, P, P])
+    sig["msat_gemm_f64acc"] = (I, [P, I, I, P, I, I, P, I, I, I, I, I, P])
     sig["msat_adam"] = (I, [P, P, P, P, Z, F, F, F, F, I, F, P])
     sig["msat_moments"] = (I, [P, Z, P, P, P])
     sig["msat_standardize"] = (I, [P, Z, F, F, P])
@@ -214,6 +215,7 @@ EXPORTED = (
     "msat_ppo_loss",
     "msat_adam",
     "msat_gemm",
+    "msat_gemm_f64acc",
     "msat_gemm_wgrad_workspace_bytes",
     "msat_gemm_wgrad",
     "msat_last_error",

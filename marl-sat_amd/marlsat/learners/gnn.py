@@ -129,6 +129,18 @@ class GNNActorCritic:
         GNNActorCritic.flops += 2 * M * N * K
         _chk(L_.msat_gemm(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, self.stream), "msat_gemm")
 
+    def _gemm64(self, A, lda, transA, B, ldb, transB, C, ldc, M, N, K, acc=0):
+        """fp64-accumulated small product, one rounding per element (the folded weights, gemm.hip)."""
+        mode = os.environ.get("MARLSAT_FOLD_F64", "1")
+        if mode == "0" or mode == ("bwd" if transA or transB else "fwd"):  # A/B: plain fp32 GEMMs (pre-r02)
+            if transA:
+                self._wgrad(A, lda, B, ldb, C, ldc, K, M, N, acc)
+            else:
+                self._gemm(A, lda, B, ldb, transB, C, ldc, None, M, N, K, acc)
+            return
+        _chk(L_.msat_gemm_f64acc(A, lda, transA, B, ldb, transB, C, ldc, M, N, K, acc, self.stream),
+             "msat_gemm_f64acc")
+
     # fp32-accurate bf16x3 split GEMM for the backward's C (+)= dG @ W^T products (gemm_x3.hip)
     use_x3 = os.environ.get("MARLSAT_GEMM_X3", "1") != "0"
 
@@ -309,16 +321,18 @@ class GNNActorCritic:
         (Fc, Fp, Fn), _ = self._fold_views()
         W3 = 3 * H
         wic = self.p("enc.gru_c_wi")
+        # F multiplies every row of every step: computed in fp64 and rounded once (a plain fp32 product's
+        # rounding is a systematic weight error that 16 GRU + LayerNorm steps accumulate coherently)
         for half, nm in ((0, "phi_cp"), (1, "phi_cn")):
             B = pp(wic[half * H])
-            self._gemm(self.p(f"enc.{nm}_w").data_ptr(), H, B, W3, 0, pp(Fc[half * H]), W3, None, H, W3, H)
-            self._gemm(self.p(f"enc.{nm}_b").data_ptr(), H, B, W3, 0, pp(Fc[2 * H + half]), W3, None, 1, W3, H)
+            self._gemm64(self.p(f"enc.{nm}_w").data_ptr(), H, 0, B, W3, 0, pp(Fc[half * H]), W3, H, W3, H)
+            self._gemm64(self.p(f"enc.{nm}_b").data_ptr(), H, 0, B, W3, 0, pp(Fc[2 * H + half]), W3, 1, W3, H)
         wv, bv = self.p("enc.phi_v_w"), self.p("enc.phi_v_b")
         for half, cell, F in ((0, "gru_vp", Fp), (1, "gru_vn", Fn)):
             wi = self.p(f"enc.{cell}_wi")
-            self._gemm(pp(wv, half * H), 2 * H, wi.data_ptr(), W3, 0, F.data_ptr(), W3, None, H, W3, H)
+            self._gemm64(pp(wv, half * H), 2 * H, 0, wi.data_ptr(), W3, 0, F.data_ptr(), W3, H, W3, H)
             F[H:H + 4].copy_(wi[H:H + 4])
-            self._gemm(pp(bv, half * H), H, wi.data_ptr(), W3, 0, pp(F[H + 4 + half]), W3, None, 1, W3, H)
+            self._gemm64(pp(bv, half * H), H, 0, wi.data_ptr(), W3, 0, pp(F[H + 4 + half]), W3, 1, W3, H)
 
     def _unfuse_grads(self):
         """dF -> phi / Wi gradients (F = W Wi: dW = dF Wi^T, dWi = W^T dF; bias rows likewise)."""
@@ -328,18 +342,18 @@ class GNNActorCritic:
         wic, gwic = self.p("enc.gru_c_wi"), self.g("enc.gru_c_wi")
         for half, nm in ((0, "phi_cp"), (1, "phi_cn")):
             B, gB = pp(wic[half * H]), pp(gwic[half * H])
-            self._gemm(pp(gFc[half * H]), W3, B, W3, 1, self.g(f"enc.{nm}_w").data_ptr(), H, None, H, H, W3, 1)
-            self._gemm(pp(gFc[2 * H + half]), W3, B, W3, 1, self.g(f"enc.{nm}_b").data_ptr(), H, None, 1, H, W3, 1)
-            self._wgrad(self.p(f"enc.{nm}_w").data_ptr(), H, pp(gFc[half * H]), W3, gB, W3, H, H, W3)
-            self._wgrad(self.p(f"enc.{nm}_b").data_ptr(), H, pp(gFc[2 * H + half]), W3, gB, W3, 1, H, W3)
+            self._gemm64(pp(gFc[half * H]), W3, 0, B, W3, 1, self.g(f"enc.{nm}_w").data_ptr(), H, H, H, W3, 1)
+            self._gemm64(pp(gFc[2 * H + half]), W3, 0, B, W3, 1, self.g(f"enc.{nm}_b").data_ptr(), H, 1, H, W3, 1)
+            self._gemm64(self.p(f"enc.{nm}_w").data_ptr(), H, 1, pp(gFc[half * H]), W3, 0, gB, W3, H, W3, H, 1)
+            self._gemm64(self.p(f"enc.{nm}_b").data_ptr(), H, 1, pp(gFc[2 * H + half]), W3, 0, gB, W3, H, W3, 1, 1)
         wv, bv = self.p("enc.phi_v_w"), self.p("enc.phi_v_b")
         gwv, gbv = self.g("enc.phi_v_w"), self.g("enc.phi_v_b")
         for half, cell, gF in ((0, "gru_vp", gFp), (1, "gru_vn", gFn)):
             wi, gwi = self.p(f"enc.{cell}_wi"), self.g(f"enc.{cell}_wi")
-            self._gemm(gF.data_ptr(), W3, wi.data_ptr(), W3, 1, pp(gwv, half * H), 2 * H, None, H, H, W3, 1)
-            self._gemm(pp(gF[H + 4 + half]), W3, wi.data_ptr(), W3, 1, pp(gbv, half * H), H, None, 1, H, W3, 1)
-            self._wgrad(pp(wv, half * H), 2 * H, gF.data_ptr(), W3, gwi.data_ptr(), W3, H, H, W3)
-            self._wgrad(pp(bv, half * H), H, pp(gF[H + 4 + half]), W3, gwi.data_ptr(), W3, 1, H, W3)
+            self._gemm64(gF.data_ptr(), W3, 0, wi.data_ptr(), W3, 1, pp(gwv, half * H), 2 * H, H, H, W3, 1)
+            self._gemm64(pp(gF[H + 4 + half]), W3, 0, wi.data_ptr(), W3, 1, pp(gbv, half * H), H, 1, H, W3, 1)
+            self._gemm64(pp(wv, half * H), 2 * H, 1, gF.data_ptr(), W3, 0, gwi.data_ptr(), W3, H, W3, H, 1)
+            self._gemm64(pp(bv, half * H), H, 1, pp(gF[H + 4 + half]), W3, 0, gwi.data_ptr(), W3, H, W3, 1, 1)
             self._colsum(pp(gF[H]), 4 * W3, 1, 4 * W3, pp(gwi[H]))  # the x / svf rows map 1:1
 
     def _transposed_weights(self, mats):

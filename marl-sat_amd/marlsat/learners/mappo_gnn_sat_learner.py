@@ -164,6 +164,9 @@ class MAPPOLearner:
         self.A, self.M = env.num_agents, env.max_vars_per_agent
         self.mode = env.action_mode
         self.svf = pool.static_var_features()
+        # parity instrumentation: a list makes ppo_update record, per Adam step, the minibatch rows,
+        # the parameters it started from, the (all-reduced) gradient and the learning rate
+        self.trace: Optional[list] = None
         self._alloc()
 
     def _alloc(self):
@@ -256,11 +259,40 @@ class MAPPOLearner:
                    "msat_standardize")
 
     # ------------------------------------------------------------- update ----
+    def minibatch_grad(self, idx: torch.Tensor, ent: float, sums: torch.Tensor, mb_size: int) -> None:
+        """net.grads = d(loss)/d(params) of the PPO loss (learner:597-645) over the flat transition rows
+        ``idx``; ``sums`` (3,) fp64 accumulates (value, actor, entropy) row sums.  Loss means divide by
+        ``mb_size`` (the minibatch size), so micro-batch gradients add up to the minibatch's."""
+        c, net, dev = self.cfg, self.net, self.device
+        N = self.T * self.B
+        flat = {k: v.reshape((N,) + tuple(v.shape[2:])) for k, v in self.tr.items()}
+        adv, tgt = self.adv.reshape(N), self.targets.reshape(N)
+        A, M = self.A, self.M
+        net.grads.zero_()
+        for m0 in range(0, idx.numel(), self.micro):
+            mi = idx[m0:m0 + self.micro]
+            S = mi.numel()
+            gb = self._batch(flat["pidx"][mi], flat["x"][mi])
+            logits, value, state = net.forward(gb, save=True)
+            act = flat["action"][mi].contiguous()
+            olp = flat["log_prob"][mi].contiguous()
+            g_ = adv[mi].contiguous()
+            vold = flat["value"][mi].contiguous()
+            tg = tgt[mi].contiguous()
+            dlog = torch.empty_like(logits)
+            dval = torch.empty_like(value)
+            rows = torch.empty((2 * S * A + S,), device=dev)
+            _lib.check(L_.msat_ppo_loss(
+                logits.data_ptr(), S, A, M, self.mode, net.base, net.rem, act.data_ptr(), olp.data_ptr(),
+                g_.data_ptr(), value.data_ptr(), vold.data_ptr(), tg.data_ptr(), float(c["CLIP_EPS"]),
+                float(c["VF_CLIP"]), ent, float(c["VF_COEF"]), mb_size, dlog.data_ptr(), dval.data_ptr(),
+                rows.data_ptr(), sums.data_ptr(), _lib.stream_ptr(dev)), "msat_ppo_loss")
+            net.backward(gb, state, dlog, dval)
+            del state
+
     def ppo_update(self, update_idx: int, generator: torch.Generator):
         c, net, dev = self.cfg, self.net, self.device
         N, MB, E = self.T * self.B, self.MB, int(c["UPDATE_EPOCHS"])
-        flat = {k: v.reshape((N,) + tuple(v.shape[2:])) for k, v in self.tr.items()}
-        adv, tgt = self.adv.reshape(N), self.targets.reshape(N)
         ent = ent_coef_at(update_idx, c)
         losses = torch.zeros((E, self.n_minibatches, 3), dtype=torch.float64, device=dev)
         A, M = self.A, self.M
@@ -269,30 +301,12 @@ class MAPPOLearner:
             perm = torch.randperm(N, generator=generator, device="cpu").to(dev)
             for k in range(self.n_minibatches):
                 idx = perm[k * MB:(k + 1) * MB]
-                net.grads.zero_()
-                sums = losses[e, k]
-                for m0 in range(0, MB, self.micro):
-                    mi = idx[m0:m0 + self.micro]
-                    S = mi.numel()
-                    gb = self._batch(flat["pidx"][mi], flat["x"][mi])
-                    logits, value, state = net.forward(gb, save=True)
-                    act = flat["action"][mi].contiguous()
-                    olp = flat["log_prob"][mi].contiguous()
-                    g_ = adv[mi].contiguous()
-                    vold = flat["value"][mi].contiguous()
-                    tg = tgt[mi].contiguous()
-                    dlog = torch.empty_like(logits)
-                    dval = torch.empty_like(value)
-                    rows = torch.empty((2 * S * A + S,), device=dev)
-                    _lib.check(L_.msat_ppo_loss(
-                        logits.data_ptr(), S, A, M, self.mode, net.base, net.rem, act.data_ptr(), olp.data_ptr(),
-                        g_.data_ptr(), value.data_ptr(), vold.data_ptr(), tg.data_ptr(), float(c["CLIP_EPS"]),
-                        float(c["VF_CLIP"]), ent, float(c["VF_COEF"]), MB, dlog.data_ptr(), dval.data_ptr(),
-                        rows.data_ptr(), sums.data_ptr(), _lib.stream_ptr(dev)), "msat_ppo_loss")
-                    net.backward(gb, state, dlog, dval)
-                    del state
+                self.minibatch_grad(idx, ent, losses[e, k], MB)
                 scale = allreduce_grads(net.grads, self.dist)
                 lr = learning_rate_at(net.adam_count, c)
+                if self.trace is not None:
+                    self.trace.append({"idx": idx.cpu(), "params": net.params.clone(),
+                                       "grads": net.grads.clone() * scale, "lr": lr})
                 net.adam_step(lr, grad_scale=scale)
         # per-minibatch means: (value_loss, loss_actor, entropy)
         losses[..., 0] /= MB

@@ -48,14 +48,15 @@ METRICS_HEADER = ("update,mean_return,solve_rate,avg_unsat_clauses,avg_solve_ste
 # ------------------------------------------------------------ evaluation ----
 @torch.no_grad()
 def evaluate_policy(key, learner: MAPPOLearner, pool, problem_idx: Sequence[int], max_steps: int,
-                    early_exit: bool = True):
+                    early_exit: bool = True, trace: Optional[list] = None):
     """runner:30-73 for a batch of problems: reset (random assignment), then max_steps greedy
     (argmax) joint actions through step_env; per problem returns
     (was_ever_solved, steps_to_solve (= first solving step + 1, else max_steps),
     solution = the assignment right after that step, zeros if never solved).
 
     The first solve is final, so stopping once every problem has been solved (checked every
-    16 steps) changes no output (early_exit)."""
+    16 steps) changes no output (early_exit).  ``trace`` (parity tests): a list that receives the
+    reset assignment and every step's greedy actions."""
     env, dev = learner.env, learner.device
     k = Key(*key) if isinstance(key, tuple) else key
     k_reset, k_run = split(k, 2)
@@ -66,9 +67,13 @@ def evaluate_policy(key, learner: MAPPOLearner, pool, problem_idx: Sequence[int]
     solved_any = torch.zeros(B, dtype=torch.bool, device=dev)
     first = torch.full((B,), max_steps, dtype=torch.int32, device=dev)
     sol = torch.zeros((B, env.num_vars), dtype=torch.uint8, device=dev)
+    if trace is not None:
+        trace.append(st.variable_assignments.clone())
     for t in range(max_steps):
         k_run, k_act = split(k_run, 2)
         act, _, _ = learner.policy(st, k_act, greedy=True, critic=False)
+        if trace is not None:
+            trace.append(act.clone())
         env.step_raw(st, act, autoreset=False, obs=obs, out=out)
         newly = out["solved"].bool() & ~solved_any
         sol = torch.where(newly[:, None], st.variable_assignments, sol)

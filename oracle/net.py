@@ -82,6 +82,48 @@ def init_params(shapes, seed=0, dtype=torch.float64) -> Dict[str, torch.Tensor]:
     return out
 
 
+# ReLU kinks.  A pre-activation within fp32 noise of 0 is resolved either way by any fp32
+# implementation (the reference's JAX-fp32 run included), and the two sides give gradients that
+# differ by g_e * dz_e/dtheta (g_e: the upstream gradient at that ReLU output).  With
+# RELU_LOG set to a list, every ReLU call appends (pre-activation, output) with their graphs so
+# that kink_bound() can bound that difference for the near-zero elements.
+RELU_LOG = None
+
+
+def _relu(z):
+    y = torch.relu(z)
+    if RELU_LOG is not None:
+        RELU_LOG.append((z, y))
+    return y
+
+
+def kink_bound(obj, params, log, tau=3e-5):
+    """Per-parameter bound on the gradient change from resolving near-zero ReLU inputs the other way:
+    sum over elements e with |z_e| <= tau * max|z| of |g_e * dz_e/dtheta| (one backward per element).
+    obj: the scalar whose gradient is compared (graph retained); log: RELU_LOG of its forward.
+    Returns ({name: bound array}, number of ambiguous elements)."""
+    names = list(params)
+    bound = {k: np.zeros(tuple(params[k].shape)) for k in names}
+    ys = [y for _, y in log]
+    gys = torch.autograd.grad(obj, ys, retain_graph=True, allow_unused=True)
+    n = 0
+    for (z, _), gy in zip(log, gys):
+        if gy is None:
+            continue
+        zf, gf = z.reshape(-1), gy.reshape(-1)
+        amb = torch.nonzero(zf.detach().abs() <= tau * zf.detach().abs().max()).reshape(-1)
+        for e in amb.tolist():
+            if float(gf[e]) == 0.0:
+                continue
+            n += 1
+            gr = torch.autograd.grad(zf[e] * gf[e].detach(), [params[k] for k in names], retain_graph=True,
+                                     allow_unused=True)
+            for k, g in zip(names, gr):
+                if g is not None:
+                    bound[k] += g.detach().abs().double().numpy()
+    return bound, n
+
+
 def _dense(P, name, x):
     y = x @ P[f"{name}/kernel"]
     b = P.get(f"{name}/bias")
@@ -141,8 +183,8 @@ def critic(P, L, svf, x, cf, A_pos, A_neg):
     Hp, Hn, Hc = encoder(P, L, svf, x, cf, A_pos, A_neg)
     Hv = torch.cat([Hp, Hn], -1)
     g = torch.cat([Hv.mean(-2), Hv.amax(-2), Hc.mean(-2), Hc.amax(-2)], -1)
-    h = torch.relu(_dense(P, "critic_dense_0", g))
-    h = torch.relu(_dense(P, "critic_dense_1", h))
+    h = _relu(_dense(P, "critic_dense_0", g))
+    h = _relu(_dense(P, "critic_dense_1", h))
     return _dense(P, "critic_output", h)[..., 0]
 
 
@@ -171,13 +213,13 @@ def actor_logits(P, L, svf, x, cf, A_pos, A_neg, agent_vars, action_mask, action
     ctx = torch.cat([my_sum, pool(Hv, nbr), pool(Hc, cm), ids], -1)  # (B,A,5H+16)
     if action_mode == 0:
         vin = torch.cat([my, ctx[:, :, None].expand(-1, -1, M, -1)], -1)
-        fl = _dense(P, "actor_flip_head_output", torch.relu(_dense(P, "actor_flip_head_dense", vin)))[..., 0]
-        no = _dense(P, "actor_noop_head_output", torch.relu(_dense(P, "actor_noop_head_dense", ctx)))
+        fl = _dense(P, "actor_flip_head_output", _relu(_dense(P, "actor_flip_head_dense", vin)))[..., 0]
+        no = _dense(P, "actor_noop_head_output", _relu(_dense(P, "actor_noop_head_dense", ctx)))
         logits = torch.cat([fl, no], -1)
         full = torch.cat([action_mask, torch.ones((Aa, 1), dtype=torch.bool)], -1)
         return torch.where(full[None], logits, torch.tensor(-math.inf, dtype=logits.dtype))
     ain = torch.cat([my, ids[:, :, None].expand(-1, -1, M, -1)], -1)
-    h = torch.relu(_dense(P, "actor_dense_1", torch.relu(_dense(P, "actor_dense_0", ain))))
+    h = _relu(_dense(P, "actor_dense_1", _relu(_dense(P, "actor_dense_0", ain))))
     vl = _dense(P, "actor_output", h)
     return torch.where(action_mask[None, :, :, None], vl, torch.tensor(-math.inf, dtype=vl.dtype))
 

@@ -29,10 +29,14 @@ def stats(dev, ref):
                 p99_rel=float(np.quantile(rel, 0.99)), min_abs_ref=float(np.abs(r).min()))
 
 
-def run(case, paths):
+def run(case, paths, own_init=False):
     V, C, vpa, H, L, S, mode = case
     from marlsat.learners.gnn import GNNActorCritic
     net, b, P, batch, av, am, A, M = _setup(V, C, vpa, H, L, S, mode)
+    if own_init:  # the learner's own parameter init (params.init_flat) instead of the oracle's
+        fresh = GNNActorCritic(H, L, A, M, mode, V, device="cuda", seed=4)
+        net.params.copy_(fresh.params)
+        P = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in net.to_flax().items()}
     args = (batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"])
     ref_l = onet.actor_logits(P, L, *args, av, am, mode)
     ref_v = onet.critic(P, L, *args)
@@ -41,7 +45,7 @@ def run(case, paths):
     with torch.no_grad():
         l32 = onet.actor_logits(P32, L, *a32, av, am, mode)
         v32 = onet.critic(P32, L, *a32)
-    print(f"case {case}")
+    print(f"case {case} own_init={own_init}")
     print("  cpu-fp32 oracle  logits", stats(l32.numpy(), ref_l.detach().numpy()))
     print("  cpu-fp32 oracle  value ", stats(v32.numpy(), ref_v.detach().numpy()))
     g = torch.Generator().manual_seed(3)
@@ -71,6 +75,12 @@ def run(case, paths):
 
 if __name__ == "__main__":
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "paths":
+        paths = {"default": (True, True, True), "fused-fp32": (True, False, False),
+                 "ref-order-x3": (False, True, True), "fp32-ref-order": (False, False, False)}
+        for own in (True, False):
+            run((50, 218, 10, 128, 16, 8, 0), paths, own_init=own)
+        sys.exit(0)
     paths = {"default": (True, True, True), "fp32-ref-order": (False, False, False)}
     for case in [(20, 91, 10, 128, 2, 3, 0), (50, 218, 10, 128, 16, 4, 0), (100, 430, 10, 128, 16, 2, 0),
                  (16, 60, 4, 128, 16, 3, 1)]:

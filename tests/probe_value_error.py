@@ -1,0 +1,105 @@
+"""Probe (test infrastructure, not collected): critic value error per kernel path on the batch of
+tests/test_mappo_gpu.py::test_train_cycle_every_adam_step_matches_oracle (uf50, H=128, L=16)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "marl-sat_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from oracle import net as onet  # noqa: E402
+from oracle.sat_env import OracleSATEnv  # noqa: E402
+
+
+H, L = 128, 16
+def D(P,n,x): return onet._dense(P,n,x)
+def enc_folded(P,svf,x,cf,Ap,An,F64=False):
+    dt=svf.dtype
+    At_p,At_n=Ap.transpose(-1,-2),An.transpose(-1,-2)
+    Hp=D(P,"encoder/literal_pos_embed",svf); Hn=D(P,"encoder/literal_neg_embed",svf); Hc=D(P,"encoder/clause_embed",cf)
+    xin=torch.cat([x[...,None],svf],-1)
+    def fold(W,b,Wi):
+        if F64: return (W.double()@Wi.double()).to(dt),(b.double()@Wi.double()).to(dt)
+        return W@Wi, b@Wi
+    g=lambda n:P[n]
+    def gru(name,h,pre_i):
+        r=torch.sigmoid(pre_i[...,:H]+h@g(f"{name}/hr/kernel"))
+        z=torch.sigmoid(pre_i[...,H:2*H]+h@g(f"{name}/hz/kernel"))
+        n=torch.tanh(pre_i[...,2*H:]+r*(h@g(f"{name}/hn/kernel")+g(f"{name}/hn/bias")))
+        return (1-z)*n+z*h
+    Wi=lambda name: torch.cat([g(f"{name}/ir/kernel"),g(f"{name}/iz/kernel"),g(f"{name}/in/kernel")],1)
+    bi=lambda name: torch.cat([g(f"{name}/ir/bias"),g(f"{name}/iz/bias"),g(f"{name}/in/bias")],0)
+    Wc=Wi("encoder/update_c"); Fcp,fcp=fold(g("encoder/phi_c_pos/kernel"),g("encoder/phi_c_pos/bias"),Wc[:H]); Fcn,fcn=fold(g("encoder/phi_c_neg/kernel"),g("encoder/phi_c_neg/bias"),Wc[H:])
+    Wvp=Wi("encoder/update_v_pos"); Wvn=Wi("encoder/update_v_neg")
+    Fvp,fvp=fold(g("encoder/phi_v_pos/kernel"),g("encoder/phi_v_pos/bias"),Wvp[:H]); Fvn,fvn=fold(g("encoder/phi_v_neg/kernel"),g("encoder/phi_v_neg/bias"),Wvn[:H])
+    npos=Ap.sum(-2)[...,None]; nneg=An.sum(-2)[...,None]; dp=Ap.sum(-1)[...,None]; dn=An.sum(-1)[...,None]
+    for l in range(L):
+        pre=(At_p@Hp)@Fcp+(At_n@Hn)@Fcn+npos*fcp+nneg*fcn+bi("encoder/update_c")
+        Hc=onet._ln(P,3*l,gru("encoder/update_c",Hc,pre))
+        prep=(Ap@Hc)@Fvp+xin@Wvp[H:]+dp*fvp+bi("encoder/update_v_pos")
+        pren=(An@Hc)@Fvn+xin@Wvn[H:]+dn*fvn+bi("encoder/update_v_neg")
+        Hp,Hn=onet._ln(P,3*l+1,gru("encoder/update_v_pos",Hp,prep)),onet._ln(P,3*l+2,gru("encoder/update_v_neg",Hn,pren))
+    return Hp,Hn,Hc
+def critic_from(P,Hp,Hn,Hc):
+    Hv=torch.cat([Hp,Hn],-1); gg=torch.cat([Hv.mean(-2),Hv.amax(-2),Hc.mean(-2),Hc.amax(-2)],-1)
+    h=torch.relu(D(P,"critic_dense_0",gg)); h=torch.relu(D(P,"critic_dense_1",h)); return D(P,"critic_output",h)[...,0]
+
+
+def main():
+    from marlsat import SATEnv
+    from marlsat.learners.gnn import GNNActorCritic
+    from marlsat.learners.mappo_gnn_sat_learner import MAPPOLearner
+    from marlsat.random import PRNGKey
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+
+    torch.cuda.set_device(0)
+    V, C, vpa, H, L = 50, 218, 10, 128, 16
+    T, B = 4, 8
+    cfg = dict(NUM_ENVS=B, NUM_STEPS=T, MINIBATCH_SIZE=B, UPDATE_EPOCHS=1, GNN_HIDDEN_DIM=H,
+               GNN_NUM_MESSAGE_PASSING_STEPS=L, action_mode=0, GAMMA=0.99, GAE_LAMBDA=0.95)
+    pool = generate_problem_pool(V, C, 5, size_id=12)
+    env = SATEnv(V, C, max_steps=2, vars_per_agent=vpa)
+    A, M = env.num_agents, env.max_vars_per_agent
+    net = GNNActorCritic(H, L, A, M, 0, V, device="cuda", seed=4)
+    learner = MAPPOLearner(cfg, env, net, env.make_pool(pool))
+    rs = learner.init_runner_state(PRNGKey(1))
+    learner.rollout(rs)
+    N = T * B
+    pidx = learner.tr["pidx"].reshape(N)
+    x = learner.tr["x"].reshape(N, V)
+    ora = OracleSATEnv(V, C, 2, vars_per_agent=vpa)
+    pn, xn = pidx.cpu().numpy(), x.cpu().numpy()
+    _, ost = ora.reset(pool[pn], xn.astype(np.int32))
+    Ap, An = onet.dense_graph(pool[pn], V)
+    args = (torch.from_numpy(ora.static_var_features(pool[pn])).double(), torch.from_numpy(xn).double(),
+            torch.from_numpy(ora.clause_features(ost)).double(), Ap, An)
+    tree = net.to_flax()
+    with torch.no_grad():
+        ref = onet.critic({k: torch.tensor(v, dtype=torch.float64) for k, v in tree.items()}, L, *args).numpy()
+        r32 = onet.critic({k: torch.tensor(v, dtype=torch.float32) for k, v in tree.items()}, L,
+                          *(a.float() for a in args)).numpy()
+    m = np.abs(ref).max()
+    print("N", N, "max|v|", m, "cpu fp32 norm err %.2e" % (np.abs(r32 - ref).max() / m))
+    P32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in tree.items()}
+    a32 = tuple(a.float() for a in args)
+    with torch.no_grad():
+        f32 = critic_from(P32, *enc_folded(P32, *a32)).numpy()
+        f32b = critic_from(P32, *enc_folded(P32, *a32, F64=True)).numpy()
+    print("cpu fold32 norm err %.2e, fold32 with F in fp64 %.2e" % (np.abs(f32 - ref).max() / m,
+                                                                     np.abs(f32b - ref).max() / m))
+    for name, (fuse, x3, x3r) in {"x3r(default)": (True, True, True), "x3": (True, True, False),
+                                  "fused-fp32": (True, False, False), "ref-order": (False, False, False)}.items():
+        GNNActorCritic.fuse_phi, GNNActorCritic.use_x3, GNNActorCritic.use_gru_x3 = fuse, x3, x3
+        GNNActorCritic.use_gru_x3r = x3r
+        with torch.no_grad():
+            v_full = learner.critic_values(pidx, x).cpu().numpy()
+            _, _, v_roll = learner.policy(rs.env_state, PRNGKey(2))
+        print(f"{name:14s} critic-only norm err %.2e" % (np.abs(v_full - ref).max() / m),
+              "per-element / fp32", np.round(np.abs(v_full - ref) / np.maximum(np.abs(r32 - ref), 1e-12), 1)[:12])
+        sys.stdout.flush()
+
+
+if __name__ == "__main__":
+    main()

@@ -380,3 +380,105 @@ def test_grouped_eight_classes_with_empty_ones():
             assert torch.equal(obs[g], o2), (g, t)
             assert torch.equal(states[g].variable_assignments, st.variable_assignments), (g, t)
             assert torch.equal(outs[g]["reward"], out2["reward"]), (g, t)
+
+
+def _config5(sizes, max_steps, seed0):
+    """BASELINE config 5 classes: uf50-218 (5 agents), uf100-430 (10), uf200-860 (25), native sizes."""
+    from marlsat.envs.mixed import MixedSATEnv
+
+    specs = [(50, 218, 10), (100, 430, 10), (200, 860, 8)]
+    classes, oras, pools = [], [], []
+    for i, ((V, C, vpa), B) in enumerate(zip(specs, sizes)):
+        env, ora = _mk(V, C, vpa, max_steps=max_steps)
+        classes.append(env)
+        oras.append(ora)
+        pools.append(_pool(V, C, 16, seed0=seed0 + 1000 * i))
+    return MixedSATEnv(classes), classes, oras, pools
+
+
+def test_config5_grouped_matches_oracle_per_class():
+    """Config 5 (mixed uf50 / uf100 / uf200 in ONE grouped launch) against the oracle: every class
+    replayed at its native size through env:225-398 (the reference cannot mix sizes,
+    runner:114-118), RNG resets replayed on the host with the class seed seed ^ group_seed(g)."""
+    from marlsat.envs.mixed import group_seed
+    from marlsat.random import Key
+
+    sizes = [24, 16, 12]
+    mixed, classes, oras, pools = _config5(sizes, 3, 7000)
+    key = Key(0x1234, 2)
+    obs, states = mixed.reset([c.make_pool(p) for c, p in zip(classes, pools)], sizes, key)
+    osts = []
+    for g, (ora, p, B) in enumerate(zip(oras, pools, sizes)):
+        p0, x0 = reset_draws(key.seed ^ group_seed(g), key.counter, B, ora.num_vars, len(p))
+        oobs, ost = ora.reset(p[p0], x0.astype(np.int32))
+        np.testing.assert_array_equal(_np(obs[g]), oobs, err_msg=f"class {g} reset")
+        _check_state(classes[g], states[g], ost, f"class {g} reset")
+        osts.append(ost)
+    outs = mixed.alloc_outs(states)
+    seed = 0xC0FFEE
+    step = mixed.stepper(states, obs, outs, autoreset=True, seed=seed)
+    rng = np.random.default_rng(5)
+    n_done = [0] * 3
+    for t in range(7):  # max_steps 3: every env auto-resets twice
+        acts = [_random_actions(rng, c, B) for c, B in zip(classes, sizes)]
+        step([torch.from_numpy(a).cuda() for a in acts], 20 + t)
+        for g, (ora, p, B) in enumerate(zip(oras, pools, sizes)):
+            p2, x2 = reset_draws(seed ^ group_seed(g), 20 + t, B, ora.num_vars, len(p))
+            oobs, osts[g], r, d, info = ora.step_autoreset(osts[g], acts[g], p[p2], x2.astype(np.int32))
+            ctx = f"class {g} t={t}"
+            np.testing.assert_array_equal(_np(obs[g]), oobs, err_msg=ctx)
+            np.testing.assert_array_equal(_np(outs[g]["reward"]), r, err_msg=ctx)
+            np.testing.assert_array_equal(_np(outs[g]["done"]).astype(bool), d, err_msg=ctx)
+            np.testing.assert_array_equal(_np(outs[g]["num_unsatisfied"]), info["num_unsatisfied"], err_msg=ctx)
+            np.testing.assert_array_equal(_np(outs[g]["episode_step"]), info["episode_step"], err_msg=ctx)
+            _check_state(classes[g], states[g], osts[g], ctx)
+            n_done[g] += int(d.sum())
+    assert all(n > 0 for n in n_done)  # the auto-reset branch ran in every class
+
+
+def test_config5_full_size_8192_properties_and_sampled_parity():
+    """Config 5 at its full size on one GPU: 2731 uf50 + 2731 uf100 + 2730 uf200 = 8192 envs in one
+    grouped launch.  Invariants on every env (num_unsat == C - sum sat, ntrue > 0 <=> sat, obs
+    segments consistent with the state) and exact oracle replay of 32 sampled envs per class."""
+    from marlsat.envs.mixed import group_seed
+    from marlsat.random import Key
+
+    sizes = [2731, 2731, 2730]
+    mixed, classes, oras, pools = _config5(sizes, 4, 9000)
+    obs, states = mixed.reset([c.make_pool(p) for c, p in zip(classes, pools)], sizes, Key(5, 0))
+    outs = mixed.alloc_outs(states)
+    seed = 0xBEEF
+    step = mixed.stepper(states, obs, outs, autoreset=True, seed=seed)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    samples = [np.random.default_rng(g).choice(B, 32, replace=False) for g, B in enumerate(sizes)]
+    n_done = [0] * 3
+    for t in range(6):
+        before = [(_np(s.problem_idx).copy(), _np(s.variable_assignments).copy(), _np(s.step).copy()) for s in states]
+        acts = [torch.randint(0, c.max_vars_per_agent + 1, (B, c.num_agents), generator=gen, device="cuda",
+                              dtype=torch.int32) for c, B in zip(classes, sizes)]
+        step(acts, 100 + t)
+        for g, (c, ora, p, B) in enumerate(zip(classes, oras, pools, sizes)):
+            st, C, V = states[g], c.num_clauses, c.num_vars
+            sat = st.clauses_satisfied_status.int()
+            assert torch.equal(C - sat.sum(1), st.num_unsatisfied), (g, t)
+            assert torch.equal(st.clause_ntrue.gt(0).int(), sat), (g, t)
+            # own-variable segment of every agent's obs holds the assignment (or -1 elsewhere)
+            o = obs[g][:, :, :V].long()
+            own = torch.from_numpy((ora.agent_vars[:, :, None] == np.arange(V)[None, None]).any(1)).cuda()
+            x = st.variable_assignments.long()[:, None, :].expand_as(o)
+            assert torch.equal(torch.where(own[None], x, torch.full_like(o, -1)), o), (g, t)
+            # clause segment: status where the clause touches the agent, -1 elsewhere
+            oc = obs[g][:, :, V:V + C].long()
+            assert bool(((oc == -1) | (oc == sat.long()[:, None, :])).all()), (g, t)
+            sm = samples[g]
+            pidx0, x0, step0 = before[g]
+            _, ost = ora.reset(p[pidx0[sm]], x0[sm].astype(np.int32))
+            ost.step = step0[sm]
+            p2, x2 = reset_draws(seed ^ group_seed(g), 100 + t, B, V, len(p))
+            oobs, ost, r, d, info = ora.step_autoreset(ost, _np(acts[g])[sm], p[p2[sm]], x2[sm].astype(np.int32))
+            np.testing.assert_array_equal(_np(obs[g])[sm], oobs, err_msg=f"class {g} t={t}")
+            np.testing.assert_array_equal(_np(outs[g]["done"])[sm].astype(bool), d)
+            np.testing.assert_array_equal(_np(outs[g]["reward"])[sm], r)
+            np.testing.assert_array_equal(_np(st.variable_assignments)[sm], ost.variable_assignments)
+            n_done[g] += int(outs[g]["done"].sum())
+    assert all(n > 0 for n in n_done)

@@ -131,3 +131,133 @@ def test_train_cycle_matches_oracle_replay(mode):
     ev = 1.0 - np.var(tg - vnew) / max(np.var(tg), 1e-8)
     np.testing.assert_allclose(metrics["explained_variance"], ev, rtol=1e-4, atol=1e-5)
     assert metrics["current_ent_coef"] == cfg["ENT_COEF"]
+
+
+def _yard_close(dev, ref, yard, factor, what, rtol=1e-5, extra=None):
+    """|dev - ref| <= rtol |ref| + factor * max|yard - ref| (+ extra) (yard: the fp32 CPU oracle's
+    value; extra: oracle.net.kink_bound's allowance for ReLU inputs within fp32 noise of 0)."""
+    dev, ref, yard = (np.asarray(a, np.float64) for a in (dev, ref, yard))
+    fin = np.isfinite(ref)
+    assert np.array_equal(fin, np.isfinite(dev)), what
+    atol = factor * (np.abs(yard[fin] - ref[fin]).max() if fin.any() else 0.0)
+    err = np.abs(dev[fin] - ref[fin])
+    bound = rtol * np.abs(ref[fin]) + atol + (0.0 if extra is None else np.asarray(extra, np.float64)[fin])
+    assert (err <= bound).all(), f"{what}: max err {err.max():.3g}, worst ratio {(err / bound).max():.3g}"
+
+
+@pytest.mark.parametrize("V,C,vpa,H,L,mode", [
+    (50, 218, 10, 128, 16, 0),  # uf50-218, 5 agents, the reference's H = 128, L = 16
+    (23, 97, 10, 64, 2, 1),  # mode 1 with a padded variable slot (agents of 8, 8, 7)
+])
+def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode):
+    """Teacher-forced replay of a whole train cycle: for every Adam step the oracle starts from the
+    parameters the device started from (recorded by ``MAPPOLearner.trace``), so each minibatch is
+    checked at the north_star bar without the drift of an independent replay (next test):
+      * rollout log-probs and values, GAE targets: 1e-5 relative (+ 4x the fp32 oracle's error);
+      * the loss triple of EVERY minibatch (the first one included): 1e-5 relative;
+      * the gradient of every minibatch: 1e-5 relative + 8x the fp32 oracle's error per tensor;
+      * the Adam step: the device's new parameters vs optax.adam applied in float64 to the device's
+        own gradient (1e-5 relative).
+    Mode 1 runs with a padded slot: the parameters must stay finite (the slot counts as 0)."""
+    from marlsat import SATEnv
+    from marlsat.learners.gnn import GNNActorCritic
+    from marlsat.learners.mappo_gnn_sat_learner import MAPPOLearner
+    from marlsat.random import PRNGKey
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+
+    T, B, MB, E = 2, 4, 4, 2
+    cfg = _cfg(NUM_ENVS=B, NUM_STEPS=T, MINIBATCH_SIZE=MB, UPDATE_EPOCHS=E, GNN_HIDDEN_DIM=H,
+               GNN_NUM_MESSAGE_PASSING_STEPS=L, action_mode=mode)
+    pool = generate_problem_pool(V, C, 5, size_id=12)
+    env = SATEnv(V, C, max_steps=2, vars_per_agent=vpa, action_mode=mode)
+    A, M = env.num_agents, env.max_vars_per_agent
+    assert mode == 0 or V % A  # the mode-1 case must have padded slots
+    net = GNNActorCritic(H, L, A, M, mode, V, device="cuda", seed=4)
+    learner = MAPPOLearner(cfg, env, net, env.make_pool(pool))
+    learner.trace = []
+    rs = learner.init_runner_state(PRNGKey(1))
+    rs, metrics = learner.train_cycle(rs, 0, torch.Generator().manual_seed(7))
+    assert torch.isfinite(net.params).all()
+    tr = {k: v.cpu().numpy() for k, v in learner.tr.items()}
+    ora = OracleSATEnv(V, C, 2, vars_per_agent=vpa, action_mode=mode)
+    av = torch.from_numpy(ora.agent_vars.astype(np.int64))
+    am = torch.from_numpy(ora.action_mask)
+    flat = lambda a: a.reshape((T * B,) + a.shape[2:])
+    pidx, x = flat(tr["pidx"]), flat(tr["x"])
+    _, ost = ora.reset(pool[pidx], x.astype(np.int32))
+    Ap, An = onet.dense_graph(pool[pidx], V)
+    bt = {"svf": torch.from_numpy(ora.static_var_features(pool[pidx])).double(),
+          "x": torch.from_numpy(x.astype(np.float64)), "cf": torch.from_numpy(ora.clause_features(ost)).double(),
+          "A_pos": Ap, "A_neg": An}
+    args = (bt["svf"], bt["x"], bt["cf"], bt["A_pos"], bt["A_neg"])
+    to_t = lambda tree, dt: {k: torch.tensor(v, dtype=dt) for k, v in tree.items()}
+    layout = lambda flat_params: _unflat(net, flat_params)
+    act = torch.from_numpy(flat(tr["action"])).long()
+
+    def rollout_terms(P):
+        with torch.no_grad():
+            lg = onet.actor_logits(P, L, *(a.to(next(iter(P.values())).dtype) for a in args), av, am, mode)
+            val = onet.critic(P, L, *(a.to(next(iter(P.values())).dtype) for a in args))
+            lp = torch.log_softmax(lg, -1).gather(-1, act[..., None])[..., 0]
+        if mode == 1:
+            lp = torch.where(am[None].expand_as(lp), lp, torch.zeros_like(lp))
+        return lp.double().numpy(), val.double().numpy()
+
+    p_start = layout(learner.trace[0]["params"])
+    lp64, v64 = rollout_terms(to_t(p_start, torch.float64))
+    lp32, v32 = rollout_terms(to_t(p_start, torch.float32))
+    _yard_close(flat(tr["log_prob"]), lp64, lp32, 4.0, "rollout log_prob")
+    _yard_close(flat(tr["value"]), v64, v32, 4.0, "rollout value")
+    adv, tgt = om.gae(tr["reward"], tr["value"], tr["done"].astype(bool), learner.last_val.cpu().numpy(),
+                      cfg["GAMMA"], cfg["GAE_LAMBDA"])
+    np.testing.assert_allclose(learner.targets.cpu().numpy(), tgt, rtol=1e-5, atol=1e-7)
+    adv_n, _, _ = om.normalize(adv)
+    full = dict(bt, action=act, log_prob=torch.from_numpy(flat(tr["log_prob"]).astype(np.float64)),
+                value=torch.from_numpy(flat(tr["value"]).astype(np.float64)),
+                targets=torch.from_numpy(learner.targets.cpu().numpy().reshape(-1).astype(np.float64)),
+                gae=torch.from_numpy(learner.adv.cpu().numpy().reshape(-1).astype(np.float64)))
+    np.testing.assert_allclose(full["gae"].numpy(), adv_n.reshape(-1), rtol=1e-5, atol=1e-6)
+    dev_losses = np.stack([metrics["epoch_value_losses"].reshape(-1), metrics["epoch_actor_losses"].reshape(-1),
+                           metrics["epoch_entropies"].reshape(-1)], 1)
+    assert len(learner.trace) == E * (T * B // MB) == dev_losses.shape[0]
+    m_st = {"count": 0, "m": None, "v": None}
+    for s, rec in enumerate(learner.trace):
+        idx = rec["idx"].numpy()
+        mb = {k: v[idx] for k, v in full.items()}
+        P_s = layout(rec["params"])
+        out = {}
+        for dt in (torch.float64, torch.float32):
+            Pk = {k: torch.tensor(v, dtype=dt, requires_grad=True) for k, v in P_s.items()}
+            mbk = {k: (v.to(dt) if v.is_floating_point() else v) for k, v in mb.items()}
+            onet.RELU_LOG = log = [] if dt == torch.float64 else None
+            try:
+                total, (vl, la, ent), _, _ = onet.ppo_loss(Pk, L, mbk, cfg, av, am, mode)
+            finally:
+                onet.RELU_LOG = None
+            if dt == torch.float64:
+                kink, _ = onet.kink_bound(total, Pk, log)
+            total.backward()
+            out[dt] = ([float(vl.detach()), float(la.detach()), float(ent.detach())],
+                       {k: (p.grad.double().numpy() if p.grad is not None else np.zeros(p.shape)) for k, p in Pk.items()})
+        np.testing.assert_allclose(dev_losses[s], out[torch.float64][0], rtol=1e-5, atol=1e-8,
+                                   err_msg=f"Adam step {s}: (value_loss, loss_actor, entropy)")
+        g_dev = layout(rec["grads"])
+        for k in P_s:
+            _yard_close(g_dev[k], out[torch.float64][1][k], out[torch.float32][1][k], 8.0, f"step {s} grad {k}",
+                        extra=kink[k])
+        # optax.adam in float64 on the device's own gradient, from the device's own parameters
+        gflat = rec["grads"].double().cpu()
+        if m_st["m"] is None:
+            m_st["m"], m_st["v"] = torch.zeros_like(gflat), torch.zeros_like(gflat)
+        pr, m_st2 = onet.adam_update({"p": rec["params"].double().cpu()}, {"p": gflat},
+                                     {"count": m_st["count"], "m": {"p": m_st["m"]}, "v": {"p": m_st["v"]}}, rec["lr"])
+        m_st = {"count": m_st2["count"], "m": m_st2["m"]["p"], "v": m_st2["v"]["p"]}
+        nxt = learner.trace[s + 1]["params"] if s + 1 < len(learner.trace) else net.params
+        np.testing.assert_allclose(nxt.double().cpu().numpy(), pr["p"].numpy(), rtol=1e-5, atol=1e-7,
+                                   err_msg=f"Adam step {s}")
+
+
+def _unflat(net, flat_params):
+    from marlsat.learners import params as Pm
+
+    return Pm.to_flax(flat_params.detach().cpu().numpy(), net.H, net.L, net.A, net.M, net.mode, net.E)

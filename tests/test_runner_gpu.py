@@ -93,3 +93,65 @@ def test_evaluate_policy_early_exit_is_exact():
     for i in np.nonzero(solved)[0]:
         _, nun = env._calculate_satisfaction_explicit(sols[i], pool.clauses[i].cpu().numpy())
         assert int(nun) == 0
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_evaluate_policy_replays_on_oracle(mode):
+    """runner:30-73 replayed on the oracle: the reset draws (oracle/rng.reset_draws), every step's
+    greedy actions (argmax of the float64 oracle logits; a near-tie within 1e-5 of the logit scale
+    may go either way in fp32 and is then replayed with the device's choice), the env steps
+    (oracle/sat_env.py), the first-solve step and the recorded solution, bit-exact."""
+    from marlsat import SATEnv
+    from marlsat.learners.gnn import GNNActorCritic
+    from marlsat.learners.mappo_gnn_sat_learner import MAPPOLearner
+    from marlsat.random import Key, split
+    from marlsat.runners.mappo_runner import evaluate_policy
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+    from oracle import net as onet
+    from oracle.rng import reset_draws
+    from oracle.sat_env import OracleSATEnv
+
+    V, C, vpa, T = (20, 91, 10, 24) if mode == 0 else (12, 40, 3, 24)
+    N = 10
+    clauses = generate_problem_pool(V, C, N, size_id=3)
+    env = SATEnv(V, C, max_steps=T, vars_per_agent=vpa, action_mode=mode)
+    pool = env.make_pool(clauses)
+    A, M = env.num_agents, env.max_vars_per_agent
+    net = GNNActorCritic(64, 2, A, M, mode, V, device="cuda", seed=6)
+    lr = MAPPOLearner(dict(NUM_ENVS=N, NUM_STEPS=1, MINIBATCH_SIZE=N), env, net, pool)
+    probs = np.arange(N)[::-1].copy()
+    trace = []
+    key = Key(21, 4)
+    solved, steps, sols = evaluate_policy(key, lr, pool, probs, T, early_exit=False, trace=trace)
+    k_reset, _ = split(key, 2)
+    _, x0 = reset_draws(k_reset.seed, k_reset.counter, N, V, N)
+    np.testing.assert_array_equal(trace[0].cpu().numpy(), x0)
+    ora = OracleSATEnv(V, C, T, vars_per_agent=vpa, action_mode=mode)
+    _, ost = ora.reset(clauses[probs], x0.astype(np.int32))
+    Pf = {k: torch.tensor(v, dtype=torch.float64) for k, v in net.to_flax().items()}
+    av, am = torch.from_numpy(ora.agent_vars.astype(np.int64)), torch.from_numpy(ora.action_mask)
+    Ap, An = onet.dense_graph(clauses[probs], V)
+    svf = torch.from_numpy(ora.static_var_features(clauses[probs])).double()
+    o_solved = np.zeros(N, bool)
+    o_steps = np.full(N, T)
+    o_sol = np.zeros((N, V), np.int32)
+    for t in range(T):
+        x = torch.from_numpy(ost.variable_assignments.astype(np.float64))
+        cf = torch.from_numpy(ora.clause_features(ost)).double()
+        with torch.no_grad():
+            lg = onet.actor_logits(Pf, 2, svf, x, cf, Ap, An, av, am, mode).numpy()
+        dev_act = trace[1 + t].cpu().numpy()
+        ref_act = lg.argmax(-1)  # jnp.argmax: first maximum
+        top = np.take_along_axis(lg, ref_act[..., None], -1)[..., 0]
+        pick = np.take_along_axis(lg, dev_act[..., None].astype(np.int64), -1)[..., 0]
+        scale = np.abs(lg[np.isfinite(lg)]).max()
+        same = dev_act == ref_act
+        assert (same | (top - pick <= 1e-5 * scale)).all(), f"step {t}: greedy action differs beyond a near-tie"
+        _, ost, _, _, info = ora.step(ost, dev_act)
+        newly = info["solved"] & ~o_solved
+        o_sol[newly] = ost.variable_assignments[newly]
+        o_steps[newly] = t + 1
+        o_solved |= newly
+    np.testing.assert_array_equal(solved, o_solved)
+    np.testing.assert_array_equal(steps, o_steps)
+    np.testing.assert_array_equal(sols, o_sol)
