@@ -11,12 +11,16 @@ Multi-GPU (torchrun, one process per GPU): independent env shards, no
 collective on the data path; barrier + synchronize around the timed region,
 max elapsed over ranks; value = all ranks' env-steps / that time (weak scaling).
 
-MAPPO leg (the metric's "MAPPO updates/sec"): one full train cycle of the device
+MAPPO legs (the metric's "MAPPO updates/sec"): one full train cycle of the device
 learner -- rollout of T steps (actor + critic forward, sampling, fused env step with
 auto-reset), GAE + global advantage normalisation, UPDATE_EPOCHS x T*B/MINIBATCH_SIZE
 PPO minibatches (forward, loss, backward, gradient all-reduce over RCCL when N>1,
-Adam) and the cycle metrics -- timed after one warm-up cycle, reported under
-"mappo" with per-phase times and the fp32-MFMA roofline of the GEMMs issued.
+Adam) and the cycle metrics -- timed after one warm-up cycle.  The headline leg is
+uf100-430 x 4096 envs (BASELINE config 3, the metric's 4096 envs), T = 8; uf50-218 x
+1024 envs, T = 32 (config 2) is reported beside it.  Each leg carries per-phase times
+and a per-kernel table of the matrix kernels (HIP events around each launch), and its
+roofline is the dominant kernel's fp32-equivalent TFLOP/s against the ceiling of the
+instruction it issues (bf16 dense / 6 for the bf16x3 kernels).
 
 Prints ONE JSON line on rank 0.
 """
@@ -43,6 +47,10 @@ WORKLOADS = {  # name: V, C, vars_per_agent, envs per GPU, size_id (seed = 1000*
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 matrix peak (~2.5 PF, MI355X_MICROARCH.md)
+# the bf16x3 kernels issue 6 bf16 MFMAs per fp32 product (x1y1, x1y2, x2y1, x1y3, x2y2, x3y1):
+# their ceiling in fp32-equivalent FLOP/s is the bf16 dense peak / 6
+X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 
 
 
@@ -173,7 +181,30 @@ def mappo_cpu_baseline(workload: str, budget_s: float = 10.0, batch: int = 8):
                       f"encoders), float32, {workload}, H=128, L=16, minibatches of {batch}, {n} samples in {wall:.1f} s"}
 
 
-def mappo_bench(args, rank, world, dist):
+def kernel_table(ktimer: dict) -> list:
+    """Per-kernel totals of the GNN's MFMA launches recorded by GNNActorCritic.ktimer (HIP events on
+    the launch stream around each launch): average duration and fp32-equivalent TFLOP/s against the
+    ceiling of the instruction the kernel issues (bf16 dense / 6 for the bf16x3 kernels, fp32 MFMA
+    for the fp32 ones).  Sorted by total time."""
+    rows = []
+    for label, recs in ktimer.items():
+        ms = sum(a.elapsed_time(b) for a, b, _ in recs)
+        fl = sum(f for _, _, f in recs)
+        if "K <= 8" in label:
+            peak, unit_note = None, "HBM-bound (K <= 8 columns), not priced against a matrix peak"
+        elif "bf16x3" in label:
+            peak, unit_note = X3_PEAK_TFLOPS, "bf16 dense peak / 6 (six bf16 MFMAs per fp32 product)"
+        else:
+            peak, unit_note = FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA peak"
+        tf = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        rows.append({"kernel": label, "launches": len(recs), "ms_total": ms, "ms_avg": ms / len(recs),
+                     "tflops_fp32_equiv": tf, "peak": peak, "frac": (tf / peak) if peak else None,
+                     "peak_basis": unit_note})
+    rows.sort(key=lambda r: -r["ms_total"])
+    return rows
+
+
+def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
     """One timed MAPPO train cycle (after one warm-up cycle) on the stated config."""
     import torch
 
@@ -183,8 +214,8 @@ def mappo_bench(args, rank, world, dist):
     from marlsat.random import PRNGKey
     from marlsat.utils.generate_cnf_dataset import generate_problem_pool
 
-    V, C, vpa, _, size_id = WORKLOADS[args.mappo_workload]
-    B, T, E = args.mappo_envs, args.mappo_T, 4
+    V, C, vpa, _, size_id = WORKLOADS[workload]
+    E = 4
     H, L = 128, 16
     cfg = dict(NUM_ENVS=B, NUM_STEPS=T, UPDATE_EPOCHS=E, MINIBATCH_SIZE=B * T // 4, NUM_UPDATES=1000,
                LEARNING_RATE=3e-4, ANNEAL_LR=True, LR_START_FACTOR=1.0, LR_END_FLOOR=1e-5, GAMMA=0.99,
@@ -206,6 +237,7 @@ def mappo_bench(args, rank, world, dist):
         dist.barrier()
     torch.cuda.synchronize()
     GNNActorCritic.flops = 0
+    GNNActorCritic.ktimer = {}
     t0 = time.perf_counter()
     ev[0].record()
     rs = learner.rollout(rs)
@@ -222,12 +254,18 @@ def mappo_bench(args, rank, world, dist):
     elapsed = time.perf_counter() - t0
     phases = [ev[i].elapsed_time(ev[i + 1]) for i in range(4)]
     flops = float(GNNActorCritic.flops)
+    kernels = kernel_table(GNNActorCritic.ktimer)
+    GNNActorCritic.ktimer = None
+    cycle_ms = sum(phases)
     if dist is not None:
         t = torch.tensor([elapsed] + phases, dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, phases = float(t[0]), [float(v) for v in t[1:]]
     n_mb = B * T // cfg["MINIBATCH_SIZE"]
     gemm_tflops = flops / (elapsed * 1e12)
+    dom = next(k for k in kernels if k["peak"])  # the matrix kernel with the most time in the cycle
+    for k in kernels:
+        k["share_of_cycle"] = k["ms_total"] / cycle_ms
     return {
         "metric": "MAPPO updates/sec",
         "value": 1.0 / elapsed,
@@ -237,14 +275,19 @@ def mappo_bench(args, rank, world, dist):
         "samples_per_s": world * B * T / elapsed,
         "ppo_samples_per_s": world * E * B * T / (phases[2] * 1e-3),
         "phase_ms": dict(zip(("rollout", "gae", "ppo_update", "metrics"), phases)),
-        "config": {"workload": args.mappo_workload, "num_vars": V, "num_clauses": C, "num_agents": env.num_agents,
+        "config": {"workload": workload, "num_vars": V, "num_clauses": C, "num_agents": env.num_agents,
                    "envs_per_gpu": B, "NUM_STEPS": T, "UPDATE_EPOCHS": E, "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"],
                    "GNN_HIDDEN_DIM": H, "GNN_NUM_MESSAGE_PASSING_STEPS": L, "micro_batch": learner.micro,
                    "parallelism": f"dp{world} (env shards; RCCL gradient all-reduce per minibatch)"},
-        "roofline": {"bound": "mfma", "achieved": gemm_tflops, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": gemm_tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                     "note": "2*M*N*K of every fp32 GEMM issued in the cycle / cycle wall time (rank max)"},
-        "dtype": "f32",
+        "roofline": {"bound": "mfma", "kernel": dom["kernel"], "achieved": dom["tflops_fp32_equiv"],
+                     "peak": dom["peak"], "unit": "TFLOP/s (fp32-equivalent)", "frac": dom["frac"], "traffic": None,
+                     "kernel_ms": dom["ms_avg"], "launches": dom["launches"], "peak_basis": dom["peak_basis"],
+                     "note": "dominant matrix kernel of the timed cycle: algorithmic fp32 FLOPs (2*R*3H*(H+Kx) per "
+                             "GRU call, 2*M*N*K per GEMM) / its launches' summed duration (HIP events on the launch "
+                             "stream); rocprofv3 trace of the same leg, timed-cycle slice: profiles/r02_mappo_uf100-430_slice.json"},
+        "kernels": kernels,
+        "issued_gemm_tflops_over_cycle": gemm_tflops,
+        "dtype": "f32 (fp32 accumulate; bf16x3 split MFMAs for the dominant products)",
         "solve_rate": met["solve_rate"],
         "peak_hbm_gb": torch.cuda.max_memory_allocated() / 1e9,
     }
@@ -298,11 +341,17 @@ def env_leg(args, rank, world, dist):
         e0 = classes[0]
         lanes = int(os.environ.get("MARLSAT_ENV_THREADS", "0")) or env_lanes(e0.num_agents, 2 * e0.num_vars + e0.num_clauses)
         kernel = f"env_kernel<2,{'int' if obs_dtype == torch.int32 else 'signed char'},{lanes}>"
+    # steady state: the episode-step counters start uniform over [0, MAX_STEPS), so ~B/512 envs time
+    # out (and auto-reset: new pool instance + assignment drawn in-kernel) in every launch, as in a
+    # long-running rollout; a fresh reset would keep the reset branch idle for 511 steps
+    for st in states:
+        st.step.copy_(torch.randint(0, 512, (st.num_envs,), generator=gen, device="cuda", dtype=torch.int32))
     counter = 1
     for i in range(args.warmup):
         step(i, counter)
         counter += 1
     torch.cuda.synchronize()
+    step_before = [st.step.clone() for st in states]
     K = args.steps
     # HIP events on the kernel's stream (torch's current stream) bracket the whole timed region:
     # the launches run back to back, so span / K is the mean launch duration.  (An event pair
@@ -339,6 +388,10 @@ def env_leg(args, rank, world, dist):
     for e, st in zip(classes, states):
         assert torch.equal(e.num_clauses - st.clauses_satisfied_status.int().sum(1), st.num_unsatisfied)
     done_frac = float(torch.cat([o["done"].float() for o in outs]).mean())
+    # envs that auto-reset inside the timed region (at most once each: K < MAX_STEPS): their counter
+    # restarted, so it ends below K; the others advanced by exactly K
+    resets = int(sum(int((st.step < K).sum()) for st in states))
+    assert all(bool(((st.step < K) | (st.step == sb + K)).all()) for st, sb in zip(states, step_before))
     per_class = []
     launch_bytes = 0
     for name, e, b in zip(names, classes, sizes):
@@ -350,7 +403,7 @@ def env_leg(args, rank, world, dist):
                           "num_agents": e.num_agents, "vars_per_agent": WORKLOADS[name][2], "envs_per_gpu": b,
                           "algorithmic_bytes_per_env_step": pe})
     return {"names": names, "sizes": sizes, "elapsed": elapsed, "kern_ms": kern_ms, "K": K, "kernel": kernel,
-            "launch_bytes": launch_bytes, "per_class": per_class, "done_frac": done_frac}
+            "launch_bytes": launch_bytes, "per_class": per_class, "done_frac": done_frac, "resets": resets}
 
 
 def main():
@@ -364,9 +417,9 @@ def main():
     ap.add_argument("--pool", type=int, default=1024, help="problem instances in the pool")
     ap.add_argument("--obs-dtype", default="int32", choices=["int32", "int8"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline per core (0: skip)")
-    ap.add_argument("--mappo-workload", default="uf50-218", choices=sorted(WORKLOADS))
-    ap.add_argument("--mappo-envs", type=int, default=1024, help="envs per GPU in the MAPPO leg")
-    ap.add_argument("--mappo-T", type=int, default=32, help="NUM_STEPS of the MAPPO leg (0: skip the leg)")
+    ap.add_argument("--mappo", default="uf100-430:4096:8,uf50-218:1024:32",
+                    help="MAPPO legs 'workload:envs_per_gpu:NUM_STEPS,...' ('' skips); the first is the headline "
+                         "(the metric's 4096 envs, BASELINE config 3), the others are reported beside it")
     ap.add_argument("--mappo-micro-gb", type=float, default=240.0, help="activation budget per PPO micro-batch")
     args = ap.parse_args()
 
@@ -409,9 +462,14 @@ def main():
             dist.init_process_group(backend)
 
     r = env_leg(args, rank, world, dist)
-    mappo = mappo_bench(args, rank, world, dist) if args.mappo_T > 0 else None
+    legs = []
+    for spec in filter(None, args.mappo.split(",")):
+        wl, envs, T = spec.split(":")
+        legs.append(mappo_bench(args, rank, world, dist, wl, int(envs), int(T)))
+    mappo = legs[0] if legs else None
     if mappo is not None and rank == 0 and world == 1 and args.cpu_budget > 0:
-        mappo["cpu_baseline"] = mappo_cpu_baseline(args.mappo_workload, budget_s=min(10.0, args.cpu_budget))
+        wl0 = mappo["config"]["workload"]
+        mappo["cpu_baseline"] = mappo_cpu_baseline(wl0, budget_s=min(10.0, args.cpu_budget))
 
     if rank == 0:
         B, K, elapsed, kern_ms = sum(r["sizes"]), r["K"], r["elapsed"], r["kern_ms"]
@@ -462,7 +520,10 @@ def main():
             },
             "cpu_baseline": cpu,
             "mappo": mappo,
+            "mappo_other_legs": legs[1:],
             "done_fraction_last_step": r["done_frac"],
+            "auto_resets_in_timed_region": r["resets"],
+            "steady_state": "episode-step counters staggered uniformly over [0, 512) before warm-up",
         }
         print(json.dumps(rec), flush=True)
     if dist is not None:

@@ -125,9 +125,25 @@ class GNNActorCritic:
 
     flops = 0  # matmul FLOPs issued (2*M*N*K per GEMM), for the MFMA roofline
 
+    # bench.py's per-kernel roofline: a dict makes the MFMA kernels' launches record
+    # {label: [(start event, end event, fp32-equivalent algorithmic FLOPs)]} on the launch stream
+    ktimer: Optional[dict] = None
+
+    def _timed(self, label: str, flop: float, call):
+        kt = GNNActorCritic.ktimer
+        if kt is None:
+            return call()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = call()
+        e1.record()
+        kt.setdefault(label, []).append((e0, e1, float(flop)))
+        return r
+
     def _gemm(self, A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc=0):
         GNNActorCritic.flops += 2 * M * N * K
-        _chk(L_.msat_gemm(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, self.stream), "msat_gemm")
+        self._timed("msat_gemm (fp32 MFMA)", 2.0 * M * N * K, lambda: _chk(
+            L_.msat_gemm(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, self.stream), "msat_gemm"))
 
     def _gemm64(self, A, lda, transA, B, ldb, transB, C, ldc, M, N, K, acc=0):
         """fp64-accumulated small product, one rounding per element (the folded weights, gemm.hip)."""
@@ -163,14 +179,17 @@ class GNNActorCritic:
             self._gemm(A, lda, Wm.data_ptr(), K, 1, C, ldc, None, M, N, K, acc)
             return
         GNNActorCritic.flops += 2 * M * N * K
-        _chk(L_.msat_gemm_x3(A, lda, planes.data_ptr(), C, ldc, None, M, N, K, acc, self.stream), "msat_gemm_x3")
+        self._timed("gemm_x3r16_kernel (dgrad, bf16x3)", 2.0 * M * N * K, lambda: _chk(
+            L_.msat_gemm_x3(A, lda, planes.data_ptr(), C, ldc, None, M, N, K, acc, self.stream), "msat_gemm_x3"))
 
     def _wgrad(self, A, lda, G, ldg, W, ldw, M, K, N, acc=1):
         if M == 0:
             return
         GNNActorCritic.flops += 2 * M * N * K
         ws = self.scr.get_ws(int(L_.msat_gemm_wgrad_workspace_bytes(M, K, N)))
-        _chk(L_.msat_gemm_wgrad(A, lda, G, ldg, W, ldw, M, K, N, acc, ws.data_ptr(), self.stream), "msat_gemm_wgrad")
+        label = "wgrad_skinny + reduce (K <= 8)" if K <= 8 else "wgrad_x3_kernel + reduce (bf16x3)"
+        self._timed(label, 2.0 * M * N * K, lambda: _chk(
+            L_.msat_gemm_wgrad(A, lda, G, ldg, W, ldw, M, K, N, acc, ws.data_ptr(), self.stream), "msat_gemm_wgrad"))
 
     def _colsum(self, G, ldg, M, N, out, acc=1):
         if M == 0:
@@ -214,13 +233,14 @@ class GNNActorCritic:
         GNNActorCritic.flops += 2 * R * 3 * H * (H + (kx + 15) // 16 * 16)
         (p0, l0, w0), (p1, l1, w1), (p2, l2, w2) = segs
         if isinstance(wt, dict) and wt.get("x3r"):  # register-A kernel: W^T planes {"wi": (planes, kxp), "wh"}
-            _chk(L_.msat_gru_ln_fused_fwd_x3r(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
-                                              wt["wi"][0].data_ptr(), wt["wi"][1],
-                                              self.p(f"enc.{cell}_bi").data_ptr(), wt["wh"].data_ptr(),
-                                              self.p(f"enc.{cell}_bh").data_ptr(), self._ptr(ln_row),
-                                              self._ptr(ln_row, H), out.data_ptr(), H,
-                                              g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
-                 "msat_gru_ln_fused_fwd_x3r")
+            self._timed("gru_ln_fused_fwd_x3r_kernel (bf16x3)", 2.0 * R * 3 * H * (H + kx), lambda: _chk(
+                L_.msat_gru_ln_fused_fwd_x3r(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
+                                             wt["wi"][0].data_ptr(), wt["wi"][1],
+                                             self.p(f"enc.{cell}_bi").data_ptr(), wt["wh"].data_ptr(),
+                                             self.p(f"enc.{cell}_bh").data_ptr(), self._ptr(ln_row),
+                                             self._ptr(ln_row, H), out.data_ptr(), H,
+                                             g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
+                "msat_gru_ln_fused_fwd_x3r"))
             return
         if isinstance(wt, dict):  # bf16x3 planes {"wi": (planes, kxp), "wh": planes}
             _chk(L_.msat_gru_ln_fused_fwd_x3(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,

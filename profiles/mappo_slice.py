@@ -1,0 +1,37 @@
+"""Per-kernel durations of the bench's TIMED MAPPO cycle from a rocprofv3 kernel trace, to set beside
+the bench's own HIP-event numbers (bench.py "mappo" -> "kernels").
+
+The timed cycle (rollout, GAE, PPO epochs, metrics) is the last GPU work of a bench run with one
+MAPPO leg and --cpu-budget 0, so its launches of a kernel are that kernel's LAST n launches in the
+trace, n = the launch count the bench reports.  Writes a JSON summary (run on the GPU box):
+    python3 profiles/mappo_slice.py <kernel_trace.csv> <bench stdout> <out.json>"""
+import csv
+import json
+import sys
+
+trace, bench_log, out = sys.argv[1:4]
+line = next(l for l in open(bench_log) if l.startswith("{") and '"mappo"' in l)
+bench = json.loads(line)["mappo"]
+ROCPROF_NAMES = {  # bench label -> rocprof kernel names whose launches the bench's event pair brackets
+    "gru_ln_fused_fwd_x3r_kernel (bf16x3)": ["gru_ln_fused_fwd_x3r_kernel"],
+    "gemm_x3r16_kernel (dgrad, bf16x3)": ["gemm_x3r16_kernel"],
+    "wgrad_x3_kernel + reduce (bf16x3)": ["wgrad_x3_kernel", "wgrad_reduce4_kernel"],
+}
+launches = {}
+for r in csv.DictReader(open(trace)):
+    launches.setdefault(r["Kernel_Name"], []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+res = {"bench_config": bench["config"], "kernels": []}
+for k in bench["kernels"]:
+    names = ROCPROF_NAMES.get(k["kernel"])
+    if not names:
+        continue
+    n, tot = k["launches"], 0.0
+    for nm in names:
+        rows = sorted(v for key, vals in launches.items() if nm in key for v in vals)
+        last = rows[-n:]
+        tot += sum(e - s for s, e in last) / len(last) / 1e6
+    res["kernels"].append({"kernel": k["kernel"], "launches": n, "bench_event_ms_avg": k["ms_avg"],
+                           "rocprof_ms_avg_last_n": tot, "ratio": k["ms_avg"] / tot,
+                           "bench_tflops_fp32_equiv": k["tflops_fp32_equiv"], "bench_frac": k["frac"]})
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 workload = sys.argv[2] if len(sys.argv) > 2 else "uf200-860/B4096/int32"
 prof = os.path.join(ROOT, "gpurun_out", "prof")
-KERNEL = "env_kernel<2"
+KERNEL = sys.argv[3] if len(sys.argv) > 3 else "env_kernel<2, int, 512>"  # the uf200 x 4096 instantiation
 
 def counter(path, name):
     rows = [r for r in csv.DictReader(open(path)) if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == name]
