@@ -192,6 +192,8 @@ def kernel_table(ktimer: dict) -> list:
         fl = sum(f for _, _, f in recs)
         if "K <= 8" in label:
             peak, unit_note = None, "HBM-bound (K <= 8 columns), not priced against a matrix peak"
+        elif "fp16x2" in label:
+            peak, unit_note = BF16_MFMA_PEAK_TFLOPS / 3.0, "fp16 dense peak (= bf16) / 3 (three fp16 MFMAs per fp32 product)"
         elif "bf16x3" in label:
             peak, unit_note = X3_PEAK_TFLOPS, "bf16 dense peak / 6 (six bf16 MFMAs per fp32 product)"
         else:

@@ -139,6 +139,22 @@ int msat_gru_ln_fused_fwd_x3r(const float *x0, int32_t ld0, int32_t w0, const fl
 /* planes[q][n][k] = bf16x3 part q of (k < K ? W[k][n] : 0) for n < N, k < Kp: the transposed,
  * zero-padded split of a (K, N) weight (row stride ldw) for msat_gru_ln_fused_fwd_x3r. */
 int msat_split_bf16x3_t(const float *W, int32_t K, int32_t N, int32_t ldw, int32_t Kp, void *planes, void *stream);
+/* The same GRU cell with fp16x2 operands (x = x1 + x2, three fp16 MFMAs per product instead of six
+ * bf16 ones; weights from msat_split_f16x2_t, scaled by 2^10).  fp16's range is checked per 128-row
+ * tile: a tile whose activations reach |a| >= 2^15, or every tile when a weight split flagged wbad[0]
+ * (wi) or wbad[1] (wh), is recomputed by the bf16x3 kernel from wiT_x3 / whT_x3 (msat_split_bf16x3_t
+ * planes) in a second launch on the same stream.  tile_flags: >= ceil(R / 128) ints of workspace. */
+int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
+                              const float *x2, int32_t ld2, int32_t w2, const float *hprev, int32_t ldp,
+                              const void *wiT_h2, const void *whT_h2, const void *wiT_x3, const void *whT_x3,
+                              int32_t kxp, const float *bi, const float *bh, const float *ln_scale,
+                              const float *ln_bias, float *out, int32_t ldo, float *g4, int32_t ldg, int32_t R,
+                              int32_t H, int32_t *tile_flags, const int32_t *wbad, void *stream);
+/* planes[q][n][k] = fp16x2 part q of 2^10 (k < K ? W[k][n] : 0) (n < N, k < Kp) for
+ * msat_gru_ln_fused_fwd_h2r; *bad (device int, cleared first) = 1 if a scaled weight is not in
+ * (-2^15, 2^15). */
+int msat_split_f16x2_t(const float *W, int32_t K, int32_t N, int32_t ldw, int32_t Kp, void *planes, int32_t *bad,
+                       void *stream);
 /* msat_gru_ln_bwd from the fused forward's g4 tape (same outputs).  dbi (3H) / dbh_n (H), both
  * or neither, receive (+=) the gate-bias gradients sum_rows dGi and sum_rows dGh[:, 2H:3H]
  * (b_ir|b_iz|b_in and b_hn) from the same pass.  partial >= msat_gru_ln_bwd_partial_floats.

@@ -514,19 +514,6 @@ constexpr int kXR = 128;  // rows per workgroup (x3 kernel)
 #ifndef MSAT_GRU_ABL
 #define MSAT_GRU_ABL 0
 #endif
-// x3r kernel: 1 = tape stored straight from the accumulators (measured 0-4 % faster), 0 = float4
-// rows staged through LDS
-// x3r kernel: 1 = activations loaded two steps ahead by asm, split among the previous step's MFMAs
-#ifndef MSAT_GRU_X3R_BPIPE
-#define MSAT_GRU_X3R_BPIPE 1
-#endif
-#ifndef MSAT_GRU_X3R_PIPE
-#define MSAT_GRU_X3R_PIPE 1
-#endif
-#ifndef MSAT_GRU_TAPE_DIRECT
-#define MSAT_GRU_TAPE_DIRECT 1
-#endif
-
 // 16 waves x 32 rows (RS = 4, RT = 1).
 //
 // Pipeline: every global read of the loop is an LDS-DMA issued from asm (glds16_async*), so the
@@ -701,17 +688,25 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Register-A bf16x3 form on v_mfma_f32_16x16x32_bf16 (msat_gru_ln_fused_fwd_x3r, H = 128).
-// 128-row tile, 8 waves; wave w owns rows 16 w .. 16 w + 15 and ALL 128 units of all four gates
-// (acc[gate][8 column tiles of 16], 128 accumulator registers), so its activation rows are private:
-// lane l needs A[l & 15][k0 + 8 (l >> 4) + j] of a 32-deep k step, two float4 loads straight from
-// the row into registers, split in registers.  Only the weights go through LDS: transposed planes
-// W^T [3 planes][3H][Kp] (msat_split_bf16x3_t, Kp % 32 == 0) arrive by LDS-DMA as per-(plane, gate)
-// images [128 units][4 chunks of 8 k] (64-byte rows, chunk c at slot c ^ f((u >> 2) & 3),
-// f = {0, 2, 3, 1}: conflict-free ds_read_b128 for this lane map), 72 KiB per step, double-buffered.
-// One barrier per 32 k.  The gate algebra is lane-local; LayerNorm row sums reduce over the 8
-// column tiles in-lane and the 16 lanes of a row group by shuffles; the tape and h' leave as
-// float4 rows staged per wave in LDS.
+// Register-A GRU forward, fp16x2 operands on v_mfma_f32_16x16x32_f16 (msat_gru_ln_fused_fwd_h2r,
+// H = 128).  The structure of the bf16x3 register-A kernel below (gru_ln_fused_fwd_x3r_kernel): 128-row
+// tile, 8 waves; wave w owns rows 16 w .. 16 w + 15 and ALL 128 units of all four gates (acc[gate][8
+// column tiles of 16], 128 accumulator registers), so its activation rows are private and go straight
+// from HBM to registers, split there; only the weights go through LDS, transposed planes
+// W^T [2][3H][Kp] (Kp % 32 == 0) by LDS-DMA as per-(plane, gate) images [128 units][4 chunks of 8 k]
+// (64-byte rows, chunk c at slot c ^ f((u >> 2) & 3), f = {0, 2, 3, 1}), double-buffered.
+//
+// Operands: x = x1 + x2, x1 = fp16(x), x2 = fp16(x - x1) (22 significant bits, x - x1 exact); the
+// weights are scaled by 2^kH2Shift before their split (msat_split_f16x2_t) and the sums by 2^-kH2Shift
+// after (both exact).  Three MFMAs per (gate, column tile) block, a1b2 a2b1 a1b1; the dropped a2b2 and
+// the representation residuals are <= 3 * 2^-22 |ab| per product, under the fp32 accumulation error of
+// a 288..416-deep dot product (tests/test_gnn_gpu.py at L = 16 bounds the network against the fp32 CPU
+// oracle).  Against bf16x3: half the MFMAs (3 vs 6), 48 instead of 72 KiB of weights per step.
+// fp16's range is checked, not assumed: a tile that loads an activation with |a| >= 2^15, or whose
+// weights overflowed at the split (wbad), writes flags[tile] = 1 and no output, and the bf16x3 kernel,
+// launched next with the same flags, recomputes exactly the flagged tiles.
+constexpr int kH2Shift = 10;  // weight scale 2^10: |W| < 32 fits, |W| >= 2^-24 keeps 11 bits
+
 __device__ __forceinline__ int gswz16(int b) { return (0x1E >> (2 * b)) & 3; }  // {0, 2, 3, 1}
 
 struct GruX3rArgs {
@@ -721,20 +716,293 @@ struct GruX3rArgs {
     const float *hp;
     int ldp;
     const float *bi, *bh, *ln_scale, *ln_bias;
-    const __bf16 *wiT, *whT;  // [3][3H][kxp] / [3][3H][H]
-    int kxp;                  // multiple of 32
+    const uint16_t *wiT, *whT;  // [planes][3H][kxp] / [planes][3H][H] (bf16 x3 or fp16 x2 bits)
+    int kxp;                    // multiple of 32
     float *out;
     int ldo;
     float *g4;
     int ldg;
     int R, Kx;
+    int *flags;        // h2r: per-tile overflow flag (written); x3r: tiles to recompute (nullptr: all)
+    const int *wbad;   // h2r: weight-split overflow flags [2] (wi, wh)
 };
 
 typedef float f32x4g __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+struct SplitH8 {
+    uint4 p[2];
+};
+
+__device__ __forceinline__ SplitH8 splith8(const float4 &u, const float4 &v) {
+    const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+    f16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const _Float16 a = (_Float16)x[j];
+        h[j] = a;
+        l[j] = (_Float16)(x[j] - (float)a);
+    }
+    SplitH8 s;
+    s.p[0] = __builtin_bit_cast(uint4, h);
+    s.p[1] = __builtin_bit_cast(uint4, l);
+    return s;
+}
+
+__device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f32x4g &c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+}
+
+__device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
+    constexpr int H = 128, IMG = H * 4;  // uint4 per (plane, gate) image: 128 units x 4 chunks = 8 KiB
+    constexpr int NI = 6;                // (plane, gate) images per step
+    __shared__ uint4 Bs[2 * NI * IMG];  // 96 KiB, double-buffered
+    const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int row0 = tile * 128, wr = 16 * w;
+    if (a.wbad[0] | a.wbad[1]) {  // weights out of fp16 range: the bf16x3 launch does every tile
+        if (t == 0) a.flags[tile] = 1;
+        return;
+    }
+    const int arow = row0 + wr + l16, arc = arow < a.R ? arow : a.R - 1;
+    constexpr int nsh = H / 32;
+    const int ns = nsh + a.kxp / 32;
+    const float *const hp = a.hp, *const sg0 = a.seg[0], *const sg1 = a.seg[1], *const sg2 = a.seg[2];
+    const int w0 = a.seg_w[0], w01 = a.seg_w[0] + a.seg_w[1], kx_end = a.Kx;
+    const unsigned ro0 = (unsigned)arc * (unsigned)a.seg_ld[0], ro1 = (unsigned)arc * (unsigned)a.seg_ld[1],
+                   ro2 = (unsigned)arc * (unsigned)a.seg_ld[2];
+    const float *const hrow = hp + (size_t)arc * a.ldp + 8 * g;
+    // weight DMA: 8 NI wave-instructions (1 KiB = 16 units x 4 chunks) per step, NI per wave;
+    // instruction e of wave w fills image x = (NI w + e) / 8 (plane * 3 + gate), units 16 p .. 16 p + 15
+    // (p = (NI w + e) % 8).  Lane -> unit 16 p + (lane >> 2), LDS chunk lane & 3 = source chunk
+    // (lane & 3) ^ f((lane >> 4) & 3).
+    const unsigned lpart = (unsigned)(lane >> 2) * 2u, chb = 16u * ((lane & 3) ^ gswz16((lane >> 4) & 3));
+    auto issueW = [&](int s, int buf) {
+        const bool hid = s < nsh;
+        const uint16_t *W = hid ? a.whT : a.wiT;
+        const int Kp = hid ? H : a.kxp;
+        const int k0 = hid ? 32 * s : 32 * (s - nsh);
+        const unsigned voff = lpart * (unsigned)Kp + chb;
+#pragma unroll
+        for (int e = 0; e < NI; ++e) {
+            const int x = NI * w + e, img = x >> 3, p = x & 7, q = img / 3, gt = img - 3 * q;
+            const uint16_t *base = W + ((size_t)q * 3 * H + gt * H + 16 * p) * Kp + k0;
+            glds16_async_s(base, voff, &Bs[(buf * NI + img) * IMG + 64 * p]);
+        }
+    };
+    f32x4g acc[4][8];
+#pragma unroll
+    for (int G = 0; G < 4; ++G)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[G][j] = f32x4g{};
+    const int slot = g ^ gswz16((l16 >> 2) & 3);
+    float amax = 0.f;  // largest |activation| this lane split (range check)
+    // Activation loads by asm (invisible to hipcc's wait insertion) two steps ahead into alternating
+    // register sets; the split of step s + 1 runs among step s's MFMAs; one vmcnt(0) + barrier per
+    // step (the weights of s + 1 and the activations of s + 2, both issued at the start of step s,
+    // have landed).  The wait names the set just loaded as an in/out operand, so no use of it is
+    // scheduled above the wait.
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v ras[2][2];  // [set = step & 1][half]
+    auto aptr = [&](int st, int e) -> const float * {
+        if (st < nsh) return hrow + 32 * st + 4 * e;
+        const int kx = (st - nsh) * 32 + 8 * g + 4 * e;
+        const float *q0 = sg0 + (ro0 + (unsigned)(kx < w0 ? kx : 0));
+        const float *q1 = sg1 + (ro1 + (unsigned)(kx - w0));
+        const float *q2 = sg2 + (ro2 + (unsigned)(kx - w01));
+        return (kx >= w01 && kx < kx_end) ? q2 : ((kx >= w0 && kx < w01) ? q1 : q0);
+    };
+    auto aload = [&](int st, f4v (&r)[2]) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[e]) : "v"(aptr(st, e)) : "memory");
+    };
+    auto await0 = [&](f4v (&r)[2]) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]) :: "memory"); };
+    auto asplit = [&](int st, const f4v (&r)[2], uint4 (&f)[2]) {  // branch-free (selects)
+        const int kx = (st - nsh) * 32 + 8 * g;
+        const bool z0 = st >= nsh && kx >= kx_end, z1 = st >= nsh && kx + 4 >= kx_end;
+        const f4v zero = {0.f, 0.f, 0.f, 0.f};
+        const float4 v0 = __builtin_bit_cast(float4, z0 ? zero : r[0]);
+        const float4 v1 = __builtin_bit_cast(float4, z1 ? zero : r[1]);
+        const float m0 = fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w)));
+        const float m1 = fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w)));
+        amax = fmaxf(amax, fmaxf(m0, m1));
+        const SplitH8 sp = splith8(v0, v1);
+        f[0] = sp.p[0];
+        f[1] = sp.p[1];
+    };
+    uint4 fas[2][2];  // split activations of step s in fas[s & 1]
+    aload(0, ras[0]);
+    if (ns > 1) aload(1, ras[1]);
+    issueW(0, 0);
+    await0(ras[0]);
+    await0(ras[1]);
+    asplit(0, ras[0], fas[0]);
+    barrier_lds();
+    auto pstep = [&](int st, auto hidc, auto parc) {
+        constexpr bool hid = decltype(hidc)::value;
+        constexpr int PB = decltype(parc)::value;  // st & 1
+        const int buf = PB;
+        if (st + 1 < ns) issueW(st + 1, buf ^ 1);
+        if (st + 2 < ns) aload(st + 2, ras[PB]);
+        // weight fragments carried across the 24 (gate, column tile) blocks: each plane is re-read
+        // for the next block as soon as its last MFMA here has issued, so the reads fly under the
+        // MFMAs instead of each block waiting for its own reads (at 255 VGPRs the compiler had
+        // issued every block's reads just before its MFMAs and waited on them).
+        auto bfrag = [&](int n, int q) {
+            const int gt = n >> 3, j = n & 7;
+            return Bs[(buf * NI + q * 3 + gt) * IMG + (16 * j + l16) * 4 + slot];
+        };
+        uint4 (&fa)[2] = fas[PB];
+        {
+            uint4 b0 = bfrag(0, 0), b1 = bfrag(0, 1);
+#pragma unroll
+            for (int n = 0; n < 24; ++n) {
+                const int gt = n >> 3, j = n & 7;
+                const int G = gt < 2 ? gt : (hid ? 3 : 2);
+                f32x4g c = acc[G][j];
+                c = h2mma(fa[0], b1, c);  // a1 b2
+                if (n + 1 < 24) b1 = bfrag(n + 1, 1);
+                c = h2mma(fa[1], b0, c);  // a2 b1
+                c = h2mma(fa[0], b0, c);  // a1 b1
+                if (n + 1 < 24) b0 = bfrag(n + 1, 0);
+                acc[G][j] = c;
+                if (n == 7) asplit(st + 1, ras[PB ^ 1], fas[PB ^ 1]);
+                __builtin_amdgcn_sched_barrier(0);  // keep the blocks in order (the reads lead by one)
+            }
+        }
+        await0(ras[PB]);
+        barrier_lds();
+    };
+    {
+        int st = 0;
+#pragma unroll 1
+        for (; st + 1 < nsh; st += 2) {
+            pstep(st, std::true_type{}, std::integral_constant<int, 0>{});
+            pstep(st + 1, std::true_type{}, std::integral_constant<int, 1>{});
+        }
+        // nsh = 4 is even: the input steps start at parity 0
+#pragma unroll 1
+        for (; st + 1 < ns; st += 2) {
+            pstep(st, std::false_type{}, std::integral_constant<int, 0>{});
+            pstep(st + 1, std::false_type{}, std::integral_constant<int, 1>{});
+        }
+        if (st < ns) pstep(st, std::false_type{}, std::integral_constant<int, 0>{});
+    }
+    {  // range check: |a| < 2^15 keeps a1 = fp16(a) finite with margin
+        const int bad = __syncthreads_or(!(amax < 32768.0f));
+        if (t == 0) a.flags[tile] = bad;
+        if (bad) return;
+    }
+
+    // ---- epilogue.  C/D map: unit u = 16 j + l16, row wr + 4 g + reg.
+    float *stage = reinterpret_cast<float *>(Bs) + w * 16 * 132;  // [16 rows][132] per wave
+    const bool tape = a.g4 != nullptr;
+    // h of each accumulator's (row, unit), loaded before the tape stores (vector-memory counts retire
+    // in issue order, so a load issued after them would wait for them)
+    float hv[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = row0 + wr + 4 * g + r;
+            hv[j][r] = hp[(size_t)(row < a.R ? row : a.R - 1) * a.ldp + 16 * j + l16];
+        }
+    constexpr float sc = 1.0f / (float)(1 << kH2Shift);  // exact power of two
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int u = 16 * j + l16;
+        const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
+        const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            acc[0][j][r] = acc[0][j][r] * sc + br;
+            acc[1][j][r] = acc[1][j][r] * sc + bz;
+            acc[2][j][r] = acc[2][j][r] * sc + bni;
+            acc[3][j][r] = acc[3][j][r] * sc + bnh;
+        }
+    }
+    // float4 rows of the wave's [16][128] stage -> dst (row stride ld), rows < R only.  The stage is
+    // wave-private and a wave's LDS operations complete in issue order, so waiting for its own stage
+    // writes (lgkmcnt) is the only ordering needed: no workgroup barrier, whose release fence would
+    // also drain the wave's global stores.
+    auto flush = [&](float *dst, int ld) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int rr = 2 * it + (lane >> 5), c4 = lane & 31;
+            const float4 v = *reinterpret_cast<const float4 *>(stage + rr * 132 + 4 * c4);
+            const int row = row0 + wr + rr;
+            if (row < a.R) *reinterpret_cast<float4 *>(dst + (size_t)row * ld + 4 * c4) = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    if (tape) {
+        // pre-activations straight from the accumulators (16 lanes x 4 B per row segment; staging them
+        // through LDS as float4 rows measured 0-4 % slower)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = row0 + wr + 4 * g + r;
+            if (row < a.R) {
+                float *q = a.g4 + (size_t)row * a.ldg + l16;
+#pragma unroll
+                for (int G = 0; G < 4; ++G)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) q[G * H + 16 * j] = acc[G][j][r];
+            }
+        }
+    }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float rg = fsig_fast(acc[0][j][r]), zg = fsig_fast(acc[1][j][r]);
+            const float ng = ftanh_fast(acc[2][j][r] + rg * acc[3][j][r]);
+            const float hn = (1.0f - zg) * ng + zg * hv[j][r];
+            acc[0][j][r] = hn;
+            s1[r] += hn;
+            s2[r] += hn * hn;
+        }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            s1[r] += __shfl_xor(s1[r], o, 16);
+            s2[r] += __shfl_xor(s2[r], o, 16);
+        }
+    float mean[4], rs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        mean[r] = s1[r] / (float)H;
+        const float var = fmaxf(s2[r] / (float)H - mean[r] * mean[r], 0.0f);
+        rs[r] = rsqrtf(var + 1e-6f);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int u = 16 * j + l16;
+        const float scl = a.ln_scale[u], lb = a.ln_bias[u];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            stage[(4 * g + r) * 132 + u] = (acc[0][j][r] - mean[r]) * (rs[r] * scl) + lb;
+    }
+    flush(a.out, a.ldo);
+}
+
+__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2r_kernel(GruX3rArgs a) {
+    gru_h2r_tile(a, blockIdx.x);
+}
+
+// bf16x3 register-A kernel (the template above is fp16x2-only: instantiated for bf16x3 it computed
+// wrong results; this is the round-1 kernel, unchanged).  Pipeline switches: activations loaded two
+// steps ahead by asm, weight fragments carried across column blocks, tape stored from the accumulators.
+#define MSAT_GRU_X3R_BPIPE 1
+#define MSAT_GRU_X3R_PIPE 1
+#define MSAT_GRU_TAPE_DIRECT 1
 __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs a) {
     constexpr int H = 128, IMG = H * 4;  // uint4 per (plane, gate) image: 128 units x 4 chunks = 8 KiB
     __shared__ uint4 Bs[2][9][IMG];      // [buf][plane * 3 + gate], 144 KiB
+    if (a.flags && a.flags[blockIdx.x] == 0) return;  // fixup launch: only the tiles the fp16x2 kernel flagged
     const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int row0 = blockIdx.x * 128, wr = 16 * w;
@@ -770,7 +1038,7 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
     const unsigned lpart = (unsigned)(lane >> 2) * 2u, chb = 16u * ((lane & 3) ^ gswz16((lane >> 4) & 3));
     auto issueW = [&](int s, int buf) {
         const bool hid = s < nsh;
-        const __bf16 *W = hid ? a.whT : a.wiT;
+        const __bf16 *W = reinterpret_cast<const __bf16 *>(hid ? a.whT : a.wiT);
         const int Kp = hid ? H : a.kxp;
         const int k0 = hid ? 32 * s : 32 * (s - nsh);
         const unsigned voff = lpart * (unsigned)Kp + chb;
@@ -1089,6 +1357,22 @@ __global__ void split_bf16x3_t_kernel(const float *__restrict__ W, int K, int N,
     }
 }
 
+// planes[q][n][k] = part q of 2^kH2Shift (k < K ? W[k][n] : 0): the transposed, zero-padded fp16x2 split
+// (x1 = fp16(x), x2 = fp16(x - x1)) for the h2r GRU kernel; *bad = 1 if a scaled weight is outside
+// (-2^15, 2^15) (or not finite): the GRU launch then recomputes every tile in bf16x3.
+__global__ void split_f16x2_t_kernel(const float *__restrict__ W, int K, int N, int ldw, int Kp,
+                                     _Float16 *__restrict__ out, int *__restrict__ bad) {
+    const size_t n = (size_t)N * Kp;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t c = i / Kp, k = i - c * Kp;
+        const float x = k < (size_t)K ? W[k * ldw + c] * (float)(1 << kH2Shift) : 0.0f;
+        const _Float16 p = (_Float16)x;
+        out[i] = p;
+        out[n + i] = (_Float16)(x - (float)p);
+        if (!(fabsf(x) < 32768.0f)) *bad = 1;
+    }
+}
+
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace msat
@@ -1282,35 +1566,32 @@ extern "C" int msat_split_bf16x3_t(const float *W, int32_t K, int32_t N, int32_t
     return check_launch("split_bf16x3_t_kernel");
 }
 
-extern "C" int msat_gru_ln_fused_fwd_x3r(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1,
-                                         int32_t w1, const float *x2, int32_t ld2, int32_t w2, const float *hprev,
-                                         int32_t ldp, const void *wiT_planes, int32_t kxp, const float *bi,
-                                         const void *whT_planes, const float *bh, const float *ln_scale,
-                                         const float *ln_bias, float *out, int32_t ldo, float *g4, int32_t ldg,
-                                         int32_t R, int32_t H, void *stream) {
-    MSAT_REQUIRE(H == 128, "gru_ln_fused_fwd_x3r: H must be 128 (got %d)", H);
-    MSAT_REQUIRE(R >= 0, "gru_ln_fused_fwd_x3r: R < 0");
-    if (R == 0) return MSAT_OK;
-    MSAT_REQUIRE(x0 && hprev && wiT_planes && bi && whT_planes && bh && ln_scale && ln_bias && out, "NULL pointer");
-    MSAT_REQUIRE(ldo >= H && ldp >= H && (!g4 || ldg >= 4 * H), "gru_ln_fused_fwd_x3r: bad dims");
+static int gru_r_args(GruX3rArgs &a, const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
+                      const float *x2, int32_t ld2, int32_t w2, const float *hprev, int32_t ldp, const void *wiT,
+                      int32_t kxp, const float *bi, const void *whT, const float *bh, const float *ln_scale,
+                      const float *ln_bias, float *out, int32_t ldo, float *g4, int32_t ldg, int32_t R, int32_t H) {
+    MSAT_REQUIRE(H == 128, "gru_ln_fused_fwd_x3r/h2r: H must be 128 (got %d)", H);
+    MSAT_REQUIRE(R > 0, "gru_ln_fused_fwd_x3r/h2r: R <= 0");
+    MSAT_REQUIRE(x0 && hprev && wiT && bi && whT && bh && ln_scale && ln_bias && out, "NULL pointer");
+    MSAT_REQUIRE(ldo >= H && ldp >= H && (!g4 || ldg >= 4 * H), "gru_ln_fused_fwd_x3r/h2r: bad dims");
     const float *seg[3] = {x0, x1, x2};
     const int lds_[3] = {ld0, ld1, ld2}, ws[3] = {w0, w1, w2};
     int Kx = 0;
     for (int g = 0; g < 3; ++g) {
-        MSAT_REQUIRE(ws[g] >= 0 && ws[g] % 4 == 0, "gru_ln_fused_fwd_x3r: segment %d width %d must be a multiple of 4",
-                     g, ws[g]);
+        MSAT_REQUIRE(ws[g] >= 0 && ws[g] % 4 == 0,
+                     "gru_ln_fused_fwd_x3r/h2r: segment %d width %d must be a multiple of 4", g, ws[g]);
         if (ws[g] == 0) continue;
         MSAT_REQUIRE(seg[g] && aligned16(seg[g]) && lds_[g] % 4 == 0 && lds_[g] >= ws[g],
-                     "gru_ln_fused_fwd_x3r: segment %d must be 16-byte aligned with ld %% 4 == 0", g);
+                     "gru_ln_fused_fwd_x3r/h2r: segment %d must be 16-byte aligned with ld %% 4 == 0", g);
         Kx += ws[g];
     }
-    MSAT_REQUIRE(Kx > 0 && w0 > 0, "gru_ln_fused_fwd_x3r: empty input");
-    MSAT_REQUIRE(kxp % 32 == 0 && kxp >= Kx, "gru_ln_fused_fwd_x3r: kxp must be >= Kx and a multiple of 32");
-    MSAT_REQUIRE(aligned16(hprev) && ldp % 4 == 0 && aligned16(wiT_planes) && aligned16(whT_planes),
-                 "gru_ln_fused_fwd_x3r: hprev / weight planes must be 16-byte aligned");
+    MSAT_REQUIRE(Kx > 0 && w0 > 0, "gru_ln_fused_fwd_x3r/h2r: empty input");
+    MSAT_REQUIRE(kxp % 32 == 0 && kxp >= Kx, "gru_ln_fused_fwd_x3r/h2r: kxp must be >= Kx and a multiple of 32");
+    MSAT_REQUIRE(aligned16(hprev) && ldp % 4 == 0 && aligned16(wiT) && aligned16(whT),
+                 "gru_ln_fused_fwd_x3r/h2r: hprev / weight planes must be 16-byte aligned");
     MSAT_REQUIRE(aligned16(out) && ldo % 4 == 0 && (!g4 || (aligned16(g4) && ldg % 4 == 0)),
-                 "gru_ln_fused_fwd_x3r: out / g4 rows must be 16-byte aligned");
-    GruX3rArgs a = {};
+                 "gru_ln_fused_fwd_x3r/h2r: out / g4 rows must be 16-byte aligned");
+    a = GruX3rArgs{};
     for (int g = 0; g < 3; ++g) {
         a.seg[g] = ws[g] ? seg[g] : nullptr;
         a.seg_ld[g] = lds_[g];
@@ -1318,8 +1599,8 @@ extern "C" int msat_gru_ln_fused_fwd_x3r(const float *x0, int32_t ld0, int32_t w
     }
     a.hp = hprev;
     a.ldp = ldp;
-    a.wiT = reinterpret_cast<const __bf16 *>(wiT_planes);
-    a.whT = reinterpret_cast<const __bf16 *>(whT_planes);
+    a.wiT = reinterpret_cast<const uint16_t *>(wiT);
+    a.whT = reinterpret_cast<const uint16_t *>(whT);
     a.kxp = kxp;
     a.bi = bi;
     a.bh = bh;
@@ -1331,6 +1612,61 @@ extern "C" int msat_gru_ln_fused_fwd_x3r(const float *x0, int32_t ld0, int32_t w
     a.ldg = ldg;
     a.R = R;
     a.Kx = Kx;
+    return MSAT_OK;
+}
+
+extern "C" int msat_gru_ln_fused_fwd_x3r(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1,
+                                         int32_t w1, const float *x2, int32_t ld2, int32_t w2, const float *hprev,
+                                         int32_t ldp, const void *wiT_planes, int32_t kxp, const float *bi,
+                                         const void *whT_planes, const float *bh, const float *ln_scale,
+                                         const float *ln_bias, float *out, int32_t ldo, float *g4, int32_t ldg,
+                                         int32_t R, int32_t H, void *stream) {
+    MSAT_REQUIRE(R >= 0, "gru_ln_fused_fwd_x3r: R < 0");
+    if (R == 0) return MSAT_OK;
+    GruX3rArgs a;
+    const int rc = gru_r_args(a, x0, ld0, w0, x1, ld1, w1, x2, ld2, w2, hprev, ldp, wiT_planes, kxp, bi, whT_planes,
+                              bh, ln_scale, ln_bias, out, ldo, g4, ldg, R, H);
+    if (rc) return rc;
     hipLaunchKernelGGL(gru_ln_fused_fwd_x3r_kernel, dim3((R + 127) / 128), dim3(512), 0, (hipStream_t)stream, a);
     return check_launch("gru_ln_fused_fwd_x3r_kernel");
+}
+
+extern "C" int msat_split_f16x2_t(const float *W, int32_t K, int32_t N, int32_t ldw, int32_t Kp, void *planes,
+                                  int32_t *bad, void *stream) {
+    MSAT_REQUIRE(W && planes && bad && K > 0 && N > 0 && ldw >= N && Kp >= K, "bad split_f16x2_t args");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(bad, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("split_f16x2_t memset");
+    const size_t n = (size_t)N * Kp;
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(split_f16x2_t_kernel, dim3(grid), dim3(256), 0, s, W, K, N, ldw, Kp,
+                       reinterpret_cast<_Float16 *>(planes), bad);
+    return check_launch("split_f16x2_t_kernel");
+}
+
+extern "C" int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1,
+                                         int32_t w1, const float *x2, int32_t ld2, int32_t w2, const float *hprev,
+                                         int32_t ldp, const void *wiT_h2, const void *whT_h2, const void *wiT_x3,
+                                         const void *whT_x3, int32_t kxp, const float *bi, const float *bh,
+                                         const float *ln_scale, const float *ln_bias, float *out, int32_t ldo,
+                                         float *g4, int32_t ldg, int32_t R, int32_t H, int32_t *tile_flags,
+                                         const int32_t *wbad, void *stream) {
+    MSAT_REQUIRE(R >= 0, "gru_ln_fused_fwd_h2r: R < 0");
+    if (R == 0) return MSAT_OK;
+    MSAT_REQUIRE(tile_flags && wbad, "gru_ln_fused_fwd_h2r: NULL flags");
+    GruX3rArgs a;
+    int rc = gru_r_args(a, x0, ld0, w0, x1, ld1, w1, x2, ld2, w2, hprev, ldp, wiT_h2, kxp, bi, whT_h2, bh, ln_scale,
+                        ln_bias, out, ldo, g4, ldg, R, H);
+    if (rc) return rc;
+    MSAT_REQUIRE(wiT_x3 && whT_x3 && aligned16(wiT_x3) && aligned16(whT_x3), "gru_ln_fused_fwd_h2r: bf16x3 planes");
+    a.flags = tile_flags;
+    a.wbad = wbad;
+    const int tiles = (R + 127) / 128;
+    hipLaunchKernelGGL(gru_ln_fused_fwd_h2r_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
+    rc = check_launch("gru_ln_fused_fwd_h2r_kernel");
+    if (rc) return rc;
+    a.wiT = reinterpret_cast<const uint16_t *>(wiT_x3);
+    a.whT = reinterpret_cast<const uint16_t *>(whT_x3);
+    a.wbad = nullptr;
+    hipLaunchKernelGGL(gru_ln_fused_fwd_x3r_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
+    return check_launch("gru_ln_fused_fwd_x3r_kernel (fixup)");
 }

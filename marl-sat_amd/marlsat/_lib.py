@@ -126,6 +126,9 @@ def _load():
     sig["msat_gru_ln_fused_fwd_x3"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, I, P, P, P, P, P, P, I, P, I, I, I, P])
     sig["msat_gru_ln_fused_fwd_x3r"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, I, P, P, P, P, P, P, I, P, I, I, I, P])
     sig["msat_split_bf16x3_t"] = (I, [P, I, I, I, I, P, P])
+    sig["msat_gru_ln_fused_fwd_h2r"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, P, P, P, I, P, P, P, P, P, I, P, I, I, I,
+                                             P, P, P])
+    sig["msat_split_f16x2_t"] = (I, [P, I, I, I, I, P, P, P])
     sig["msat_gru_ln_bwd_g4"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, I, P])
     sig["msat_gru_ln_bwd_g4f"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, P, P, I, I, I, P])
     sig["msat_gru_ln_bwd_partial_floats"] = (Z, [I, I])
@@ -187,6 +190,8 @@ EXPORTED = (
     "msat_gru_ln_fused_fwd_x3",
     "msat_gru_ln_fused_fwd_x3r",
     "msat_split_bf16x3_t",
+    "msat_gru_ln_fused_fwd_h2r",
+    "msat_split_f16x2_t",
     "msat_split_bf16x3",
     "msat_split_bf16x3_rot",
     "msat_gemm_x3",

@@ -52,6 +52,11 @@ class _Scratch:
             self.ws = torch.empty(max(n, 2 * self.ws.numel()), device=self.device)
         return self.ws
 
+    def get_flags(self, n):
+        if getattr(self, "flags", None) is None or self.flags.numel() < n:
+            self.flags = torch.empty(max(n, 1024), dtype=torch.int32, device=self.device)
+        return self.flags
+
     def get_part(self, n):
         if self.part.numel() < n:
             self.part = torch.empty(max(n, 2 * self.part.numel()), device=self.device)
@@ -217,6 +222,29 @@ class GNNActorCritic:
             out[key] = (buf, Kp)
         return out
 
+    # fp16x2 operands for the register-A GRU forward (gru_fused.hip kRH2: three fp16 MFMAs per product
+    # instead of six bf16 ones, two weight planes instead of three; tiles whose activations leave fp16's
+    # range are recomputed in bf16x3 by the same launch pair); MARLSAT_GRU_H2=0 keeps bf16x3 throughout
+    use_gru_h2 = os.environ.get("MARLSAT_GRU_H2", "1") != "0"
+
+    def _split_weights_h2(self, cells):
+        """{cell: (Wi (Kx, 3H), Wh (H, 3H))} -> ({cell: (wi planes, wh planes)}, wbad (cells, 2) int32):
+        the transposed fp16x2 planes (msat_split_f16x2_t, weights scaled by 2^10) of both matrices of each
+        cell; wbad[c] = [wi overflowed, wh overflowed] (device flags read by the GRU launch)."""
+        bad = torch.empty((len(cells), 2), dtype=torch.int32, device=self.device)
+        out = {}
+        for c, (key, mats) in enumerate(cells.items()):
+            bufs = []
+            for m, Wm in enumerate(mats):
+                K, N = Wm.shape
+                Kp = (K + 31) // 32 * 32
+                buf = torch.empty(2 * N * Kp + 8, dtype=torch.int16, device=self.device)
+                _chk(L_.msat_split_f16x2_t(Wm.data_ptr(), K, N, Wm.stride(0), Kp, buf.data_ptr(),
+                                           self._ptr(bad[c], m), self.stream), "split_f16x2_t")
+                bufs.append(buf)
+            out[key] = (bufs[0], bufs[1], self._ptr(bad[c]))
+        return out, bad
+
     # transposed-weight GRU kernel (k-major images, ds_read_b128 fragments): measured equal to the
     # [K][3H] form (profiles/gru_bench.py: 855-3060 vs 888-3049 us) plus the per-forward transposes,
     # so it is opt-in (MARLSAT_GRU_T=1)
@@ -232,6 +260,19 @@ class GNNActorCritic:
         kx = sum(w for _, _, w in segs)
         GNNActorCritic.flops += 2 * R * 3 * H * (H + (kx + 15) // 16 * 16)
         (p0, l0, w0), (p1, l1, w1), (p2, l2, w2) = segs
+        if isinstance(wt, dict) and wt.get("h2"):  # fp16x2 register-A kernel + bf16x3 fixup of flagged tiles
+            h2wi, h2wh, wbad = wt["h2"]
+            flags = self.scr.get_flags((R + 127) // 128)
+            self._timed("gru_ln_fused_fwd_h2r_kernel (fp16x2, + x3r fixup launch)", 2.0 * R * 3 * H * (H + kx), lambda: _chk(
+                L_.msat_gru_ln_fused_fwd_h2r(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
+                                             h2wi.data_ptr(), h2wh.data_ptr(), wt["wi"][0].data_ptr(),
+                                             wt["wh"].data_ptr(), wt["wi"][1], self.p(f"enc.{cell}_bi").data_ptr(),
+                                             self.p(f"enc.{cell}_bh").data_ptr(), self._ptr(ln_row),
+                                             self._ptr(ln_row, H), out.data_ptr(), H,
+                                             g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, flags.data_ptr(),
+                                             wbad, self.stream),
+                "msat_gru_ln_fused_fwd_h2r"))
+            return
         if isinstance(wt, dict) and wt.get("x3r"):  # register-A kernel: W^T planes {"wi": (planes, kxp), "wh"}
             self._timed("gru_ln_fused_fwd_x3r_kernel (bf16x3)", 2.0 * R * 3 * H * (H + kx), lambda: _chk(
                 L_.msat_gru_ln_fused_fwd_x3r(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
@@ -400,6 +441,12 @@ class GNNActorCritic:
                                         "hvp": self.p("enc.gru_vp_wh"), "hvn": self.p("enc.gru_vn_wh")})
             wt = {c: {"x3r": True, "wi": pl[k], "wh": pl[hk][0]}
                   for c, k, hk in (("gru_c", "c", "hc"), ("gru_vp", "vp", "hvp"), ("gru_vn", "vn", "hvn"))}
+            if self.use_gru_h2:
+                h2, self._h2bad = self._split_weights_h2({
+                    "gru_c": (Fc, self.p("enc.gru_c_wh")), "gru_vp": (Fp, self.p("enc.gru_vp_wh")),
+                    "gru_vn": (Fn, self.p("enc.gru_vn_wh"))})
+                for c in wt:
+                    wt[c]["h2"] = h2[c]
         elif self.use_gru_x3 and H == 128:
             (Pc, Pp, Pn), _ = self._fold_views(padded=True)
             pl = self._split_weights({"c": (Pc, 0), "vp": (Pp, 0), "vn": (Pn, 0), "hc": (self.p("enc.gru_c_wh"), 0),

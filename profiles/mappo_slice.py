@@ -14,6 +14,7 @@ line = next(l for l in open(bench_log) if l.startswith("{") and '"mappo"' in l)
 bench = json.loads(line)["mappo"]
 ROCPROF_NAMES = {  # bench label -> rocprof kernel names whose launches the bench's event pair brackets
     "gru_ln_fused_fwd_x3r_kernel (bf16x3)": ["gru_ln_fused_fwd_x3r_kernel"],
+    "gru_ln_fused_fwd_h2r_kernel (fp16x2, + x3r fixup launch)": ["gru_ln_fused_fwd_h2r_kernel", "gru_ln_fused_fwd_x3r_kernel"],
     "gemm_x3r16_kernel (dgrad, bf16x3)": ["gemm_x3r16_kernel"],
     "wgrad_x3_kernel + reduce (bf16x3)": ["wgrad_x3_kernel", "wgrad_reduce4_kernel"],
 }

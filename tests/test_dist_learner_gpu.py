@@ -60,6 +60,11 @@ def test_two_rank_learner_equals_union(tmp_path):
     np.testing.assert_allclose(cat("adv").numpy(), u["adv"].numpy(), rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(cat("targets").numpy(), u["targets"].numpy(), rtol=1e-6, atol=1e-7)
     net = learner.net
+    # from here on the union evaluates every step on the sharded run's normalised advantages and targets
+    # (equal to 1e-6 above): otherwise a ratio sitting within 1e-7 of the clip edge 1 +- eps could take
+    # the other branch of min(r A, clip(r) A) and move a whole sample's actor gradient
+    learner.adv.copy_(cat("adv").to(learner.adv.device))
+    learner.targets.copy_(cat("targets").to(learner.targets.device))
     losses_sharded = 0.5 * (ranks[0]["losses"] + ranks[1]["losses"])  # each (E, n_mb, 3) of equal-size means
     for s, rec in enumerate(ranks[0]["trace"]):
         rows = []

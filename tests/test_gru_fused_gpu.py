@@ -109,6 +109,30 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
                                                       4 * H, R, H, s), "gru_ln_fused_fwd_x3r")
         torch.cuda.synchronize()
         return out
+    if layout == "h2r":  # register-A fp16x2 kernel + bf16x3 fixup of out-of-range tiles
+        K = wi.shape[0]
+        kxp = (K + 31) // 32 * 32
+        s = _lib.stream_ptr()
+        pi = torch.empty(3 * 3 * H * kxp + 8, dtype=torch.int16, device="cuda")
+        ph = torch.empty(3 * 3 * H * H + 8, dtype=torch.int16, device="cuda")
+        qi = torch.empty(2 * 3 * H * kxp + 8, dtype=torch.int16, device="cuda")
+        qh = torch.empty(2 * 3 * H * H + 8, dtype=torch.int16, device="cuda")
+        bad = torch.full((2,), 7, dtype=torch.int32, device="cuda")
+        flags = torch.full(((R + 127) // 128 + 1,), 7, dtype=torch.int32, device="cuda")
+        _lib.check(_lib.lib.msat_split_bf16x3_t(wi.data_ptr(), K, 3 * H, 3 * H, kxp, pi.data_ptr(), s), "split_t")
+        _lib.check(_lib.lib.msat_split_bf16x3_t(wh.data_ptr(), H, 3 * H, 3 * H, H, ph.data_ptr(), s), "split_t")
+        _lib.check(_lib.lib.msat_split_f16x2_t(wi.data_ptr(), K, 3 * H, 3 * H, kxp, qi.data_ptr(), bad.data_ptr(), s),
+                   "split_f16x2_t")
+        _lib.check(_lib.lib.msat_split_f16x2_t(wh.data_ptr(), H, 3 * H, 3 * H, H, qh.data_ptr(), bad.data_ptr() + 4,
+                                                s), "split_f16x2_t")
+        _lib.check(_lib.lib.msat_gru_ln_fused_fwd_h2r(*args, h.data_ptr(), H, qi.data_ptr(), qh.data_ptr(),
+                                                      pi.data_ptr(), ph.data_ptr(), kxp, bi.data_ptr(), bh.data_ptr(),
+                                                      sc.data_ptr(), lb.data_ptr(), out.data_ptr(), H,
+                                                      g4.data_ptr() if g4 is not None else 0, 4 * H, R, H,
+                                                      flags.data_ptr(), bad.data_ptr(), s), "gru_ln_fused_fwd_h2r")
+        torch.cuda.synchronize()
+        _fwd.last_flags = (flags[:(R + 127) // 128].cpu(), bad.cpu())
+        return out
     if layout == "t":  # transposed-weight kernel (k-major images, ds_read_b128 fragments)
         wiT, whT = _transposed(wi), _transposed(wh)
         assert bool((wiT[:, wi.shape[0]:] == 0).all()) and torch.equal(wiT[:, :wi.shape[0]], wi.t())
@@ -127,9 +151,9 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
 
 def _fwd_cases():
     """(layout, H, R): the plain kernel at H 64 / 128 / 256, the transposed-weight kernel at H 64 /
-    128, the bf16x3 kernels (LDS-staged, register-A) at H 128; the 70,000-row case at the
-    production width H = 128 only."""
-    widths = {"plain": (64, 128, 256), "t": (64, 128), "x3": (128,), "x3r": (128,)}
+    128, the bf16x3 kernels (LDS-staged, register-A) and the fp16x2 register-A kernel at H 128; the
+    70,000-row case at the production width H = 128 only."""
+    widths = {"plain": (64, 128, 256), "t": (64, 128), "x3": (128,), "x3r": (128,), "h2r": (128,)}
     return [(lay, H, R) for lay, hs in widths.items() for H in hs for R in (0, 1, 77, 1000, 70000)
             if R != 70000 or H == 128]
 
@@ -156,6 +180,37 @@ def test_fused_forward_matches_reference(R, H, kind, layout):
                     absx[:, 2 * H:3 * H], absx[:, 5 * H:]], 1)
     terr = (g4.double() - tape_ref).abs()
     assert bool((terr <= 2e-6 * ab + 1e-30).all()), float((terr / (ab + 1e-30)).max())
+
+
+@pytest.mark.parametrize("kind", ["var8", "clause4"])
+def test_h2r_out_of_range_tiles_take_the_bf16x3_path(kind):
+    """fp16x2 range check: activations with |a| >= 2^15 in two rows flag exactly their 128-row tiles,
+    which the fixup launch recomputes in bf16x3 (bitwise the x3r kernel's rows there), the other tiles
+    keep the fp16x2 result; weights with |W| >= 32 flag the split and every tile is bf16x3."""
+    R, H = 1000, 128
+    segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=3)
+    segs[0][0][130, 5] = 4.0e4   # tile 1
+    segs[0][0][777, 17] = -9.0e4  # tile 6
+    x = torch.cat([segs[0][0][:, segs[0][1]:segs[0][1] + segs[0][3]], segs[1][0]], 1)
+    g4 = torch.empty(R, 4 * H, device="cuda")
+    out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, "h2r")
+    flags, bad = _fwd.last_flags
+    assert bad.tolist() == [0, 0]
+    assert flags.tolist() == [1 if t in (1, 6) else 0 for t in range((R + 127) // 128)]
+    g4x = torch.empty(R, 4 * H, device="cuda")
+    ox = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4x, "x3r")
+    for t in (1, 6):
+        rows = slice(128 * t, min(R, 128 * t + 128))
+        assert torch.equal(out[rows], ox[rows]) and torch.equal(g4[rows], g4x[rows])
+    d = lambda t: t.double()
+    ref, _, _ = _ref_gru_ln(d(x), d(h), d(wi), d(bi), d(wh), d(bh), d(sc), d(lb), H)
+    err = (out.double() - ref).abs()
+    assert bool((err <= 1e-5 * ref.abs() + 1e-5).all()), float(err.max())
+    big = wh * 400.0  # |W| >= 32 somewhere
+    out2 = _fwd(segs, h, wi, bi, big, bh, sc, lb, R, H, None, "h2r")
+    flags2, bad2 = _fwd.last_flags
+    assert bad2.tolist() == [0, 1] and bool((flags2 == 1).all())
+    assert torch.equal(out2, _fwd(segs, h, wi, bi, big, bh, sc, lb, R, H, None, "x3r"))
 
 
 @pytest.mark.parametrize("nfeat", [0, 2, 6])  # msat_gru_ln_bwd_g4f feature-weighted gate sums
