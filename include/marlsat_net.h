@@ -49,6 +49,16 @@ int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, float *C, int
 size_t msat_gemm_wgrad_workspace_bytes(int32_t M, int32_t K, int32_t N);
 int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
                     int32_t M, int32_t K, int32_t N, int32_t accumulate, void *workspace, void *stream);
+/* W[:, (n + rot) % N] (+)= (A^T G)[:, n], 0 <= rot < N: the packed GRU backward rows' gate blocks
+ * (n | r | z) into a weight stored (r | z | n) in one pass (learner:62-80 update cells' input rows). */
+/* The same in fp16x2 (three fp16 MFMAs per product) for G = a GRU backward's packed rows with their
+ * row scale exponents rexp (msat_gru_ln_bwd_g4fe): K > 8, N <= 384, rot % 4 == 0. */
+int msat_gemm_wgrad_h2(const float *A, int32_t lda, const float *G, int32_t ldg, const int32_t *rexp, float *W,
+                       int32_t ldw, int32_t M, int32_t K, int32_t N, int32_t rot, int32_t accumulate, void *workspace,
+                       void *stream);
+int msat_gemm_wgrad_rot(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
+                        int32_t M, int32_t K, int32_t N, int32_t rot, int32_t accumulate, void *workspace,
+                        void *stream);
 
 /* ---- graph batch assembly (learner:148-195 features + the agents' local graphs) ----
  * Block per sample: instantiate the per-instance templates (marlsat/learners/graphs.py) at the
@@ -170,6 +180,13 @@ int msat_gru_ln_bwd_g4f(const float *dy, int32_t ldy, const float *g4, int32_t l
                         int32_t lddp, float *dln_scale, float *dln_bias, float *dbi, float *dbh_n, const float *feat,
                         int32_t ldf, int32_t nfeat, float *dfeat, float *partial, int32_t R, int32_t H,
                         int32_t accumulate_ln, void *stream);
+/* msat_gru_ln_bwd_g4f (packed rows) + rexp[r] = the fp16x2 scale exponent of row r's largest |dG|
+ * (max |dG| 2^e in [2^14, 2^15); 0x3fff for an all-zero row) for msat_gemm_wgrad_h2 / msat_gemm_h2. */
+int msat_gru_ln_bwd_g4fe(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev, int32_t ldp,
+                         const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh, float *dhprev,
+                         int32_t lddp, float *dln_scale, float *dln_bias, float *dbi, float *dbh_n, const float *feat,
+                         int32_t ldf, int32_t nfeat, float *dfeat, float *partial, int32_t R, int32_t H,
+                         int32_t accumulate_ln, int32_t *rexp, void *stream);
 int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
                        int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
                        float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *dbi, float *dbh_n,

@@ -380,6 +380,12 @@ int msat_gemm2_launch(const float *A, int lda, const float *B, int ldb, int tran
                       const float *bias, int M, int N, int K, int accumulate, hipStream_t s);
 bool msat_wgrad2_ok(const float *A, int lda, const float *G, int ldg, int K, int N);
 bool msat_wgrad_x3_ok(const float *A, int lda, const float *G, int ldg, int K, int N);
+bool msat_wgrad_x3w_ok(const float *A, int lda, const float *G, int ldg, int K, int N);
+int msat_wgrad_x3w_splits(int M, int K);
+int msat_wgrad_x3w_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int rot,
+                          int splits, hipStream_t s);
+int msat_wgrad_h2w_launch(const float *A, int lda, const float *G, int ldg, const int *rexp, float *part, int M, int K,
+                          int N, int rot, int splits, int *flags, hipStream_t s);
 int msat_wgrad_x3_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
                          int rows_per_split, hipStream_t s);
 
@@ -446,9 +452,25 @@ extern "C" int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ld
     return check_launch("gemm_kernel");
 }
 
+constexpr size_t kWgradFlagBytes = 1024 * sizeof(int);  // >= 256 workgroups' flags
+
 extern "C" size_t msat_gemm_wgrad_workspace_bytes(int32_t M, int32_t K, int32_t N) {
-    const size_t sp = std::max(wgrad_splits(M, K, N), K <= kSkinnyK ? skinny_splits(M, N) : 0);
-    return sp * K * N * sizeof(float);
+    const size_t sp = std::max({wgrad_splits(M, K, N), K <= kSkinnyK ? skinny_splits(M, N) : 0,
+                                msat_wgrad_x3w_splits(M, K)});
+    return sp * K * N * sizeof(float) + kWgradFlagBytes;  // + the fp16x2 kernel's workgroup flags
+}
+
+static int wgrad_reduce(const float *part, int splits, int K, int N, float *W, int ldw, int accumulate, hipStream_t s) {
+    if (N % 4 == 0 && ldw % 4 == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(part) & 15) == 0) {
+        const int n4 = N / 4;
+        hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((K * n4 + 255) / 256), dim3(256), 0, s,
+                           (const float4 *)part, splits, K, n4, (float4 *)W, ldw / 4, accumulate);
+        return check_launch("wgrad_reduce4_kernel");
+    }
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((K * N + 255) / 256), dim3(256), 0, s, part, splits, K, N, W, ldw,
+                       accumulate);
+    return check_launch("wgrad_reduce_kernel");
 }
 
 extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
@@ -456,6 +478,12 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
     MSAT_REQUIRE(A && G && W && workspace, "NULL operand");
     MSAT_REQUIRE(M >= 0 && K >= 1 && N >= 1 && lda >= K && ldg >= N && ldw >= N, "bad dims");
     hipStream_t s = (hipStream_t)stream;
+    if (!legacy_gemm() && wgrad_x3() && K > kSkinnyK && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
+        const int splits = msat_wgrad_x3w_splits(M, K);
+        const int rc = msat_wgrad_x3w_launch(A, lda, G, ldg, (float *)workspace, M, K, N, 0, splits, s);
+        if (rc) return rc;
+        return wgrad_reduce((const float *)workspace, splits, K, N, W, ldw, accumulate, s);
+    }
     if (!legacy_gemm() && skinny_ok(G, ldg, W, ldw, K, N) && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0) {
         const int sp = skinny_splits(M, N), rows_per = (M + sp - 1) / sp, N4 = N / 4;
         float4 *ws4 = reinterpret_cast<float4 *>(workspace);
@@ -489,14 +517,48 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
         rc = check_launch("gemm_wgrad_kernel");
     }
     if (rc) return rc;
-    if (N % 4 == 0 && ldw % 4 == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0 &&
-        (reinterpret_cast<uintptr_t>(workspace) & 15) == 0) {
-        const int n4 = N / 4;
-        hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((K * n4 + 255) / 256), dim3(256), 0, s,
-                           (const float4 *)workspace, splits, K, n4, (float4 *)W, ldw / 4, accumulate);
-        return check_launch("wgrad_reduce4_kernel");
+    return wgrad_reduce((const float *)workspace, splits, K, N, W, ldw, accumulate, s);
+}
+
+// W[:, (n + rot) % N] (+)= (A^T G)[:, n]: the packed backward rows' gate blocks (n | r | z) into a
+// weight stored (r | z | n).  The whole-row kernel rotates in its partial store; otherwise two
+// column ranges of the plain product.
+extern "C" int msat_gemm_wgrad_rot(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
+                                   int32_t M, int32_t K, int32_t N, int32_t rot, int32_t accumulate, void *workspace,
+                                   void *stream) {
+    MSAT_REQUIRE(rot >= 0 && rot < N, "gemm_wgrad_rot: rot must be in [0, N)");
+    if (rot == 0) return msat_gemm_wgrad(A, lda, G, ldg, W, ldw, M, K, N, accumulate, workspace, stream);
+    MSAT_REQUIRE(A && G && W && workspace, "NULL operand");
+    MSAT_REQUIRE(M >= 0 && K >= 1 && N >= 1 && lda >= K && ldg >= N && ldw >= N, "bad dims");
+    hipStream_t s = (hipStream_t)stream;
+    if (!legacy_gemm() && wgrad_x3() && K > kSkinnyK && rot % 4 == 0 && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
+        const int splits = msat_wgrad_x3w_splits(M, K);
+        const int rc = msat_wgrad_x3w_launch(A, lda, G, ldg, (float *)workspace, M, K, N, rot, splits, s);
+        if (rc) return rc;
+        return wgrad_reduce((const float *)workspace, splits, K, N, W, ldw, accumulate, s);
     }
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((K * N + 255) / 256), dim3(256), 0, s, (const float *)workspace,
-                       splits, K, N, W, ldw, accumulate);
-    return check_launch("wgrad_reduce_kernel");
+    const int rc = msat_gemm_wgrad(A, lda, G, ldg, W + rot, ldw, M, K, N - rot, accumulate, workspace, stream);
+    if (rc) return rc;
+    return msat_gemm_wgrad(A, lda, G + (N - rot), ldg, W, ldw, M, K, rot, accumulate, workspace, stream);
+}
+
+// fp16x2 whole-row weight gradient of a GRU backward's packed rows: G's rows carry scale exponents
+// (rexp, msat_gru_ln_bwd_g4fe), A is range-checked (a workgroup that sees |a| >= 2^15 is recomputed
+// in bf16x3).  Same product and rotation as msat_gemm_wgrad_rot.
+extern "C" int msat_gemm_wgrad_h2(const float *A, int32_t lda, const float *G, int32_t ldg, const int32_t *rexp,
+                                  float *W, int32_t ldw, int32_t M, int32_t K, int32_t N, int32_t rot,
+                                  int32_t accumulate, void *workspace, void *stream) {
+    MSAT_REQUIRE(A && G && W && rexp && workspace, "NULL operand");
+    MSAT_REQUIRE(M >= 0 && K > kSkinnyK && N >= 1 && N <= 384 && lda >= K && ldg >= N && ldw >= N,
+                 "gemm_wgrad_h2: bad dims (K > 8, N <= 384)");
+    MSAT_REQUIRE(rot >= 0 && rot < N && rot % 4 == 0, "gemm_wgrad_h2: rot must be in [0, N), a multiple of 4");
+    MSAT_REQUIRE(msat_wgrad_x3_ok(A, lda, G, ldg, K, N) && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0,
+                 "gemm_wgrad_h2: K %% 4, N %% 4, ld %% 4 and 16-byte aligned operands required");
+    hipStream_t s = (hipStream_t)stream;
+    const int splits = msat_wgrad_x3w_splits(M, K);
+    float *part = (float *)workspace;
+    int *flags = reinterpret_cast<int *>(part + (size_t)splits * K * N);
+    const int rc = msat_wgrad_h2w_launch(A, lda, G, ldg, rexp, part, M, K, N, rot, splits, flags, s);
+    if (rc) return rc;
+    return wgrad_reduce(part, splits, K, N, W, ldw, accumulate, s);
 }

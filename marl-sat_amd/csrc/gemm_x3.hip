@@ -698,6 +698,220 @@ wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ 
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Whole-row weight gradient: part[s][k][(n + rot) % N] = sum_{m in split s} A[m][k] G[m][n] for one
+// 128-row k tile and ALL N <= 384 columns per workgroup.  Every A element is loaded by exactly one
+// workgroup and every G element by ceil(K / 128), so the kernel streams A and G from HBM once
+// (the 128 x 128 tiles of wgrad_x3_kernel re-read each operand per tile of the other, from L2 at
+// best).  512 threads, 8 waves at two per SIMD, one workgroup per CU; wave w owns k rows
+// 64 (w & 1) .. +63 x columns 96 (w >> 1) .. +95 as 2 x 3 tiles of 32x32 (96 accumulator registers).
+// Staging as wgrad_x3_kernel: 16-row slabs loaded two ahead in registers, split into NP planes of
+// [16 rows][128 cols] images (G: three column blocks), transposed fragment reads, one barrier per
+// slab.  rot rotates the output columns (the packed backward rows' gate blocks are (n | r | z), the
+// weights' (r | z | n)); rot % 4 == 0.
+//
+// NP = 3: bf16x3 (six bf16 MFMAs per tile and slab).  With `flags` it is the fixup launch of the
+// fp16x2 kernel: it computes only the workgroups flagged there.
+// NP = 2: fp16x2 (three fp16 MFMAs).  G is scaled by 2^e with e the smallest row exponent of the
+// split (rexp, written by the GRU backward that produced G: every scaled row below 2^15, the
+// largest at full precision) and the partial by 2^-e (exact).  A is range-checked (|a| < 2^15): a
+// workgroup that loads anything outside sets flags[id] and stores nothing.
+//
+// IL: the split and LDS store of slab s + 1 are interleaved with slab s's MFMAs by scheduling groups
+// (one MFMA, then a few vector instructions; an LDS store every few MFMAs), so the split fills the
+// MFMA issue gaps instead of running as its own phase between the MFMA phase and the barrier.
+//
+// diagnostic ablations (timing only, wrong results; never set in the product build): bit 0 no
+// operand loads after the prologue, 1 no MFMAs, 2 no split / LDS store after it
+#ifndef MSAT_WW_ABL
+#define MSAT_WW_ABL 0
+#endif
+constexpr int kWWT = 512;
+constexpr int kWWN = 384;  // widest N
+
+template <int NP, bool IL>
+__global__ void __launch_bounds__(kWWT, 1)
+wgrad_w_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G, int ldg, const int *__restrict__ rexp,
+               float *__restrict__ part, int M, int K, int N, int rot, int rows_per_split, int ktiles,
+               int *__restrict__ flags) {
+    // [buf][A planes 0 .. NP-1 | G plane q, column block u at NP + 3 q + u]
+    __shared__ __attribute__((aligned(16))) unsigned short lds[2][4 * NP][kW3Plane];
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    if (NP == 3 && flags && flags[id] == 0) return;  // fixup launch: only the flagged workgroups
+    const int sp = id / ktiles, k0 = (id % ktiles) * kX3M;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int wk = (w & 1) * 64, wn = __builtin_amdgcn_readfirstlane((w >> 1) * 96);
+    const int rb = sp * rows_per_split, re = min(M, rb + rows_per_split);
+    const int ns = (re - rb + 15) / 16;
+    int ge = 0;  // fp16x2: G scale exponent of this split
+    if constexpr (NP == 2) {
+        __shared__ int red[kWWT / 64];
+        int mn = kExpZero;
+        for (int r = rb + t; r < re; r += kWWT) mn = min(mn, rexp[r]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mn = min(mn, __shfl_xor(mn, o, 64));
+        if (lane == 0) red[w] = mn;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kWWT / 64; ++i) mn = min(mn, red[i]);
+        ge = mn == kExpZero ? 0 : mn;
+    }
+    f32x16v acc[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = f32x16v{};
+    // staging: thread t -> slab row t >> 5, columns sc .. sc + 3 of the A tile and of each G block
+    const int srow = t >> 5, sc = (t & 31) * 4;
+    const bool kok = k0 + sc < K;
+    bool nok[3];
+    const float *pa = A + (kok ? k0 + sc : 0);
+    const float *pg[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+        nok[u] = sc + 128 * u < N;
+        pg[u] = G + (nok[u] ? sc + 128 * u : 0);
+    }
+    struct Stage {
+        float4 a, g[3];
+    };
+    auto load = [&](int s, Stage &r) {
+        const int m = rb + s * 16 + srow;
+        const size_t mc = m < re ? m : re - 1;
+        r.a = *reinterpret_cast<const float4 *>(pa + mc * lda);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) r.g[u] = *reinterpret_cast<const float4 *>(pg[u] + mc * ldg);
+    };
+    float amax = 0.f;  // fp16x2: largest |operand| staged by this thread (range check)
+    const int off = w3off(srow, sc >> 3) + 8 * ((sc >> 2) & 1);
+    auto put = [&](int buf, int plane, const uint2 &v) {
+        *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(lds[buf][plane]) + off) = v;
+    };
+    auto store = [&](int s, Stage r, int buf) {
+        const bool mok = rb + s * 16 + srow < re;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!(mok && kok)) r.a = z;
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+            if (!(mok && nok[u])) r.g[u] = z;
+        if constexpr (NP == 3) {
+            const Split4 xa = split4(r.a);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) put(buf, q, xa.p[q]);
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const Split4 xg = split4(r.g[u]);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) put(buf, 3 + 3 * q + u, xg.p[q]);
+            }
+        } else {
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(r.a.x), fabsf(r.a.y)), fmaxf(fabsf(r.a.z), fabsf(r.a.w))));
+            const SplitH4 xa = splith4(r.a);
+            put(buf, 0, xa.p[0]);
+            put(buf, 1, xa.p[1]);
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const float4 v = make_float4(ldexpf(r.g[u].x, ge), ldexpf(r.g[u].y, ge), ldexpf(r.g[u].z, ge),
+                                             ldexpf(r.g[u].w, ge));
+                amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+                const SplitH4 xg = splith4(v);
+                put(buf, 2 + u, xg.p[0]);
+                put(buf, 5 + u, xg.p[1]);
+            }
+        }
+    };
+    const int h = lane >> 5, g = (lane >> 4) & 1;
+    auto slab = [&](int buf) {
+        bf16x8 fa[2][NP], fb[3][NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fa[i][q] = tr_frag(lds[buf][q], 8 * h, (wk + 32 * i + 16 * g) >> 3, lane);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int n = wn + 32 * j;
+                fb[j][q] = tr_frag(lds[buf][NP + 3 * q + (n >> 7)], 8 * h, ((n & 127) + 16 * g) >> 3, lane);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                f32x16v c = acc[i][j];
+                if constexpr (NP == 3) {
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+                } else {
+                    typedef _Float16 f16x8w __attribute__((ext_vector_type(8)));
+                    const f16x8w a0 = __builtin_bit_cast(f16x8w, fa[i][0]), a1 = __builtin_bit_cast(f16x8w, fa[i][1]);
+                    const f16x8w b0 = __builtin_bit_cast(f16x8w, fb[j][0]), b1 = __builtin_bit_cast(f16x8w, fb[j][1]);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, c, 0, 0, 0);  // h l
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, c, 0, 0, 0);  // l h
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, c, 0, 0, 0);  // h h
+                }
+                acc[i][j] = c;
+            }
+    };
+    if (ns > 0) {
+        Stage R0, R1;
+        load(0, R0);
+        load(1 < ns ? 1 : 0, R1);
+        store(0, R0, 0);
+        __syncthreads();
+        // Rn holds slab s + 1, Rf receives slab s + 2 (past the end: a repeated, never stored load)
+        auto iter = [&](int s, const Stage &Rn, Stage &Rf) {
+            const int buf = s & 1;
+            if (!(MSAT_WW_ABL & 1)) load(s + 2 < ns ? s + 2 : ns - 1, Rf);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!(MSAT_WW_ABL & 2)) slab(buf);
+            if constexpr (IL) {
+                if (!(MSAT_WW_ABL & 4)) store(s + 1, Rn, buf ^ 1);
+                constexpr int NM = 6 * NP;  // MFMAs per wave and slab
+                __builtin_amdgcn_sched_group_barrier(0x100, 10 * NP, 0);  // the fragment reads first
+#pragma unroll
+                for (int k = 0; k < NM; ++k) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);               // one MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, NP == 3 ? 4 : 5, 0);  // vector ALU
+                    if (k % (NP == 3 ? 3 : 2) == 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // LDS store
+                }
+            } else {
+                __builtin_amdgcn_sched_barrier(0);
+                store(s + 1, Rn, buf ^ 1);
+            }
+            __syncthreads();
+        };
+        int s = 0;
+        for (; s + 1 < ns; s += 2) {
+            iter(s, R1, R0);
+            iter(s + 1, R0, R1);
+        }
+        if (s < ns) iter(s, R1, R0);
+    }
+    if constexpr (NP == 2) {
+        const int bad = __syncthreads_or(!(amax < 32768.0f));
+        if (t == 0) flags[id] = bad;
+        if (bad) return;
+    }
+    float *P = part + (size_t)sp * K * N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int n = wn + 32 * j + (lane & 31);
+            if (n >= N) continue;
+            const int oc = n + rot < N ? n + rot : n + rot - N;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = k0 + wk + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                if (row < K) P[(size_t)row * N + oc] = NP == 2 ? ldexpf(acc[i][j][reg], -ge) : acc[i][j][reg];
+            }
+        }
+}
+
 static bool a16x3(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace msat
@@ -772,4 +986,49 @@ int msat_wgrad_x3_launch(const float *A, int lda, const float *G, int ldg, float
     hipLaunchKernelGGL(wgrad_x3_kernel, dim3(tiles * splits), dim3(kX3T), 0, s, A, lda, G, ldg, part, M, K, N,
                        rows_per_split, ntn, tiles);
     return check_launch("wgrad_x3_kernel");
+}
+
+// Whole-row weight gradient (wgrad_w_kernel): N <= 384 besides the x3 conditions.
+bool msat_wgrad_x3w_ok(const float *A, int lda, const float *G, int ldg, int K, int N) {
+    const char *e = getenv("MARLSAT_WGRAD_W");  // 0: the 128 x 128 tile kernel (A/B measurements)
+    if (e && e[0] == '0') return false;
+    return N <= kWWN && msat_wgrad_x3_ok(A, lda, G, ldg, K, N);
+}
+
+// one workgroup per CU: 256 workgroups over the k tiles and row splits, >= 512 rows per split
+int msat_wgrad_x3w_splits(int M, int K) {
+    const int ktiles = (K + kX3M - 1) / kX3M;
+    return std::max(1, std::min(256 / ktiles, (M + 511) / 512));
+}
+
+static bool wgrad_interleave() {
+    const char *e = getenv("MARLSAT_WGRAD_WI");  // 0: split as its own phase after the MFMAs (A/B)
+    return !(e && e[0] == '0');
+}
+
+int msat_wgrad_x3w_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int rot,
+                          int splits, hipStream_t s) {
+    const int ktiles = (K + kX3M - 1) / kX3M;
+    const int rows = (M + splits - 1) / splits, rows16 = ((rows + 15) / 16) * 16;
+    if (wgrad_interleave())
+        hipLaunchKernelGGL((wgrad_w_kernel<3, true>), dim3(ktiles * splits), dim3(kWWT), 0, s, A, lda, G, ldg, nullptr,
+                           part, M, K, N, rot, rows16, ktiles, nullptr);
+    else
+        hipLaunchKernelGGL((wgrad_w_kernel<3, false>), dim3(ktiles * splits), dim3(kWWT), 0, s, A, lda, G, ldg, nullptr,
+                           part, M, K, N, rot, rows16, ktiles, nullptr);
+    return check_launch("wgrad_w_kernel<3> (bf16x3)");
+}
+
+// fp16x2 form + its bf16x3 fixup launch over the workgroups it flagged (flags: ktiles * splits ints)
+int msat_wgrad_h2w_launch(const float *A, int lda, const float *G, int ldg, const int *rexp, float *part, int M, int K,
+                          int N, int rot, int splits, int *flags, hipStream_t s) {
+    const int ktiles = (K + kX3M - 1) / kX3M;
+    const int rows = (M + splits - 1) / splits, rows16 = ((rows + 15) / 16) * 16;
+    hipLaunchKernelGGL((wgrad_w_kernel<2, true>), dim3(ktiles * splits), dim3(kWWT), 0, s, A, lda, G, ldg, rexp, part,
+                       M, K, N, rot, rows16, ktiles, flags);
+    int rc = check_launch("wgrad_w_kernel<2> (fp16x2)");
+    if (rc) return rc;
+    hipLaunchKernelGGL((wgrad_w_kernel<3, true>), dim3(ktiles * splits), dim3(kWWT), 0, s, A, lda, G, ldg, nullptr,
+                       part, M, K, N, rot, rows16, ktiles, flags);
+    return check_launch("wgrad_w_kernel<3> (fixup)");
 }

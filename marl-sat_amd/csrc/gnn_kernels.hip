@@ -11,6 +11,7 @@
 // GRU + LayerNorm (flax nn.GRUCell / nn.LayerNorm semantics) are fused row kernels
 // (one wave per row) on top of the fp32 MFMA GEMMs of gemm.hip.
 #include "common.h"
+#include "split3.h"
 
 namespace msat {
 
@@ -186,7 +187,7 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
                   const float *__restrict__ scale, float *__restrict__ dGi, int lddi, float *__restrict__ dGh, int lddh,
                   float *__restrict__ dh, int lddh_prev, float *__restrict__ part, int R, int H, int dh_assign,
-                  int packed, const float *__restrict__ feat, int ldf) {
+                  int packed, const float *__restrict__ feat, int ldf, int *__restrict__ rexp) {
     constexpr int NQT = NQ + 3 * NF, QC = NQ;  // partial rows; LDS reduction in chunks of QC rows
     __shared__ float s_part[4][QC * 64 * PER];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -241,6 +242,7 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
         }
         a1 = wave_sum_f32(a1) / (float)H;
         a2 = wave_sum_f32(a2) / (float)H;
+        float rmax = 0.f;  // largest |dG| of the row (rexp)
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int j = lane + 64 * u;
@@ -265,6 +267,7 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
                 dhh[H + j] = daz;
                 dhh[2 * H + j] = dan * rg[u];
             }
+            if (rexp) rmax = fmaxf(rmax, fmaxf(fmaxf(fabsf(dan), fabsf(dar)), fmaxf(fabsf(daz), fabsf(dan * rg[u]))));
             float *dhp = dh + (size_t)r * lddh_prev + j;
             *dhp = dh_assign ? dhn * zg[u] : *dhp + dhn * zg[u];
             if constexpr (NQ == 6) {
@@ -279,6 +282,10 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
                 pq[NQ + 3 * k + 1][u] += fw[k] * daz;
                 pq[NQ + 3 * k + 2][u] += fw[k] * dan;
             }
+        }
+        if (rexp) {
+            rmax = wave_max_f32(rmax);
+            if (lane == 0) rexp[r] = f16x2_row_exp(rmax);
         }
     }
 #pragma unroll
@@ -607,20 +614,20 @@ extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, in
     hipStream_t s = (hipStream_t)stream;
     const int nb = bwd_blocks(R);
     const dim3 g(nb), b(kRowThreads);
-    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0);
-    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0);
-    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0);
+    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0, nullptr);
+    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0, nullptr);
+    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0, nullptr);
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
     return reduce_partials(partial, nb, 2 * H, dln_scale, accumulate_ln, partial + (size_t)nb * 2 * H, s);
 }
 
-extern "C" int msat_gru_ln_bwd_g4f(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
-                                   int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh,
-                                   int32_t lddh, float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias,
-                                   float *dbi, float *dbh_n, const float *feat, int32_t ldf, int32_t nfeat,
-                                   float *dfeat, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
-                                   void *stream) {
+static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
+                              int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh,
+                              float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias, float *dbi,
+                              float *dbh_n, const float *feat, int32_t ldf, int32_t nfeat, float *dfeat,
+                              float *partial, int32_t R, int32_t H, int32_t accumulate_ln, int32_t *rexp,
+                              void *stream) {
     MSAT_REQUIRE(H == 64 || H == 128 || H == 256, "gru_ln: H must be 64, 128 or 256 (got %d)", H);
     MSAT_REQUIRE(ldg >= 4 * H, "gru_ln_bwd_g4: ldg must be >= 4H");
     MSAT_REQUIRE(dln_bias == dln_scale + H, "dln_bias must follow dln_scale (contiguous [scale|bias] grads)");
@@ -641,7 +648,7 @@ extern "C" int msat_gru_ln_bwd_g4f(const float *dy, int32_t ldy, const float *g4
     const int NQ = (bias ? 6 : 2) + 3 * nfeat;
 #define MSAT_BWD1(PER, Q, F)                                                                                      \
     hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,   \
-                       ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed, feat, ldf)
+                       ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed, feat, ldf, rexp)
 #define MSAT_BWD(PER)                                                                                             \
     if (!bias) MSAT_BWD1(PER, 2, 0);                                                                               \
     else if (nfeat == 0) MSAT_BWD1(PER, 6, 0);                                                                     \
@@ -678,6 +685,29 @@ extern "C" int msat_gru_ln_bwd_g4f(const float *dy, int32_t ldy, const float *g4
                            reinterpret_cast<float4 *>(dfeat), 1);
     }
     return check_launch("partial_reduce4_kernel");
+}
+
+extern "C" int msat_gru_ln_bwd_g4f(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
+                                   int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh,
+                                   int32_t lddh, float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias,
+                                   float *dbi, float *dbh_n, const float *feat, int32_t ldf, int32_t nfeat,
+                                   float *dfeat, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
+                                   void *stream) {
+    return gru_ln_bwd_g4_impl(dy, ldy, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, dln_scale,
+                              dln_bias, dbi, dbh_n, feat, ldf, nfeat, dfeat, partial, R, H, accumulate_ln, nullptr,
+                              stream);
+}
+
+extern "C" int msat_gru_ln_bwd_g4fe(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,
+                                    int32_t ldp, const float *ln_scale, float *dGi, int32_t lddi, float *dGh,
+                                    int32_t lddh, float *dhprev, int32_t lddp, float *dln_scale, float *dln_bias,
+                                    float *dbi, float *dbh_n, const float *feat, int32_t ldf, int32_t nfeat,
+                                    float *dfeat, float *partial, int32_t R, int32_t H, int32_t accumulate_ln,
+                                    int32_t *rexp, void *stream) {
+    MSAT_REQUIRE(rexp, "gru_ln_bwd_g4fe: NULL rexp");
+    MSAT_REQUIRE((accumulate_ln >> 2) & 1, "gru_ln_bwd_g4fe: row exponents need the packed rows (flags bit 2)");
+    return gru_ln_bwd_g4_impl(dy, ldy, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, dln_scale,
+                              dln_bias, dbi, dbh_n, feat, ldf, nfeat, dfeat, partial, R, H, accumulate_ln, rexp, stream);
 }
 
 extern "C" int msat_gru_ln_bwd_g4(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,

@@ -85,6 +85,42 @@ __device__ __forceinline__ Split2 split2(const float2 &u) {
     return s;
 }
 
+// fp16x2 split: x = h + l, h = fp16(x), l = fp16(x - h) (x - h exact; 22 significant bits while x and
+// l stay in fp16's normal range).  Three fp16 MFMAs per product (h h, h l, l h) keep every term above
+// 3 * 2^-22 |a b|.  fp16's range is the caller's business: operands are scaled by exact powers of
+// two (f16x2_row_exp) or range-checked.
+struct SplitH4 {
+    uint2 p[2];
+};
+
+__device__ __forceinline__ SplitH4 splith4(const float4 &u) {
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    const float x[4] = {u.x, u.y, u.z, u.w};
+    f16x4 h, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const _Float16 a = (_Float16)x[j];
+        h[j] = a;
+        l[j] = (_Float16)(x[j] - (float)a);
+    }
+    SplitH4 s;
+    s.p[0] = __builtin_bit_cast(uint2, h);
+    s.p[1] = __builtin_bit_cast(uint2, l);
+    return s;
+}
+
+// Scale exponent of a row whose largest |x| is m, for the fp16x2 split: m * 2^e in [2^14, 2^15), so the
+// scaled row is inside fp16's range with its largest elements at full precision.  kExpZero marks an
+// all-zero row (no constraint); a non-finite m gives 0 (the Inf / NaN then propagates as in fp32).
+constexpr int kExpZero = 0x3fff;
+__device__ __forceinline__ int f16x2_row_exp(float m) {
+    if (!(m <= 3.402823466e38f)) return 0;
+    if (m == 0.0f) return kExpZero;
+    int E;
+    (void)frexpf(m, &E);  // m = f 2^E, f in [0.5, 1)
+    return 15 - E;
+}
+
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int w3off(int row, int ch) {  // byte offset of 16-byte chunk ch of row

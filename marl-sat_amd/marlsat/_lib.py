@@ -110,6 +110,10 @@ def _load():
                                   P])
     sig["msat_gemm_wgrad_workspace_bytes"] = (c_size_t, [c_int32, c_int32, c_int32])
     sig["msat_gemm_wgrad"] = (c_int32, [P, c_int32, P, c_int32, P, c_int32, c_int32, c_int32, c_int32, c_int32, P, P])
+    sig["msat_gemm_wgrad_h2"] = (c_int32, [P, c_int32, P, c_int32, P, P, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                           c_int32, P, P])
+    sig["msat_gemm_wgrad_rot"] = (c_int32, [P, c_int32, P, c_int32, P, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                            c_int32, P, P])
     I, F, Z, U = c_int32, c_float, c_size_t, c_uint64
     sig["msat_assemble_graph_batch"] = (I, [I, I, I, I, I] + [P] * 26 + [I, I, P])
     sig["msat_clause_gather"] = (I, [P, I, P, P, I, I, I, I, P])
@@ -131,6 +135,7 @@ def _load():
     sig["msat_split_f16x2_t"] = (I, [P, I, I, I, I, P, P, P])
     sig["msat_gru_ln_bwd_g4"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, I, P])
     sig["msat_gru_ln_bwd_g4f"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, P, P, I, I, I, P])
+    sig["msat_gru_ln_bwd_g4fe"] = (I, [P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, P, P, I, I, P, P, I, I, I, P, P])
     sig["msat_gru_ln_bwd_partial_floats"] = (Z, [I, I])
     sig["msat_gru_ln_bwd"] = (I, [P, I, P, I, P, I, P, I, P, P, I, P, I, P, I, P, P, P, I, I, I, P])
     sig["msat_colsum_workspace_floats"] = (Z, [I, I])
@@ -201,6 +206,7 @@ EXPORTED = (
     "msat_gru_ln_fused_fwd",
     "msat_gru_ln_bwd_g4",
     "msat_gru_ln_bwd_g4f",
+    "msat_gru_ln_bwd_g4fe",
     "msat_gru_ln_bwd_partial_floats",
     "msat_gru_ln_bwd",
     "msat_colsum_workspace_floats",
@@ -223,6 +229,8 @@ EXPORTED = (
     "msat_gemm_f64acc",
     "msat_gemm_wgrad_workspace_bytes",
     "msat_gemm_wgrad",
+    "msat_gemm_wgrad_rot",
+    "msat_gemm_wgrad_h2",
     "msat_last_error",
     "msat_version",
     "msat_pool_pack",

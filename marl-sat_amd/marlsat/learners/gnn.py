@@ -187,14 +187,36 @@ class GNNActorCritic:
         self._timed("gemm_x3r16_kernel (dgrad, bf16x3)", 2.0 * M * N * K, lambda: _chk(
             L_.msat_gemm_x3(A, lda, planes.data_ptr(), C, ldc, None, M, N, K, acc, self.stream), "msat_gemm_x3"))
 
-    def _wgrad(self, A, lda, G, ldg, W, ldw, M, K, N, acc=1):
+    def _wgrad(self, A, lda, G, ldg, W, ldw, M, K, N, acc=1, rot=0):
+        """W[:, (n + rot) % N] (+)= (A^T G)[:, n] (rot: the packed rows' gate-block rotation)."""
         if M == 0:
             return
         GNNActorCritic.flops += 2 * M * N * K
         ws = self.scr.get_ws(int(L_.msat_gemm_wgrad_workspace_bytes(M, K, N)))
-        label = "wgrad_skinny + reduce (K <= 8)" if K <= 8 else "wgrad_x3_kernel + reduce (bf16x3)"
+        if K <= 8:
+            label = "wgrad_skinny + reduce (K <= 8)"
+        elif N <= 384 and os.environ.get("MARLSAT_WGRAD_W", "1") != "0":
+            label = "wgrad_x3w_kernel + reduce (bf16x3)"
+        else:
+            label = "wgrad_x3_kernel + reduce (bf16x3)"
         self._timed(label, 2.0 * M * N * K, lambda: _chk(
-            L_.msat_gemm_wgrad(A, lda, G, ldg, W, ldw, M, K, N, acc, ws.data_ptr(), self.stream), "msat_gemm_wgrad"))
+            L_.msat_gemm_wgrad_rot(A, lda, G, ldg, W, ldw, M, K, N, rot, acc, ws.data_ptr(), self.stream),
+            "msat_gemm_wgrad_rot"))
+
+    # fp16x2 whole-row weight gradients of the GRU backward's packed rows (gemm_x3.hip wgrad_w_kernel<2>):
+    # the backward writes each row's scale exponent, the kernel scales G per row split
+    use_wgrad_h2 = os.environ.get("MARLSAT_WGRAD_H2", "1") != "0"
+
+    def _wgrad_h2(self, A, lda, G, ldg, rexp, W, ldw, M, K, N, acc=1, rot=0):
+        """W[:, (n + rot) % N] (+)= (A^T G)[:, n] in fp16x2; rexp: G's row scale exponents."""
+        if M == 0:
+            return
+        GNNActorCritic.flops += 2 * M * N * K
+        ws = self.scr.get_ws(int(L_.msat_gemm_wgrad_workspace_bytes(M, K, N)))
+        self._timed("wgrad_w_kernel<2> + fixup + reduce (fp16x2)", 2.0 * M * N * K, lambda: _chk(
+            L_.msat_gemm_wgrad_h2(A, lda, G, ldg, rexp.data_ptr(), W, ldw, M, K, N, rot, acc, ws.data_ptr(),
+                                  self.stream),
+            "msat_gemm_wgrad_h2"))
 
     def _colsum(self, G, ldg, M, N, out, acc=1):
         if M == 0:
@@ -512,13 +534,32 @@ class GNNActorCritic:
             dGI, dGH = e(R, W3), e(R, W3)
             return dGI.data_ptr(), dGH.data_ptr(), W3, (dGI, dGH)
 
-        def dF_wgrad(A, lda, dgi, ld, W, R, K):
+        h2 = packed and self.use_wgrad_h2
+
+        def dF_wgrad(A, lda, dgi, ld, W, R, K, rexp):
             """W (dF rows, ld 3H) += A^T dGi; in packed rows dGi's gate blocks are (n | r z)."""
-            if packed:
-                self._wgrad(A, lda, dgi, ld, pp_addr(W, 2 * H), W3, R, K, H)
-                self._wgrad(A, lda, dgi + 4 * H, ld, W, W3, R, K, 2 * H)
+            if h2:
+                self._wgrad_h2(A, lda, dgi, ld, rexp, W, W3, R, K, W3, rot=2 * H)
+            elif packed:
+                self._wgrad(A, lda, dgi, ld, W, W3, R, K, W3, rot=2 * H)
             else:
                 self._wgrad(A, lda, dgi, ld, W, W3, R, K, W3)
+
+        def Wh_wgrad(A, dgh, ld, W, R, rexp):
+            """W (ld 3H) += A^T dGh (A = the cell's previous state, ld H)."""
+            if h2:
+                self._wgrad_h2(A, H, dgh, ld, rexp, W, W3, R, H, W3)
+            else:
+                self._wgrad(A, H, dgh, ld, W, W3, R, H, W3)
+
+        def bwd(dHx, G4, Hx, ln_row, dgi, dgh, ldd, dHx0, dln_row, cell, feat, ldf, nfeat, dfeat, part, R, rexp):
+            args = (dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, ln_row, dgi, ldd, dgh, ldd,
+                    dHx0.data_ptr(), H, dln_row, dln_row + 4 * H, self.g(f"enc.{cell}_bi").data_ptr(),
+                    pp(self.g(f"enc.{cell}_bh"), 2 * H), feat, ldf, nfeat, dfeat, part.data_ptr(), R, H, flags)
+            if h2:
+                _chk(L_.msat_gru_ln_bwd_g4fe(*args, rexp.data_ptr(), self.stream), "gru_ln_bwd_g4fe")
+            else:
+                _chk(L_.msat_gru_ln_bwd_g4f(*args, self.stream), "gru_ln_bwd_g4f")
 
         pp_addr = lambda ptr, col: ptr + 4 * col
         for l in range(self.L - 1, -1, -1):
@@ -530,19 +571,17 @@ class GNNActorCritic:
                 dgi, dgh, ldd, keep = dG_buffers(Nv)
                 dHx0 = e(Nv, H)  # written (not accumulated) by the backward kernel: flags bit 1
                 part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nv, H)))
+                rexp = torch.empty(Nv, dtype=torch.int32, device=dev) if h2 else None
                 # dF rows H..H+5 (x, svf, n+, n-) from the same pass: feature-weighted gate sums
-                _chk(L_.msat_gru_ln_bwd_g4f(dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, pp(ln[k]),
-                                            dgi, ldd, dgh, ldd, dHx0.data_ptr(), H,
-                                            pp(dln[k]), pp(dln[k], H), self.g(f"enc.{cell}_bi").data_ptr(),
-                                            pp(self.g(f"enc.{cell}_bh"), 2 * H), b.vfeat.data_ptr(), 8, 6,
-                                            pp(gF[H]), part.data_ptr(), Nv, H, flags, self.stream), "gru_ln_bwd_g4f")
+                bwd(dHx, G4, Hx, pp(ln[k]), dgi, dgh, ldd, dHx0, pp(dln[k]), cell, b.vfeat.data_ptr(), 8, 6,
+                    pp(gF[H]), part, Nv, rexp)
                 wh, gwh = self.p(f"enc.{cell}_wh"), self.g(f"enc.{cell}_wh")
                 sfx = cell[-2:]
                 self._dgrad(dgh, ldd, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1)
-                self._wgrad(Hx.data_ptr(), H, dgh, ldd, gwh.data_ptr(), W3, Nv, H, W3)
+                Wh_wgrad(Hx.data_ptr(), dgh, ldd, gwh.data_ptr(), Nv, rexp)
                 # input path: d(gathered) and dF rows [fold | x/svf | counts]
                 self._dgrad(dgi, ldd, F, pl["Fp" if half == 0 else "Fn"], pp(dNV, half * H), 2 * H, Nv, H, W3, 0)
-                dF_wgrad(pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), Nv, H)
+                dF_wgrad(pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), Nv, H, rexp)
                 dprev[half] = dHx0
             # var gather backward: dH_c (+)= A+^T dNV+ + A-^T dNV-  (one merged clause gather)
             _chk(L_.msat_clause_gather2(dNV.data_ptr(), pp(dNV, H), 2 * H, b.slots.data_ptr(), dHc.data_ptr(), H, Nc,
@@ -551,16 +590,14 @@ class GNNActorCritic:
             dgi, dgh, ldd, keep = dG_buffers(Nc)
             dHc0 = e(Nc, H)
             part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nc, H)))
-            _chk(L_.msat_gru_ln_bwd_g4f(dHc.data_ptr(), H, t.G4c.data_ptr(), 4 * H, t.Hc.data_ptr(), H,
-                                        pp(ln[3 * l]), dgi, ldd, dgh, ldd, dHc0.data_ptr(), H,
-                                        pp(dln[3 * l]), pp(dln[3 * l], H), self.g("enc.gru_c_bi").data_ptr(),
-                                        pp(self.g("enc.gru_c_bh"), 2 * H), b.cdeg.data_ptr(), 4, 2,
-                                        pp(gFc[2 * H]), part.data_ptr(), Nc, H, flags, self.stream), "gru_ln_bwd_g4f")
+            rexp = torch.empty(Nc, dtype=torch.int32, device=dev) if h2 else None
+            bwd(dHc, t.G4c, t.Hc, pp(ln[3 * l]), dgi, dgh, ldd, dHc0, pp(dln[3 * l]), "gru_c", b.cdeg.data_ptr(), 4, 2,
+                pp(gFc[2 * H]), part, Nc, rexp)
             self._dgrad(dgh, ldd, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1)
-            self._wgrad(t.Hc.data_ptr(), H, dgh, ldd, self.g("enc.gru_c_wh").data_ptr(), W3, Nc, H, W3)
+            Wh_wgrad(t.Hc.data_ptr(), dgh, ldd, self.g("enc.gru_c_wh").data_ptr(), Nc, rexp)
             dGIN = e(Nc, 2 * H)
             self._dgrad(dgi, ldd, Fc, pl["Fc"], dGIN.data_ptr(), 2 * H, Nc, 2 * H, W3, 0)
-            dF_wgrad(t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), Nc, 2 * H)
+            dF_wgrad(t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), Nc, 2 * H, rexp)
             # clause gather backward: dH_v+/- (+)= A+/- dGIN+/-
             _chk(L_.msat_var_gather2(dGIN.data_ptr(), pp(dGIN, H), 2 * H, b.ptr.data_ptr(), b.inc.data_ptr(),
                                      dprev[0].data_ptr(), dprev[1].data_ptr(), H, Nv, H, 1, self.stream),

@@ -17,6 +17,7 @@ ROCPROF_NAMES = {  # bench label -> rocprof kernel names whose launches the benc
     "gru_ln_fused_fwd_h2r_kernel (fp16x2, + x3r fixup launch)": ["gru_ln_fused_fwd_h2r_kernel", "gru_ln_fused_fwd_x3r_kernel"],
     "gemm_x3r16_kernel (dgrad, bf16x3)": ["gemm_x3r16_kernel"],
     "wgrad_x3_kernel + reduce (bf16x3)": ["wgrad_x3_kernel", "wgrad_reduce4_kernel"],
+    "wgrad_x3w_kernel + reduce (bf16x3)": ["wgrad_x3w_kernel", "wgrad_reduce4_kernel"],
 }
 launches = {}
 for r in csv.DictReader(open(trace)):

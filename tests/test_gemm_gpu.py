@@ -94,16 +94,20 @@ def test_gemm_fast_path_shapes(M, N, K, transB, path, monkeypatch):
         _ref_close(C, ref, absprod)
 
 
-@pytest.mark.parametrize("path", ["1", "0", "x3"])  # register-staged / fp32 LDS-DMA / bf16x3 split (default)
+# register-staged / fp32 LDS-DMA / bf16x3 128x128 tiles / bf16x3 whole-row (default for N <= 384)
+@pytest.mark.parametrize("path", ["1", "0", "x3", "x3w"])
 @pytest.mark.parametrize("M,K,N", [(1, 4, 4), (33, 128, 384), (5000, 132, 384), (70001, 128, 128), (100, 256, 8),
-                                   (407001, 128, 384), (9999, 256, 260), (17, 16, 4)])
+                                   (407001, 128, 384), (9999, 256, 260), (17, 16, 4), (1000, 12, 36), (3000, 300, 384),
+                                   (2049, 256, 512)])
 def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
     """Row tails (M % 32 != 0, splits of uneven length) go through zero-filled slabs; the bf16x3
-    kernel (transposed LDS reads) is held to the same fp32 bound as the fp32 MFMA kernels."""
+    kernels (transposed LDS reads) are held to the same fp32 bound as the fp32 MFMA kernels."""
     from marlsat import _lib
 
-    monkeypatch.setenv("MARLSAT_GEMM", "0" if path == "x3" else path)
-    monkeypatch.setenv("MARLSAT_WGRAD_X3", "1" if path == "x3" else "0")
+    x3 = path in ("x3", "x3w")
+    monkeypatch.setenv("MARLSAT_GEMM", "0" if x3 else path)
+    monkeypatch.setenv("MARLSAT_WGRAD_X3", "1" if x3 else "0")
+    monkeypatch.setenv("MARLSAT_WGRAD_W", "1" if path == "x3w" else "0")
     g = torch.Generator(device="cuda").manual_seed(M + K + N)
     A = torch.randn(M, K, device="cuda", generator=g)
     G = torch.randn(M, N, device="cuda", generator=g)
@@ -116,6 +120,72 @@ def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
         ref = A.double().t() @ G.double() + (W0.double() if acc else 0)
         absprod = A.double().abs().t() @ G.double().abs() + (W0.double().abs() if acc else 0)
         _ref_close(W, ref, absprod)
+
+
+@pytest.mark.parametrize("path", ["x3w", "x3"])
+@pytest.mark.parametrize("M,K,N,rot,ldg", [(5000, 128, 384, 256, 512), (70001, 256, 384, 256, 512), (999, 128, 128, 32, 128),
+                                           (300, 256, 384, 128, 384)])
+def test_wgrad_rot(M, K, N, rot, ldg, path, monkeypatch):
+    """msat_gemm_wgrad_rot: W[:, (n + rot) % N] (+)= (A^T G)[:, n] (the packed GRU backward rows), on the
+    whole-row kernel's rotated store and on the two-range fallback; G read from a wider row (ld > N)."""
+    from marlsat import _lib
+
+    monkeypatch.setenv("MARLSAT_WGRAD_W", "1" if path == "x3w" else "0")
+    g = torch.Generator(device="cuda").manual_seed(M + K + N + rot)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    Gw = torch.randn(M, ldg, device="cuda", generator=g)
+    G = Gw[:, :N]
+    W0 = torch.randn(K, N, device="cuda", generator=g)
+    ws = torch.empty(int(_lib.lib.msat_gemm_wgrad_workspace_bytes(M, K, N)) // 4 + 1, device="cuda")
+    for acc in (0, 1):
+        W = W0.clone()
+        _lib.check(_lib.lib.msat_gemm_wgrad_rot(A.data_ptr(), K, Gw.data_ptr(), ldg, W.data_ptr(), N, M, K, N, rot, acc,
+                                                ws.data_ptr(), _lib.stream_ptr()), "wgrad_rot")
+        ref = torch.roll(A.double().t() @ G.double(), rot, dims=1) + (W0.double() if acc else 0)
+        absprod = torch.roll(A.double().abs().t() @ G.double().abs(), rot, dims=1) + (W0.double().abs() if acc else 0)
+        _ref_close(W, ref, absprod)
+
+
+def row_exp(G: torch.Tensor) -> torch.Tensor:
+    """The fp16x2 row scale exponent (split3.h f16x2_row_exp): max|row| * 2^e in [2^14, 2^15)."""
+    m = G.abs().amax(dim=1)
+    e = 15 - torch.frexp(m)[1]
+    return torch.where(m == 0, torch.full_like(e, 0x3FFF), e).to(torch.int32)
+
+
+@pytest.mark.parametrize("M,K,N,rot,ldg,amp", [(5000, 128, 384, 256, 512, 0), (70001, 256, 384, 256, 512, 0),
+                                               (999, 128, 128, 32, 128, 0), (300, 256, 384, 128, 384, 0),
+                                               (407001, 128, 384, 0, 512, 0), (20000, 128, 384, 0, 384, 1),
+                                               (3000, 16, 260, 4, 260, 0), (17, 16, 4, 0, 4, 0)])
+def test_wgrad_h2(M, K, N, rot, ldg, amp):
+    """fp16x2 whole-row weight gradient: rows of G spread over 10^-30 .. 10^2 (and all-zero rows), scaled
+    per split by the row exponents; amp = 1 puts |a| >= 2^15 into one split's A rows, which the bf16x3
+    fixup launch recomputes.  Held to the fp32 bound against fp64 (max err / sum|a g| printed)."""
+    from marlsat import _lib
+
+    g = torch.Generator(device="cuda").manual_seed(M + K + N + rot + amp)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    if amp:
+        A[M // 3: M // 3 + 5] *= 1e6
+    Gw = torch.randn(M, ldg, device="cuda", generator=g)
+    Gw *= torch.pow(10.0, torch.empty(M, 1, device="cuda").uniform_(-30, 2, generator=g))
+    Gw[::7] = 0
+    G = Gw[:, :N]
+    rexp = row_exp(Gw)
+    W0 = torch.randn(K, N, device="cuda", generator=g)
+    ws = torch.empty(int(_lib.lib.msat_gemm_wgrad_workspace_bytes(M, K, N)) // 4 + 1, device="cuda")
+    for acc in (0, 1):
+        W = W0.clone()
+        _lib.check(_lib.lib.msat_gemm_wgrad_h2(A.data_ptr(), K, Gw.data_ptr(), ldg, rexp.data_ptr(), W.data_ptr(), N, M,
+                                               K, N, rot, acc, ws.data_ptr(), _lib.stream_ptr()), "wgrad_h2")
+        ref = torch.roll(A.double().t() @ G.double(), rot, dims=1) + (W0.double() if acc else 0)
+        absprod = torch.roll(A.double().abs().t() @ G.double().abs(), rot, dims=1) + (W0.double().abs() if acc else 0)
+        _ref_close(W, ref, absprod, rtol=4e-6)
+        W1 = W.clone()
+        if not acc:
+            _lib.check(_lib.lib.msat_gemm_wgrad_h2(A.data_ptr(), K, Gw.data_ptr(), ldg, rexp.data_ptr(), W.data_ptr(),
+                                                   N, M, K, N, rot, 0, ws.data_ptr(), _lib.stream_ptr()), "wgrad_h2")
+            assert torch.equal(W, W1)  # bitwise reproducible
 
 
 @pytest.mark.parametrize("M,K,N,lda,aoff,ldw", [(1, 1, 4, 1, 0, 4), (1000, 3, 384, 4, 1, 384), (300001, 4, 384, 8, 4, 384),
