@@ -43,6 +43,15 @@ int msat_split_bf16x3_rot(const float *W, int32_t rows, int32_t cols, int32_t ld
                           void *stream);
 int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, float *C, int32_t ldc, const float *bias,
                  int32_t M, int32_t N, int32_t K, int32_t accumulate, void *stream);
+/* fp16x2 form of msat_gemm_x3 for A = a GRU backward's packed rows with their row scale exponents
+ * (rexp, msat_gru_ln_bwd_g4fe): three fp16 MFMAs per product.  Wplanes_h2 = msat_split_f16x2_rot of W
+ * (fp16x2 planes of 2^10 W, *wbad = 1 if that overflowed), Wplanes_x3 = msat_split_bf16x3_rot of the
+ * same W: with *wbad set the kernel runs the bf16x3 product instead.  K % 32 == 0. */
+int msat_split_f16x2_rot(const float *W, int32_t rows, int32_t cols, int32_t ldw, int32_t rot, void *planes,
+                         int32_t *wbad, void *stream);
+int msat_gemm_h2(const float *A, int32_t lda, const int32_t *rexp, const void *Wplanes_h2, const void *Wplanes_x3,
+                 const int32_t *wbad, float *C, int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K,
+                 int32_t accumulate, void *stream);
 
 /* W[K,N] (+)= A[M,K]^T @ G[M,N]: split over M, partial slabs reduced in a fixed order.
  * K <= 8 (feature / degree columns) streams G once instead of running 128-row MFMA tiles. */

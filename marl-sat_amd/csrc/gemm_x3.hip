@@ -569,6 +569,240 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
 }
 
 // ---------------------------------------------------------------------------------------------
+// fp16x2 form of the register-A data gradient (msat_gemm_h2): C[M,N] (+)= A[M,K] @ W^T for A = a GRU
+// backward's packed rows, whose row scale exponents rexp (written by that backward, split3.h
+// f16x2_row_exp) put every scaled row inside fp16's range with its largest elements at full
+// precision.  Each lane's activation rows are fixed (register-A: lane l holds row l & 15 of each 16-row
+// tile), so a row's scale is one load per tile, the split is x 2^e -> (h, l) in registers, and the
+// epilogue rescales each output row by 2^-(e + kDgW) (exact).  Weights: [2][N][K] fp16x2 planes of
+// 2^kDgW W (msat_split_f16x2_rot), two LDS images per slab instead of three.  Three fp16 MFMAs per
+// 16x16x32 block instead of six bf16.  If the weight split overflowed (*wbad), the kernel runs the
+// bf16x3 body on the bf16x3 planes instead (same grid and LDS).
+constexpr int kDgW = 10;  // weight scale 2^10: |W| < 32 fits
+
+template <int RT, int NP>
+__device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int lda, const int *__restrict__ rexp,
+                                              const uint16_t *__restrict__ Wp, float *__restrict__ C, int ldc,
+                                              const float *__restrict__ bias, int M, int N, int K, int accumulate,
+                                              int ntn, int vec_out, uint4 (*lds_w)[3][kX3M * 4]) {
+    typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    const int m0 = (id / ntn) * 64 * RT, n0 = (id % ntn) * kX3M;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63, l16 = lane & 15, g = lane >> 4;
+    const int wr = w * 16 * RT;
+    const float *arow[RT];
+    int ea[RT];  // fp16x2: the scale exponent of this lane's activation row in each tile
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        const int r = min(m0 + wr + 16 * i + l16, M - 1);
+        arow[i] = A + (size_t)r * lda + 8 * g;
+        if constexpr (NP == 2) {
+            const int e = rexp[r];
+            ea[i] = e == kExpZero ? 0 : e;
+        }
+    }
+    // weight DMA: 8 NP wave-instructions (1 KiB = 16 rows x 4 chunks) per double slab, 2 NP per wave
+    constexpr int PW = 2 * NP;
+    unsigned voff[PW];
+#pragma unroll
+    for (int e = 0; e < PW; ++e) {
+        const int x = PW * w + e, q = x >> 3, p = x & 7, row = 16 * p + (lane >> 2);
+        const int ch = (lane & 3) ^ x3swz16((row >> 2) & 3);
+        voff[e] = (unsigned)(((size_t)q * N * K + (size_t)min(n0 + row, N - 1) * K + 8 * ch) * 2);
+    }
+    auto issueW = [&](int d, int buf) {
+        const char *base = reinterpret_cast<const char *>(Wp) + (size_t)d * 64;
+#pragma unroll
+        for (int e = 0; e < PW; ++e) {
+            const int x = PW * w + e;
+            glds16_async_s(base, voff[e], &lds_w[buf][x >> 3][64 * (x & 7)]);
+        }
+    };
+    f32x4 acc[RT][8];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
+    float4 ra[RT][2];
+    auto loadA = [&](int d) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) ra[i][e] = *reinterpret_cast<const float4 *>(arow[i] + 32 * d + 4 * e);
+    };
+    const int slot = g ^ x3swz16((l16 >> 2) & 3);
+    const int nd = K / 32;
+    loadA(0);
+    issueW(0, 0);
+    wait_vmcnt<0>();
+    barrier_lds();
+    for (int d = 0; d < nd; ++d) {
+        const int buf = d & 1;
+        uint4 fa[RT][NP];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            if constexpr (NP == 3) {
+                const Split8 sp = split8(ra[i][0], ra[i][1]);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) fa[i][q] = sp.p[q];
+            } else {
+                const float4 u = ra[i][0], v = ra[i][1];
+                const int e = ea[i];
+                const SplitH4 s0 = splith4(make_float4(ldexpf(u.x, e), ldexpf(u.y, e), ldexpf(u.z, e), ldexpf(u.w, e)));
+                const SplitH4 s1 = splith4(make_float4(ldexpf(v.x, e), ldexpf(v.y, e), ldexpf(v.z, e), ldexpf(v.w, e)));
+                fa[i][0] = make_uint4(s0.p[0].x, s0.p[0].y, s1.p[0].x, s1.p[0].y);
+                fa[i][1] = make_uint4(s0.p[1].x, s0.p[1].y, s1.p[1].x, s1.p[1].y);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bool more = d + 1 < nd;
+        if (more) issueW(d + 1, buf ^ 1);
+        if (more) loadA(d + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint4 fb[NP];
+#pragma unroll
+            for (int q = 0; q < NP; ++q) fb[q] = lds_w[buf][q][(16 * j + l16) * 4 + slot];
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                f32x4 c = acc[i][j];
+                if constexpr (NP == 3) {
+                    auto m = [](const uint4 &a, const uint4 &b, const f32x4 &c) {
+                        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                                       __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+                    };
+                    c = m(fa[i][2], fb[0], c);
+                    c = m(fa[i][1], fb[1], c);
+                    c = m(fa[i][0], fb[2], c);
+                    c = m(fa[i][1], fb[0], c);
+                    c = m(fa[i][0], fb[1], c);
+                    c = m(fa[i][0], fb[0], c);
+                } else {
+                    auto m = [](const uint4 &a, const uint4 &b, const f32x4 &c) {
+                        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8v, a),
+                                                                      __builtin_bit_cast(f16x8v, b), c, 0, 0, 0);
+                    };
+                    c = m(fa[i][0], fb[1], c);  // h l
+                    c = m(fa[i][1], fb[0], c);  // l h
+                    c = m(fa[i][0], fb[0], c);  // h h
+                }
+                acc[i][j] = c;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) wait_vmcnt<2 * RT>();
+        else wait_vmcnt<0>();
+        barrier_lds();
+    }
+    // fp16x2: rescale each output row (C/D map: row 4 (lane >> 4) + reg of the tile) by 2^-(e + kDgW)
+    if constexpr (NP == 2) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int e = rexp[min(m0 + wr + 16 * i + 4 * g + reg, M - 1)];
+                const int sh = -((e == kExpZero ? 0 : e) + kDgW);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[i][j][reg] = ldexpf(acc[i][j][reg], sh);
+            }
+    }
+    float *stage = reinterpret_cast<float *>(&lds_w[0][0][0]) + w * 32 * 64;
+    if (vec_out) {
+        auto stage_sync = [&] {
+            if (accumulate) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            else __syncthreads();
+        };
+#pragma unroll
+        for (int i0 = 0; i0 < RT; i0 += 2) {
+            float4 o[2][8];
+#pragma unroll
+            for (int hc = 0; hc < 2; ++hc) {
+                const int col = n0 + 64 * hc + l16 * 4;
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int row = m0 + wr + 16 * i0 + it * 4 + g;
+                    if (accumulate && row < M && col < N)
+                        o[hc][it] = *reinterpret_cast<const float4 *>(C + (size_t)row * ldc + col);
+                }
+            }
+#pragma unroll
+            for (int hc = 0; hc < 2; ++hc) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                        for (int reg = 0; reg < 4; ++reg)
+                            stage[(16 * i + 4 * g + reg) * 64 + 16 * jj + l16] = acc[i0 + i][4 * hc + jj][reg];
+                stage_sync();
+                const int col = n0 + 64 * hc + l16 * 4;
+                float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (bias && col < N) bv = *reinterpret_cast<const float4 *>(bias + col);
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int rr = it * 4 + g;
+                    const int row = m0 + wr + 16 * i0 + rr;
+                    float4 v = *reinterpret_cast<const float4 *>(stage + rr * 64 + l16 * 4);
+                    v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+                    if (accumulate) {
+                        const float4 &ov = o[hc][it];
+                        v.x = ov.x + v.x; v.y = ov.y + v.y; v.z = ov.z + v.z; v.w = ov.w + v.w;
+                    }
+                    if (row < M && col < N) *reinterpret_cast<float4 *>(C + (size_t)row * ldc + col) = v;
+                }
+                stage_sync();
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int col = n0 + 16 * j + l16;
+            if (col >= N) continue;
+            const float bv = bias ? bias[col] : 0.0f;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int row = m0 + wr + 16 * i + 4 * g + reg;
+                if (row >= M) continue;
+                float *c = C + (size_t)row * ldc + col;
+                const float v = acc[i][j][reg] + bv;
+                *c = accumulate ? *c + v : v;
+            }
+        }
+}
+
+template <int RT>
+__global__ void __launch_bounds__(kX3T, RT == 2 ? 3 : 2)
+gemm_h2r16_kernel(const float *__restrict__ A, int lda, const int *__restrict__ rexp, const uint16_t *__restrict__ Wh2,
+                  const uint16_t *__restrict__ Wx3, const int *__restrict__ wbad, float *__restrict__ C, int ldc,
+                  const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
+    __shared__ uint4 lds_w[2][3][kX3M * 4];  // 48 KiB (the fp16x2 body uses two of the three images)
+    if (*wbad)
+        gemm_r16_body<RT, 3>(A, lda, nullptr, Wx3, C, ldc, bias, M, N, K, accumulate, ntn, vec_out, lds_w);
+    else
+        gemm_r16_body<RT, 2>(A, lda, rexp, Wh2, C, ldc, bias, M, N, K, accumulate, ntn, vec_out, lds_w);
+}
+
+// planes[q][r][c] = part q of 2^kDgW W[r][(c + rot) % cols] (fp16x2, q = 0, 1); *bad = 1 if a scaled
+// weight is outside (-2^15, 2^15) or not finite (msat_gemm_h2 then runs its bf16x3 body)
+__global__ void split_f16x2_rot_kernel(const float *__restrict__ W, int rows, int cols, int ldw, int rot,
+                                       _Float16 *__restrict__ out, int *__restrict__ bad) {
+    const size_t n = (size_t)rows * cols;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / cols, c = i - r * cols;
+        const size_t cs = c + rot < (size_t)cols ? c + rot : c + rot - cols;
+        const float x = W[r * ldw + cs] * (float)(1 << kDgW);
+        const _Float16 p = (_Float16)x;
+        out[i] = p;
+        out[n + i] = (_Float16)(x - (float)p);
+        if (!(fabsf(x) < 32768.0f)) *bad = 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Weight gradient on the same split: part[s][k][n] = sum_{m in split s} A[m][k] G[m][n].
 // The MFMA reduction runs over the rows m, so both fragments are 8-row column strips.  Both
 // operands are staged row-major as three bf16 planes [16 rows][128 cols] (256-byte rows, chunks
@@ -1031,4 +1265,33 @@ int msat_wgrad_h2w_launch(const float *A, int lda, const float *G, int ldg, cons
     hipLaunchKernelGGL((wgrad_w_kernel<3, true>), dim3(ktiles * splits), dim3(kWWT), 0, s, A, lda, G, ldg, nullptr,
                        part, M, K, N, rot, rows16, ktiles, flags);
     return check_launch("wgrad_w_kernel<3> (fixup)");
+}
+
+extern "C" int msat_split_f16x2_rot(const float *W, int32_t rows, int32_t cols, int32_t ldw, int32_t rot, void *planes,
+                                    int32_t *bad, void *stream) {
+    MSAT_REQUIRE(W && planes && bad && rows > 0 && cols > 0 && ldw >= cols && rot >= 0 && rot < cols,
+                 "bad split_f16x2_rot args");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(bad, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("split_f16x2_rot memset");
+    const size_t n = (size_t)rows * cols;
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(split_f16x2_rot_kernel, dim3(grid), dim3(256), 0, s, W, rows, cols, ldw, rot,
+                       reinterpret_cast<_Float16 *>(planes), bad);
+    return check_launch("split_f16x2_rot_kernel");
+}
+
+extern "C" int msat_gemm_h2(const float *A, int32_t lda, const int32_t *rexp, const void *Wplanes_h2,
+                            const void *Wplanes_x3, const int32_t *wbad, float *C, int32_t ldc, const float *bias,
+                            int32_t M, int32_t N, int32_t K, int32_t accumulate, void *stream) {
+    if (M == 0) return MSAT_OK;
+    MSAT_REQUIRE(A && rexp && Wplanes_h2 && Wplanes_x3 && wbad && C && M > 0 && N > 0 && K > 0, "bad gemm_h2 args");
+    MSAT_REQUIRE(K % 32 == 0 && lda % 4 == 0 && lda >= K && ldc >= N && a16x3(A) && a16x3(Wplanes_h2) &&
+                     a16x3(Wplanes_x3),
+                 "gemm_h2: K %% 32, lda %% 4 and 16-byte aligned operands required");
+    const int ntn = (N + kX3M - 1) / kX3M, ntm = (M + 127) / 128;
+    const int vec = (N % 4 == 0 && ldc % 4 == 0 && a16x3(C) && (!bias || a16x3(bias))) ? 1 : 0;
+    hipLaunchKernelGGL((gemm_h2r16_kernel<2>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda, rexp,
+                       reinterpret_cast<const uint16_t *>(Wplanes_h2), reinterpret_cast<const uint16_t *>(Wplanes_x3),
+                       wbad, C, ldc, bias, M, N, K, accumulate, ntn, vec);
+    return check_launch("gemm_h2r16_kernel");
 }

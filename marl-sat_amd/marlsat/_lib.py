@@ -122,6 +122,8 @@ def _load():
     sig["msat_split_bf16x3"] = (I, [P, I, I, I, P, P])
     sig["msat_split_bf16x3_rot"] = (I, [P, I, I, I, I, P, P])
     sig["msat_gemm_x3"] = (I, [P, I, P, P, I, P, I, I, I, I, P])
+    sig["msat_split_f16x2_rot"] = (I, [P, I, I, I, I, P, P, P])
+    sig["msat_gemm_h2"] = (I, [P, I, P, P, P, P, P, I, P, I, I, I, I, P])
     sig["msat_clause_gather2"] = (I, [P, P, I, P, P, I, I, I, I, I, P])
     sig["msat_var_gather2"] = (I, [P, P, I, P, P, P, P, I, I, I, I, P])
     sig["msat_gru_ln_fwd"] = (I, [P, I, P, I, P, I, P, P, P, I, I, I, P])
@@ -200,6 +202,8 @@ EXPORTED = (
     "msat_split_bf16x3",
     "msat_split_bf16x3_rot",
     "msat_gemm_x3",
+    "msat_split_f16x2_rot",
+    "msat_gemm_h2",
     "msat_clause_gather2",
     "msat_var_gather2",
     "msat_gru_ln_fwd",

@@ -178,8 +178,33 @@ class GNNActorCritic:
             out[key] = buf
         return out
 
-    def _dgrad(self, A, lda, Wm: torch.Tensor, planes, C, ldc, M, N, K, acc):
-        """C[M,N] (+)= A[M,K] @ Wm[:N]^T (Wm rows = N, row stride K)."""
+    # fp16x2 data gradients of the packed backward rows (gemm_x3.hip gemm_h2r16_kernel)
+    use_dgrad_h2 = os.environ.get("MARLSAT_DGRAD_H2", "1") != "0"
+
+    def _split_weights_f16(self, mats):
+        """fp16x2 planes (2^10 W, msat_split_f16x2_rot) of each block of `mats` (as _split_weights):
+        ({key: planes tensor}, {key: wbad pointer}); wbad[key] = 1 if the block overflowed fp16."""
+        bad = torch.empty(len(mats), dtype=torch.int32, device=self.device)
+        out, bp = {}, {}
+        for i, (key, (Wm, rot)) in enumerate(mats.items()):
+            rows, cols = Wm.shape
+            buf = torch.empty(2 * rows * cols + 8, dtype=torch.int16, device=self.device)
+            _chk(L_.msat_split_f16x2_rot(Wm.data_ptr(), rows, cols, cols, rot, buf.data_ptr(), self._ptr(bad, i),
+                                         self.stream), "split_f16x2_rot")
+            out[key], bp[key] = buf, self._ptr(bad, i)
+        out["_bad"] = bad  # keep-alive
+        return out, bp
+
+    def _dgrad(self, A, lda, Wm: torch.Tensor, planes, C, ldc, M, N, K, acc, h2=None):
+        """C[M,N] (+)= A[M,K] @ Wm[:N]^T (Wm rows = N, row stride K).  h2 = (fp16x2 planes, wbad pointer,
+        A's row exponents): the fp16x2 kernel (its bf16x3 body on `planes` if the split overflowed)."""
+        if h2 is not None and M > 0:
+            p2, wbad, rexp = h2
+            GNNActorCritic.flops += 2 * M * N * K
+            self._timed("gemm_h2r16_kernel (dgrad, fp16x2)", 2.0 * M * N * K, lambda: _chk(
+                L_.msat_gemm_h2(A, lda, rexp.data_ptr(), p2.data_ptr(), planes.data_ptr(), wbad, C, ldc, None, M, N,
+                                K, acc, self.stream), "msat_gemm_h2"))
+            return
         if planes is None:
             self._gemm(A, lda, Wm.data_ptr(), K, 1, C, ldc, None, M, N, K, acc)
             return
@@ -196,7 +221,7 @@ class GNNActorCritic:
         if K <= 8:
             label = "wgrad_skinny + reduce (K <= 8)"
         elif N <= 384 and os.environ.get("MARLSAT_WGRAD_W", "1") != "0":
-            label = "wgrad_x3w_kernel + reduce (bf16x3)"
+            label = "wgrad_w_kernel<3> + reduce (bf16x3)"
         else:
             label = "wgrad_x3_kernel + reduce (bf16x3)"
         self._timed(label, 2.0 * M * N * K, lambda: _chk(
@@ -525,6 +550,9 @@ class GNNActorCritic:
                 "Fn": (Fn[:H], rot)}
         pl = self._split_weights(mats) if self.use_x3 else {k: None for k in mats}
         flags = 3 | (4 if packed else 0)
+        dh2 = packed and self.use_dgrad_h2
+        pl2, wbad = self._split_weights_f16(mats) if dh2 else (None, None)
+        hx = lambda key, rexp: (pl2[key], wbad[key], rexp) if dh2 else None
 
         def dG_buffers(R):
             """-> (dGi ptr, dGh ptr, ld, keep-alive tensor)"""
@@ -535,6 +563,7 @@ class GNNActorCritic:
             return dGI.data_ptr(), dGH.data_ptr(), W3, (dGI, dGH)
 
         h2 = packed and self.use_wgrad_h2
+        need_rexp = h2 or dh2
 
         def dF_wgrad(A, lda, dgi, ld, W, R, K, rexp):
             """W (dF rows, ld 3H) += A^T dGi; in packed rows dGi's gate blocks are (n | r z)."""
@@ -556,7 +585,7 @@ class GNNActorCritic:
             args = (dHx.data_ptr(), H, G4.data_ptr(), 4 * H, Hx.data_ptr(), H, ln_row, dgi, ldd, dgh, ldd,
                     dHx0.data_ptr(), H, dln_row, dln_row + 4 * H, self.g(f"enc.{cell}_bi").data_ptr(),
                     pp(self.g(f"enc.{cell}_bh"), 2 * H), feat, ldf, nfeat, dfeat, part.data_ptr(), R, H, flags)
-            if h2:
+            if need_rexp:
                 _chk(L_.msat_gru_ln_bwd_g4fe(*args, rexp.data_ptr(), self.stream), "gru_ln_bwd_g4fe")
             else:
                 _chk(L_.msat_gru_ln_bwd_g4f(*args, self.stream), "gru_ln_bwd_g4f")
@@ -571,16 +600,17 @@ class GNNActorCritic:
                 dgi, dgh, ldd, keep = dG_buffers(Nv)
                 dHx0 = e(Nv, H)  # written (not accumulated) by the backward kernel: flags bit 1
                 part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nv, H)))
-                rexp = torch.empty(Nv, dtype=torch.int32, device=dev) if h2 else None
+                rexp = torch.empty(Nv, dtype=torch.int32, device=dev) if need_rexp else None
                 # dF rows H..H+5 (x, svf, n+, n-) from the same pass: feature-weighted gate sums
                 bwd(dHx, G4, Hx, pp(ln[k]), dgi, dgh, ldd, dHx0, pp(dln[k]), cell, b.vfeat.data_ptr(), 8, 6,
                     pp(gF[H]), part, Nv, rexp)
                 wh, gwh = self.p(f"enc.{cell}_wh"), self.g(f"enc.{cell}_wh")
                 sfx = cell[-2:]
-                self._dgrad(dgh, ldd, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1)
+                self._dgrad(dgh, ldd, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1, hx("wh_" + sfx, rexp))
                 Wh_wgrad(Hx.data_ptr(), dgh, ldd, gwh.data_ptr(), Nv, rexp)
                 # input path: d(gathered) and dF rows [fold | x/svf | counts]
-                self._dgrad(dgi, ldd, F, pl["Fp" if half == 0 else "Fn"], pp(dNV, half * H), 2 * H, Nv, H, W3, 0)
+                fk = "Fp" if half == 0 else "Fn"
+                self._dgrad(dgi, ldd, F, pl[fk], pp(dNV, half * H), 2 * H, Nv, H, W3, 0, hx(fk, rexp))
                 dF_wgrad(pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), Nv, H, rexp)
                 dprev[half] = dHx0
             # var gather backward: dH_c (+)= A+^T dNV+ + A-^T dNV-  (one merged clause gather)
@@ -590,13 +620,14 @@ class GNNActorCritic:
             dgi, dgh, ldd, keep = dG_buffers(Nc)
             dHc0 = e(Nc, H)
             part = self.scr.get_part(int(L_.msat_gru_ln_bwd_partial_floats(Nc, H)))
-            rexp = torch.empty(Nc, dtype=torch.int32, device=dev) if h2 else None
+            rexp = torch.empty(Nc, dtype=torch.int32, device=dev) if need_rexp else None
             bwd(dHc, t.G4c, t.Hc, pp(ln[3 * l]), dgi, dgh, ldd, dHc0, pp(dln[3 * l]), "gru_c", b.cdeg.data_ptr(), 4, 2,
                 pp(gFc[2 * H]), part, Nc, rexp)
-            self._dgrad(dgh, ldd, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1)
+            self._dgrad(dgh, ldd, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1,
+                        hx("wh_c", rexp))
             Wh_wgrad(t.Hc.data_ptr(), dgh, ldd, self.g("enc.gru_c_wh").data_ptr(), Nc, rexp)
             dGIN = e(Nc, 2 * H)
-            self._dgrad(dgi, ldd, Fc, pl["Fc"], dGIN.data_ptr(), 2 * H, Nc, 2 * H, W3, 0)
+            self._dgrad(dgi, ldd, Fc, pl["Fc"], dGIN.data_ptr(), 2 * H, Nc, 2 * H, W3, 0, hx("Fc", rexp))
             dF_wgrad(t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), Nc, 2 * H, rexp)
             # clause gather backward: dH_v+/- (+)= A+/- dGIN+/-
             _chk(L_.msat_var_gather2(dGIN.data_ptr(), pp(dGIN, H), 2 * H, b.ptr.data_ptr(), b.inc.data_ptr(),

@@ -188,6 +188,41 @@ def test_wgrad_h2(M, K, N, rot, ldg, amp):
             assert torch.equal(W, W1)  # bitwise reproducible
 
 
+@pytest.mark.parametrize("M,N,K,rot,lda,wbig,acc", [(1, 128, 384, 256, 512, 0, 0), (130, 128, 384, 0, 512, 0, 1),
+                                                     (70001, 256, 384, 256, 512, 0, 0), (4999, 128, 384, 0, 384, 0, 1),
+                                                     (3000, 130, 96, 32, 100, 0, 1), (257, 128, 384, 256, 512, 1, 1)])
+def test_gemm_h2(M, N, K, rot, lda, wbig, acc):
+    """fp16x2 data gradient C (+)= A @ W^T with per-row scale exponents: rows of A spread over 10^-30 .. 10^2
+    and all-zero rows; W's gate blocks rotated as in the packed backward (planes of W[:, (c + rot) % K]);
+    wbig = 1 puts a weight >= 32 in W (fp16 overflow at 2^10 scale), which runs the bf16x3 body."""
+    from marlsat import _lib
+
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + rot + wbig)
+    Aw = torch.randn(M, lda, device="cuda", generator=g)
+    Aw *= torch.pow(10.0, torch.empty(M, 1, device="cuda").uniform_(-30, 2, generator=g))
+    Aw[::5] = 0
+    A = Aw[:, :K]
+    rexp = row_exp(Aw)
+    W = torch.randn(N, K, device="cuda", generator=g) * 0.1
+    if wbig:
+        W[3, 7] = 40.0
+    C0 = torch.randn(M, N, device="cuda", generator=g)
+    p2 = torch.empty(2 * N * K + 8, dtype=torch.int16, device="cuda")
+    p3 = torch.empty(3 * N * K + 8, dtype=torch.int16, device="cuda")
+    bad = torch.empty(1, dtype=torch.int32, device="cuda")
+    s = _lib.stream_ptr()
+    _lib.check(_lib.lib.msat_split_f16x2_rot(W.data_ptr(), N, K, K, rot, p2.data_ptr(), bad.data_ptr(), s), "split")
+    _lib.check(_lib.lib.msat_split_bf16x3_rot(W.data_ptr(), N, K, K, rot, p3.data_ptr(), s), "split3")
+    assert int(bad) == wbig
+    C = C0.clone()
+    _lib.check(_lib.lib.msat_gemm_h2(Aw.data_ptr(), lda, rexp.data_ptr(), p2.data_ptr(), p3.data_ptr(), bad.data_ptr(),
+                                     C.data_ptr(), N, None, M, N, K, acc, s), "gemm_h2")
+    Wr = torch.roll(W.double(), -rot, dims=1)  # planes hold W[:, (c + rot) % K]
+    ref = A.double() @ Wr.t() + (C0.double() if acc else 0)
+    absprod = A.double().abs() @ Wr.abs().t() + (C0.double().abs() if acc else 0)
+    _ref_close(C, ref, absprod)
+
+
 @pytest.mark.parametrize("M,K,N,lda,aoff,ldw", [(1, 1, 4, 1, 0, 4), (1000, 3, 384, 4, 1, 384), (300001, 4, 384, 8, 4, 384),
                                                 (77777, 8, 260, 8, 0, 264), (5000, 5, 128, 7, 2, 132),
                                                 (64, 2, 768, 2, 0, 768)])
