@@ -49,6 +49,12 @@ int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, float *C, int
  * same W: with *wbad set the kernel runs the bf16x3 product instead.  K % 32 == 0. */
 int msat_split_f16x2_rot(const float *W, int32_t rows, int32_t cols, int32_t ldw, int32_t rot, void *planes,
                          int32_t *wbad, void *stream);
+/* Both data gradients of a GRU cell's packed backward rows in one launch: C0 (+)= A0 @ W0^T (N0 columns)
+ * and C1 (+)= A1 @ W1^T (N1) over the same M rows (row exponents rexp), each as msat_gemm_h2. */
+int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h2, const void *W0_x3, const int32_t *wbad0,
+                      float *C0, int32_t ldc0, int32_t N0, int32_t acc0, const float *A1, int32_t lda1,
+                      const void *W1_h2, const void *W1_x3, const int32_t *wbad1, float *C1, int32_t ldc1, int32_t N1,
+                      int32_t acc1, const int32_t *rexp, int32_t M, int32_t K, void *stream);
 int msat_gemm_h2(const float *A, int32_t lda, const int32_t *rexp, const void *Wplanes_h2, const void *Wplanes_x3,
                  const int32_t *wbad, float *C, int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K,
                  int32_t accumulate, void *stream);
@@ -65,6 +71,13 @@ int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int32_t ldg, fl
 int msat_gemm_wgrad_h2(const float *A, int32_t lda, const float *G, int32_t ldg, const int32_t *rexp, float *W,
                        int32_t ldw, int32_t M, int32_t K, int32_t N, int32_t rot, int32_t accumulate, void *workspace,
                        void *stream);
+/* Both weight gradients of a GRU cell's packed backward rows in one fp16x2 launch: W0 (+)= A0^T G0 and
+ * W1 (+)= A1^T G1 (columns rotated by rot0 / rot1) over the same M rows, row exponents rexp. */
+size_t msat_gemm_wgrad_dual_workspace_bytes(int32_t M, int32_t K0, int32_t N0, int32_t K1, int32_t N1);
+int msat_gemm_wgrad_h2_dual(const float *A0, int32_t lda0, const float *G0, int32_t ldg0, float *W0, int32_t ldw0,
+                            int32_t K0, int32_t N0, int32_t rot0, const float *A1, int32_t lda1, const float *G1,
+                            int32_t ldg1, float *W1, int32_t ldw1, int32_t K1, int32_t N1, int32_t rot1,
+                            const int32_t *rexp, int32_t M, int32_t accumulate, void *workspace, void *stream);
 int msat_gemm_wgrad_rot(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
                         int32_t M, int32_t K, int32_t N, int32_t rot, int32_t accumulate, void *workspace,
                         void *stream);

@@ -584,10 +584,8 @@ template <int RT, int NP>
 __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int lda, const int *__restrict__ rexp,
                                               const uint16_t *__restrict__ Wp, float *__restrict__ C, int ldc,
                                               const float *__restrict__ bias, int M, int N, int K, int accumulate,
-                                              int ntn, int vec_out, uint4 (*lds_w)[3][kX3M * 4]) {
+                                              int m0, int n0, int vec_out, uint4 (*lds_w)[3][kX3M * 4]) {
     typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
-    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
-    const int m0 = (id / ntn) * 64 * RT, n0 = (id % ntn) * kX3M;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int wr = w * 16 * RT;
     const float *arow[RT];
@@ -780,10 +778,42 @@ gemm_h2r16_kernel(const float *__restrict__ A, int lda, const int *__restrict__ 
                   const uint16_t *__restrict__ Wx3, const int *__restrict__ wbad, float *__restrict__ C, int ldc,
                   const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
     __shared__ uint4 lds_w[2][3][kX3M * 4];  // 48 KiB (the fp16x2 body uses two of the three images)
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    const int m0 = (id / ntn) * 64 * RT, n0 = (id % ntn) * kX3M;
     if (*wbad)
-        gemm_r16_body<RT, 3>(A, lda, nullptr, Wx3, C, ldc, bias, M, N, K, accumulate, ntn, vec_out, lds_w);
+        gemm_r16_body<RT, 3>(A, lda, nullptr, Wx3, C, ldc, bias, M, N, K, accumulate, m0, n0, vec_out, lds_w);
     else
-        gemm_r16_body<RT, 2>(A, lda, rexp, Wh2, C, ldc, bias, M, N, K, accumulate, ntn, vec_out, lds_w);
+        gemm_r16_body<RT, 2>(A, lda, rexp, Wh2, C, ldc, bias, M, N, K, accumulate, m0, n0, vec_out, lds_w);
+}
+
+// Two data gradients of the same packed rows in one launch (a GRU cell's dh and d(input)): for each
+// 128-row block the n tiles of both products are consecutive workgroup ids, so the workgroups that read
+// the same rows of the packed buffer run together on one XCD and all but the first read them from L2.
+struct DgradProblem {
+    const float *A;
+    int lda;
+    const uint16_t *Wh2, *Wx3;
+    const int *wbad;
+    float *C;
+    int ldc, N, accumulate, vec_out, ntn;
+};
+
+template <int RT>
+__global__ void __launch_bounds__(kX3T, RT == 2 ? 3 : 2)
+gemm_h2r16_dual_kernel(DgradProblem p0, DgradProblem p1, const int *__restrict__ rexp, int M, int K) {
+    __shared__ uint4 lds_w[2][3][kX3M * 4];
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    const int T = p0.ntn + p1.ntn, sub = id % T;
+    const int m0 = (id / T) * 64 * RT;
+    const bool first = sub < p0.ntn;
+    const DgradProblem &p = first ? p0 : p1;
+    const int n0 = (first ? sub : sub - p0.ntn) * kX3M;
+    if (*p.wbad)
+        gemm_r16_body<RT, 3>(p.A, p.lda, nullptr, p.Wx3, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0,
+                             p.vec_out, lds_w);
+    else
+        gemm_r16_body<RT, 2>(p.A, p.lda, rexp, p.Wh2, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0, p.vec_out,
+                             lds_w);
 }
 
 // planes[q][r][c] = part q of 2^kDgW W[r][(c + rot) % cols] (fp16x2, q = 0, 1); *bad = 1 if a scaled
@@ -963,23 +993,24 @@ wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ 
 constexpr int kWWT = 512;
 constexpr int kWWN = 384;  // widest N
 
+typedef unsigned short WwLds[2][12][kW3Plane];  // [buf][A planes | G planes]: 96 KiB
+
+// one workgroup's share: split sp (rows sp * rows_per_split ..), k tile k0; flag: this workgroup's
+// range flag (fp16x2), lds: the kernel's WwLds
 template <int NP, bool IL>
-__global__ void __launch_bounds__(kWWT, 1)
-wgrad_w_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G, int ldg, const int *__restrict__ rexp,
-               float *__restrict__ part, int M, int K, int N, int rot, int rows_per_split, int ktiles,
-               int *__restrict__ flags) {
+__device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int lda, const float *__restrict__ G, int ldg,
+                                             const int *__restrict__ rexp, float *__restrict__ part, int M, int K,
+                                             int N, int rot, int rows_per_split, int sp, int k0, int *flag,
+                                             WwLds &ldsr) {
     // [buf][A planes 0 .. NP-1 | G plane q, column block u at NP + 3 q + u]
-    __shared__ __attribute__((aligned(16))) unsigned short lds[2][4 * NP][kW3Plane];
-    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
-    if (NP == 3 && flags && flags[id] == 0) return;  // fixup launch: only the flagged workgroups
-    const int sp = id / ktiles, k0 = (id % ktiles) * kX3M;
+    unsigned short (*lds)[4 * NP][kW3Plane] = reinterpret_cast<unsigned short (*)[4 * NP][kW3Plane]>(&ldsr[0][0][0]);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const int wk = (w & 1) * 64, wn = __builtin_amdgcn_readfirstlane((w >> 1) * 96);
     const int rb = sp * rows_per_split, re = min(M, rb + rows_per_split);
     const int ns = (re - rb + 15) / 16;
     int ge = 0;  // fp16x2: G scale exponent of this split
     if constexpr (NP == 2) {
-        __shared__ int red[kWWT / 64];
+        int *red = reinterpret_cast<int *>(&ldsr[1][11][0]);  // the last image: free until the first store
         int mn = kExpZero;
         for (int r = rb + t; r < re; r += kWWT) mn = min(mn, rexp[r]);
 #pragma unroll
@@ -1127,7 +1158,7 @@ wgrad_w_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G
     }
     if constexpr (NP == 2) {
         const int bad = __syncthreads_or(!(amax < 32768.0f));
-        if (t == 0) flags[id] = bad;
+        if (t == 0) *flag = bad;
         if (bad) return;
     }
     float *P = part + (size_t)sp * K * N;
@@ -1144,6 +1175,45 @@ wgrad_w_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G
                 if (row < K) P[(size_t)row * N + oc] = NP == 2 ? ldexpf(acc[i][j][reg], -ge) : acc[i][j][reg];
             }
         }
+}
+
+template <int NP, bool IL>
+__global__ void __launch_bounds__(kWWT, 1)
+wgrad_w_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G, int ldg, const int *__restrict__ rexp,
+               float *__restrict__ part, int M, int K, int N, int rot, int rows_per_split, int ktiles,
+               int *__restrict__ flags) {
+    __shared__ __attribute__((aligned(16))) WwLds lds;
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    if (NP == 3 && flags && flags[id] == 0) return;  // fixup launch: only the flagged workgroups
+    wgrad_w_body<NP, IL>(A, lda, G, ldg, rexp, part, M, K, N, rot, rows_per_split, id / ktiles, (id % ktiles) * kX3M,
+                         flags ? flags + id : nullptr, lds);
+}
+
+// Two weight gradients over the same rows of G's buffer in one launch (a GRU cell's dWh = h^T dGh and
+// dF = x^T dGi, both from the packed backward rows): the k tiles of both products for one row split
+// are consecutive workgroup ids, so they stream the same rows together (L2 hits for all but one).
+struct WgradProblem {
+    const float *A;
+    int lda;
+    const float *G;
+    int ldg;
+    float *part;
+    int K, N, rot, ktiles;
+};
+
+template <int NP>
+__global__ void __launch_bounds__(kWWT, 1)
+wgrad_w_dual_kernel(WgradProblem p0, WgradProblem p1, const int *__restrict__ rexp, int M, int rows_per_split,
+                    int *__restrict__ flags) {
+    __shared__ __attribute__((aligned(16))) WwLds lds;
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    if (NP == 3 && flags[id] == 0) return;  // fixup launch: only the flagged workgroups
+    const int T = p0.ktiles + p1.ktiles, sub = id % T, sp = id / T;
+    const bool first = sub < p0.ktiles;
+    const WgradProblem &p = first ? p0 : p1;
+    const int k0 = (first ? sub : sub - p0.ktiles) * kX3M;
+    wgrad_w_body<NP, true>(p.A, p.lda, p.G, p.ldg, rexp, p.part, M, p.K, p.N, p.rot, rows_per_split, sp, k0, flags + id,
+                           lds);
 }
 
 static bool a16x3(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -1253,6 +1323,26 @@ int msat_wgrad_x3w_launch(const float *A, int lda, const float *G, int ldg, floa
     return check_launch("wgrad_w_kernel<3> (bf16x3)");
 }
 
+int msat_wgrad_dual_splits(int M, int K0, int K1) {
+    const int T = (K0 + kX3M - 1) / kX3M + (K1 + kX3M - 1) / kX3M;
+    return std::max(1, std::min(std::max(1, 256 / T), (M + 511) / 512));
+}
+
+// both products of a cell (wgrad_w_dual_kernel, fp16x2) + the bf16x3 fixup over the flagged workgroups
+int msat_wgrad_h2_dual_launch(const float *A0, int lda0, const float *G0, int ldg0, float *part0, int K0, int N0, int rot0,
+                              const float *A1, int lda1, const float *G1, int ldg1, float *part1, int K1, int N1,
+                              int rot1, const int *rexp, int M, int splits, int *flags, hipStream_t s) {
+    WgradProblem p0 = {A0, lda0, G0, ldg0, part0, K0, N0, rot0, (K0 + kX3M - 1) / kX3M};
+    WgradProblem p1 = {A1, lda1, G1, ldg1, part1, K1, N1, rot1, (K1 + kX3M - 1) / kX3M};
+    const int rows = (M + splits - 1) / splits, rows16 = ((rows + 15) / 16) * 16;
+    const dim3 grid(splits * (p0.ktiles + p1.ktiles));
+    hipLaunchKernelGGL(wgrad_w_dual_kernel<2>, grid, dim3(kWWT), 0, s, p0, p1, rexp, M, rows16, flags);
+    const int rc = check_launch("wgrad_w_dual_kernel<2> (fp16x2)");
+    if (rc) return rc;
+    hipLaunchKernelGGL(wgrad_w_dual_kernel<3>, grid, dim3(kWWT), 0, s, p0, p1, rexp, M, rows16, flags);
+    return check_launch("wgrad_w_dual_kernel<3> (fixup)");
+}
+
 // fp16x2 form + its bf16x3 fixup launch over the workgroups it flagged (flags: ktiles * splits ints)
 int msat_wgrad_h2w_launch(const float *A, int lda, const float *G, int ldg, const int *rexp, float *part, int M, int K,
                           int N, int rot, int splits, int *flags, hipStream_t s) {
@@ -1294,4 +1384,43 @@ extern "C" int msat_gemm_h2(const float *A, int32_t lda, const int32_t *rexp, co
                        reinterpret_cast<const uint16_t *>(Wplanes_h2), reinterpret_cast<const uint16_t *>(Wplanes_x3),
                        wbad, C, ldc, bias, M, N, K, accumulate, ntn, vec);
     return check_launch("gemm_h2r16_kernel");
+}
+
+// C0 (+)= A0 @ W0^T and C1 (+)= A1 @ W1^T over the same M rows (one row-exponent array), in one launch
+// (gemm_h2r16_dual_kernel).  Conditions of msat_gemm_h2 for each product; no bias.
+extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h2, const void *W0_x3,
+                                 const int32_t *wbad0, float *C0, int32_t ldc0, int32_t N0, int32_t acc0,
+                                 const float *A1, int32_t lda1, const void *W1_h2, const void *W1_x3,
+                                 const int32_t *wbad1, float *C1, int32_t ldc1, int32_t N1, int32_t acc1,
+                                 const int32_t *rexp, int32_t M, int32_t K, void *stream) {
+    if (M == 0) return MSAT_OK;
+    MSAT_REQUIRE(A0 && A1 && W0_h2 && W0_x3 && W1_h2 && W1_x3 && wbad0 && wbad1 && C0 && C1 && rexp && M > 0 &&
+                     N0 > 0 && N1 > 0 && K > 0,
+                 "bad gemm_h2_dual args");
+    MSAT_REQUIRE(K % 32 == 0 && lda0 % 4 == 0 && lda1 % 4 == 0 && lda0 >= K && lda1 >= K && ldc0 >= N0 && ldc1 >= N1 &&
+                     a16x3(A0) && a16x3(A1) && a16x3(W0_h2) && a16x3(W0_x3) && a16x3(W1_h2) && a16x3(W1_x3),
+                 "gemm_h2_dual: K %% 32, lda %% 4 and 16-byte aligned operands required");
+    DgradProblem p[2];
+    const float *As[2] = {A0, A1};
+    const int ldas[2] = {lda0, lda1}, ldcs[2] = {ldc0, ldc1}, Ns[2] = {N0, N1}, accs[2] = {acc0, acc1};
+    const void *W2[2] = {W0_h2, W1_h2}, *W3[2] = {W0_x3, W1_x3};
+    const int32_t *wb[2] = {wbad0, wbad1};
+    float *Cs[2] = {C0, C1};
+    for (int i = 0; i < 2; ++i) {
+        p[i].A = As[i];
+        p[i].lda = ldas[i];
+        p[i].Wh2 = reinterpret_cast<const uint16_t *>(W2[i]);
+        p[i].Wx3 = reinterpret_cast<const uint16_t *>(W3[i]);
+        p[i].wbad = wb[i];
+        p[i].C = Cs[i];
+        p[i].ldc = ldcs[i];
+        p[i].N = Ns[i];
+        p[i].accumulate = accs[i];
+        p[i].vec_out = (Ns[i] % 4 == 0 && ldcs[i] % 4 == 0 && a16x3(Cs[i])) ? 1 : 0;
+        p[i].ntn = (Ns[i] + kX3M - 1) / kX3M;
+    }
+    const int ntm = (M + 127) / 128;
+    hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(kX3T), 0,
+                       (hipStream_t)stream, p[0], p[1], rexp, M, K);
+    return check_launch("gemm_h2r16_dual_kernel");
 }

@@ -181,6 +181,32 @@ class GNNActorCritic:
     # fp16x2 data gradients of the packed backward rows (gemm_x3.hip gemm_h2r16_kernel)
     use_dgrad_h2 = os.environ.get("MARLSAT_DGRAD_H2", "1") != "0"
 
+    # a cell's two data gradients / two weight gradients in one launch each (gemm_x3.hip *_dual_kernel)
+    use_dual = os.environ.get("MARLSAT_DUAL", "1") != "0"
+
+    def _dgrad_dual(self, p0, p1, rexp, M, K):
+        """p = (A, lda, fp16x2 planes, bf16x3 planes, wbad pointer, C, ldc, N, accumulate): both
+        C (+)= A @ W^T products over the same M rows (row exponents rexp) in one fp16x2 launch."""
+        if M == 0:
+            return
+        fl = 2.0 * M * K * (p0[7] + p1[7])
+        GNNActorCritic.flops += fl
+        self._timed("gemm_h2r16_kernel (dgrad, fp16x2)", fl, lambda: _chk(L_.msat_gemm_h2_dual(
+            p0[0], p0[1], p0[2].data_ptr(), p0[3].data_ptr(), p0[4], p0[5], p0[6], p0[7], p0[8],
+            p1[0], p1[1], p1[2].data_ptr(), p1[3].data_ptr(), p1[4], p1[5], p1[6], p1[7], p1[8],
+            rexp.data_ptr(), M, K, self.stream), "msat_gemm_h2_dual"))
+
+    def _wgrad_h2_dual(self, p0, p1, rexp, M, acc=1):
+        """p = (A, lda, G, ldg, W, ldw, K, N, rot): both W[:, (n + rot) % N] (+)= (A^T G)[:, n] over the same M
+        rows of G's buffer (row exponents rexp) in one fp16x2 launch."""
+        if M == 0:
+            return
+        fl = 2.0 * M * (p0[6] * p0[7] + p1[6] * p1[7])
+        GNNActorCritic.flops += fl
+        ws = self.scr.get_ws(int(L_.msat_gemm_wgrad_dual_workspace_bytes(M, p0[6], p0[7], p1[6], p1[7])))
+        self._timed("wgrad_w_kernel<2> + fixup + reduce (fp16x2)", fl, lambda: _chk(L_.msat_gemm_wgrad_h2_dual(
+            *p0, *p1, rexp.data_ptr(), M, acc, ws.data_ptr(), self.stream), "msat_gemm_wgrad_h2_dual"))
+
     def _split_weights_f16(self, mats):
         """fp16x2 planes (2^10 W, msat_split_f16x2_rot) of each block of `mats` (as _split_weights):
         ({key: planes tensor}, {key: wbad pointer}); wbad[key] = 1 if the block overflowed fp16."""
@@ -564,6 +590,7 @@ class GNNActorCritic:
 
         h2 = packed and self.use_wgrad_h2
         need_rexp = h2 or dh2
+        dual = h2 and dh2 and self.use_dual
 
         def dF_wgrad(A, lda, dgi, ld, W, R, K, rexp):
             """W (dF rows, ld 3H) += A^T dGi; in packed rows dGi's gate blocks are (n | r z)."""
@@ -606,12 +633,19 @@ class GNNActorCritic:
                     pp(gF[H]), part, Nv, rexp)
                 wh, gwh = self.p(f"enc.{cell}_wh"), self.g(f"enc.{cell}_wh")
                 sfx = cell[-2:]
-                self._dgrad(dgh, ldd, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1, hx("wh_" + sfx, rexp))
-                Wh_wgrad(Hx.data_ptr(), dgh, ldd, gwh.data_ptr(), Nv, rexp)
-                # input path: d(gathered) and dF rows [fold | x/svf | counts]
                 fk = "Fp" if half == 0 else "Fn"
-                self._dgrad(dgi, ldd, F, pl[fk], pp(dNV, half * H), 2 * H, Nv, H, W3, 0, hx(fk, rexp))
-                dF_wgrad(pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), Nv, H, rexp)
+                if dual:  # dh and d(gathered) in one launch, dWh and dF in another (same packed rows)
+                    self._dgrad_dual((dgh, ldd, pl2["wh_" + sfx], pl["wh_" + sfx], wbad["wh_" + sfx], dHx0.data_ptr(),
+                                      H, H, 1),
+                                     (dgi, ldd, pl2[fk], pl[fk], wbad[fk], pp(dNV, half * H), 2 * H, H, 0), rexp, Nv, W3)
+                    self._wgrad_h2_dual((Hx.data_ptr(), H, dgh, ldd, gwh.data_ptr(), W3, H, W3, 0),
+                                        (pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), W3, H, W3, 2 * H), rexp, Nv)
+                else:
+                    self._dgrad(dgh, ldd, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1, hx("wh_" + sfx, rexp))
+                    Wh_wgrad(Hx.data_ptr(), dgh, ldd, gwh.data_ptr(), Nv, rexp)
+                    # input path: d(gathered) and dF rows [fold | x/svf | counts]
+                    self._dgrad(dgi, ldd, F, pl[fk], pp(dNV, half * H), 2 * H, Nv, H, W3, 0, hx(fk, rexp))
+                    dF_wgrad(pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), Nv, H, rexp)
                 dprev[half] = dHx0
             # var gather backward: dH_c (+)= A+^T dNV+ + A-^T dNV-  (one merged clause gather)
             _chk(L_.msat_clause_gather2(dNV.data_ptr(), pp(dNV, H), 2 * H, b.slots.data_ptr(), dHc.data_ptr(), H, Nc,
@@ -623,12 +657,19 @@ class GNNActorCritic:
             rexp = torch.empty(Nc, dtype=torch.int32, device=dev) if need_rexp else None
             bwd(dHc, t.G4c, t.Hc, pp(ln[3 * l]), dgi, dgh, ldd, dHc0, pp(dln[3 * l]), "gru_c", b.cdeg.data_ptr(), 4, 2,
                 pp(gFc[2 * H]), part, Nc, rexp)
-            self._dgrad(dgh, ldd, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1,
-                        hx("wh_c", rexp))
-            Wh_wgrad(t.Hc.data_ptr(), dgh, ldd, self.g("enc.gru_c_wh").data_ptr(), Nc, rexp)
             dGIN = e(Nc, 2 * H)
-            self._dgrad(dgi, ldd, Fc, pl["Fc"], dGIN.data_ptr(), 2 * H, Nc, 2 * H, W3, 0, hx("Fc", rexp))
-            dF_wgrad(t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), Nc, 2 * H, rexp)
+            if dual:
+                self._dgrad_dual((dgh, ldd, pl2["wh_c"], pl["wh_c"], wbad["wh_c"], dHc0.data_ptr(), H, H, 1),
+                                 (dgi, ldd, pl2["Fc"], pl["Fc"], wbad["Fc"], dGIN.data_ptr(), 2 * H, 2 * H, 0), rexp, Nc,
+                                 W3)
+                self._wgrad_h2_dual((t.Hc.data_ptr(), H, dgh, ldd, self.g("enc.gru_c_wh").data_ptr(), W3, H, W3, 0),
+                                    (t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), W3, 2 * H, W3, 2 * H), rexp, Nc)
+            else:
+                self._dgrad(dgh, ldd, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1,
+                            hx("wh_c", rexp))
+                Wh_wgrad(t.Hc.data_ptr(), dgh, ldd, self.g("enc.gru_c_wh").data_ptr(), Nc, rexp)
+                self._dgrad(dgi, ldd, Fc, pl["Fc"], dGIN.data_ptr(), 2 * H, Nc, 2 * H, W3, 0, hx("Fc", rexp))
+                dF_wgrad(t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), Nc, 2 * H, rexp)
             # clause gather backward: dH_v+/- (+)= A+/- dGIN+/-
             _chk(L_.msat_var_gather2(dGIN.data_ptr(), pp(dGIN, H), 2 * H, b.ptr.data_ptr(), b.inc.data_ptr(),
                                      dprev[0].data_ptr(), dprev[1].data_ptr(), H, Nv, H, 1, self.stream),

@@ -18,8 +18,9 @@ ROCPROF_NAMES = {  # bench label -> rocprof kernel names whose launches the benc
     "gemm_x3r16_kernel (dgrad, bf16x3)": ["gemm_x3r16_kernel"],
     "wgrad_x3_kernel + reduce (bf16x3)": ["wgrad_x3_kernel", "wgrad_reduce4_kernel"],
     "wgrad_w_kernel<3> + reduce (bf16x3)": ["wgrad_w_kernel<3", "wgrad_reduce4_kernel"],
-    "wgrad_w_kernel<2> + fixup + reduce (fp16x2)": ["wgrad_w_kernel<2", "wgrad_w_kernel<3", "wgrad_reduce4_kernel"],
-    "gemm_h2r16_kernel (dgrad, fp16x2)": ["gemm_h2r16_kernel"],
+    "wgrad_w_kernel<2> + fixup + reduce (fp16x2)": ["wgrad_w_dual_kernel<2", "wgrad_w_dual_kernel<3",
+                                                    "wgrad_reduce4_kernel"],
+    "gemm_h2r16_kernel (dgrad, fp16x2)": ["gemm_h2r16_dual_kernel"],
 }
 launches = {}
 for r in csv.DictReader(open(trace)):

@@ -345,3 +345,56 @@ def test_gemm_x3_register_a_bitwise(M, N, K, lda, monkeypatch):
         Ak = A[:, :K].double()
         _ref_close(C, Ak @ W.double().t() + (C0.double() if acc else 0),
                    Ak.abs() @ W.double().abs().t() + (C0.double().abs() if acc else 0))
+
+
+@pytest.mark.parametrize("M,K1", [(1, 128), (4999, 128), (70001, 256)])
+def test_dual_launches_match_fp64(M, K1):
+    """A GRU cell's two data gradients (msat_gemm_h2_dual) and two weight gradients (msat_gemm_wgrad_h2_dual)
+    from one packed buffer D = [dan | dar | daz | dan r] (ld 4H): dh (+)= D[:, H:] @ Wh^T, dx = D[:, :3H] @ F^T,
+    dWh (+)= h^T D[:, H:], dF (+)= x^T D[:, :3H] rotated by 2H -- each against fp64 at the fp32 bound."""
+    from marlsat import _lib
+
+    H = 128
+    g = torch.Generator(device="cuda").manual_seed(M + K1)
+    D = torch.randn(M, 4 * H, device="cuda", generator=g)
+    D *= torch.pow(10.0, torch.empty(M, 1, device="cuda").uniform_(-12, 1, generator=g))
+    rexp = row_exp(D)
+    Wh = torch.randn(H, 3 * H, device="cuda", generator=g) * 0.1   # dh rows N0 = H, K = 3H
+    F = torch.randn(K1, 3 * H, device="cuda", generator=g) * 0.1   # dx rows N1 = K1
+    s = _lib.stream_ptr()
+    planes = []
+    for Wm in (Wh, F):
+        n, k = Wm.shape
+        p2 = torch.empty(2 * n * k + 8, dtype=torch.int16, device="cuda")
+        p3 = torch.empty(3 * n * k + 8, dtype=torch.int16, device="cuda")
+        bad = torch.empty(1, dtype=torch.int32, device="cuda")
+        rot = 0 if Wm is Wh else 2 * H
+        _lib.check(_lib.lib.msat_split_f16x2_rot(Wm.data_ptr(), n, k, k, rot, p2.data_ptr(), bad.data_ptr(), s), "s2")
+        _lib.check(_lib.lib.msat_split_bf16x3_rot(Wm.data_ptr(), n, k, k, rot, p3.data_ptr(), s), "s3")
+        planes.append((p2, p3, bad))
+    C0 = torch.randn(M, H, device="cuda", generator=g)
+    dh = C0.clone()
+    dx = torch.empty(M, K1, device="cuda")
+    dgh, dgi = D[:, H:], D[:, :3 * H]
+    _lib.check(_lib.lib.msat_gemm_h2_dual(
+        dgh.data_ptr(), 4 * H, planes[0][0].data_ptr(), planes[0][1].data_ptr(), planes[0][2].data_ptr(), dh.data_ptr(),
+        H, H, 1, dgi.data_ptr(), 4 * H, planes[1][0].data_ptr(), planes[1][1].data_ptr(), planes[1][2].data_ptr(),
+        dx.data_ptr(), K1, K1, 0, rexp.data_ptr(), M, 3 * H, s), "dual dgrad")
+    Fr = torch.roll(F.double(), -2 * H, dims=1)
+    _ref_close(dh, dgh.double() @ Wh.double().t() + C0.double(),
+               dgh.double().abs() @ Wh.double().abs().t() + C0.double().abs())
+    _ref_close(dx, dgi.double() @ Fr.t(), dgi.double().abs() @ Fr.abs().t())
+    hx = torch.randn(M, H, device="cuda", generator=g)
+    xx = torch.randn(M, K1, device="cuda", generator=g)
+    W0 = torch.randn(H, 3 * H, device="cuda", generator=g)
+    W1 = torch.randn(K1, 3 * H, device="cuda", generator=g)
+    gW0, gW1 = W0.clone(), W1.clone()
+    ws = torch.empty(int(_lib.lib.msat_gemm_wgrad_dual_workspace_bytes(M, H, 3 * H, K1, 3 * H)) // 4 + 1, device="cuda")
+    _lib.check(_lib.lib.msat_gemm_wgrad_h2_dual(
+        hx.data_ptr(), H, dgh.data_ptr(), 4 * H, gW0.data_ptr(), 3 * H, H, 3 * H, 0,
+        xx.data_ptr(), K1, dgi.data_ptr(), 4 * H, gW1.data_ptr(), 3 * H, K1, 3 * H, 2 * H,
+        rexp.data_ptr(), M, 1, ws.data_ptr(), s), "dual wgrad")
+    _ref_close(gW0, hx.double().t() @ dgh.double() + W0.double(),
+               hx.double().abs().t() @ dgh.double().abs() + W0.double().abs(), rtol=4e-6)
+    _ref_close(gW1, torch.roll(xx.double().t() @ dgi.double(), 2 * H, dims=1) + W1.double(),
+               torch.roll(xx.double().abs().t() @ dgi.double().abs(), 2 * H, dims=1) + W1.double().abs(), rtol=4e-6)
