@@ -707,7 +707,8 @@ gru_ln_fused_fwd_x3_kernel(GruFwdArgs a) {
 // launched next with the same flags, recomputes exactly the flagged tiles.
 constexpr int kH2Shift = 10;  // weight scale 2^10: |W| < 32 fits, |W| >= 2^-24 keeps 11 bits
 
-__device__ __forceinline__ int gswz16(int b) { return (0x1E >> (2 * b)) & 3; }  // {0, 2, 3, 1}
+
+__device__ __forceinline__ int gswz16(int b) { return (0x78 >> (2 * b)) & 3; }  // {0, 2, 3, 1}
 
 struct GruX3rArgs {
     const float *seg[3];
@@ -871,6 +872,10 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
                 __builtin_amdgcn_sched_barrier(0);  // keep the blocks in order (the reads lead by one)
             }
         }
+        // Every asm load must complete within the step that issued it: hipcc treats an asm output as
+        // ready at the asm and reuses or moves its registers at the loop back-edge (leaving the step-s+2
+        // activations in flight across it, vmcnt(2) here, faulted: the late data landed in registers the
+        // latch block had reassigned to index arithmetic).
         await0(ras[PB]);
         barrier_lds();
     };

@@ -56,10 +56,13 @@ for cell, R, segs_w, segs_ld in (("clause", RC, (2 * H, 4), (2 * H, 4)), ("var",
                                                         H, gp, 4 * H, R, H, flags.data_ptr(), bad.data_ptr(), s),
         }
         for name, fn in runs.items():
+            if name not in os.environ.get("GRU_KERNELS", "x3r,h2r").split(",") or str(tape) not in os.environ.get(
+                    "GRU_TAPE", "False,True"):
+                continue
             for _ in range(3):
                 assert fn() == 0
             torch.cuda.synchronize()
-            n = 10
+            n = int(os.environ.get("GRU_REPS", "10"))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(n):
