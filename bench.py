@@ -18,9 +18,10 @@ PPO minibatches (forward, loss, backward, gradient all-reduce over RCCL when N>1
 Adam) and the cycle metrics -- timed after one warm-up cycle.  The headline leg is
 uf100-430 x 4096 envs (BASELINE config 3, the metric's 4096 envs), T = 8; uf50-218 x
 1024 envs, T = 32 (config 2) is reported beside it.  Each leg carries per-phase times
-and a per-kernel table of the matrix kernels (HIP events around each launch), and its
-roofline is the dominant kernel's fp32-equivalent TFLOP/s against the ceiling of the
-instruction it issues (bf16 dense / 6 for the bf16x3 kernels).
+and a per-kernel table of the matrix kernels (HIP events around each launch, algorithmic
+FLOPs and HBM bytes per launch), and its roofline is the dominant kernel's against the lower
+of its two roofs: the ceiling of the matrix instruction it issues (fp16 dense / 3 for the
+fp16x2 kernels, bf16 dense / 6 for bf16x3) and its intensity x the 8 TB/s HBM peak.
 
 Prints ONE JSON line on rank 0.
 """
@@ -188,8 +189,9 @@ def kernel_table(ktimer: dict) -> list:
     for the fp32 ones).  Sorted by total time."""
     rows = []
     for label, recs in ktimer.items():
-        ms = sum(a.elapsed_time(b) for a, b, _ in recs)
-        fl = sum(f for _, _, f in recs)
+        ms = sum(a.elapsed_time(b) for a, b, _, _ in recs)
+        fl = sum(f for _, _, f, _ in recs)
+        nb = sum(n for _, _, _, n in recs)
         if "K <= 8" in label:
             peak, unit_note = None, "HBM-bound (K <= 8 columns), not priced against a matrix peak"
         elif "fp16x2" in label:
@@ -199,11 +201,44 @@ def kernel_table(ktimer: dict) -> list:
         else:
             peak, unit_note = FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA peak"
         tf = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-        rows.append({"kernel": label, "launches": len(recs), "ms_total": ms, "ms_avg": ms / len(recs),
-                     "tflops_fp32_equiv": tf, "peak": peak, "frac": (tf / peak) if peak else None,
-                     "peak_basis": unit_note})
+        gbs = nb / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        row = {"kernel": label, "launches": len(recs), "ms_total": ms, "ms_avg": ms / len(recs),
+               "tflops_fp32_equiv": tf, "peak": peak, "frac": (tf / peak) if peak else None,
+               "peak_basis": unit_note, "algorithmic_bytes_avg": nb / len(recs), "hbm_GBps": gbs,
+               "hbm_frac": gbs / HBM_PEAK_GBS}
+        if peak and nb > 0:
+            # roofline: attainable = min(matrix ceiling, intensity x HBM peak); frac against the lower roof
+            inten = fl / nb  # fp32-equivalent FLOP per algorithmic byte
+            roof = min(peak, inten * HBM_PEAK_GBS / 1e3)
+            row.update({"intensity_flop_per_byte": inten, "bound": "mfma" if peak <= roof + 1e-9 else "hbm",
+                        "attainable_tflops": roof, "roofline_frac": tf / roof})
+        rows.append(row)
     rows.sort(key=lambda r: -r["ms_total"])
     return rows
+
+
+def mappo_roofline(dom: dict) -> dict:
+    """The MAPPO leg's roofline object for its dominant matrix kernel: against the lower of its two roofs
+    (the matrix ceiling of the instruction it issues, and its algorithmic intensity x the HBM peak).
+    HBM-bound: achieved = algorithmic GB/s vs 8 TB/s; MFMA-bound: fp32-equivalent TF/s vs the ceiling.
+    Both views are carried either way."""
+    hbm = dom.get("bound") == "hbm"
+    r = {"bound": "hbm" if hbm else "mfma", "kernel": dom["kernel"],
+         "achieved": dom["hbm_GBps"] if hbm else dom["tflops_fp32_equiv"],
+         "peak": HBM_PEAK_GBS if hbm else dom["peak"], "unit": "GB/s" if hbm else "TFLOP/s (fp32-equivalent)",
+         "frac": dom["hbm_frac"] if hbm else dom["frac"], "traffic": None,
+         "kernel_ms": dom["ms_avg"], "launches": dom["launches"],
+         "algorithmic_bytes_per_launch": dom.get("algorithmic_bytes_avg"),
+         "mfma": {"achieved_tflops_fp32_equiv": dom["tflops_fp32_equiv"], "peak": dom["peak"], "frac": dom["frac"],
+                  "peak_basis": dom["peak_basis"]},
+         "hbm": {"achieved_GBps": dom["hbm_GBps"], "peak": HBM_PEAK_GBS, "frac": dom["hbm_frac"]},
+         "intensity_flop_per_byte": dom.get("intensity_flop_per_byte"),
+         "frac_of_attainable": dom.get("roofline_frac"),
+         "note": "dominant matrix kernel of the timed cycle; algorithmic fp32 FLOPs (2*R*3H*(H+Kx) per GRU call, "
+                 "2*M*N*K per GEMM) and algorithmic HBM bytes (operands once + results, GRU: x, h in, h' and the "
+                 "4H tape out) over its launches' summed duration (HIP events on the launch stream); rocprofv3 "
+                 "trace of the same leg, timed-cycle slice: profiles/r02_mappo_uf100-430_slice.json"}
+    return r
 
 
 def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
@@ -281,15 +316,11 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
                    "envs_per_gpu": B, "NUM_STEPS": T, "UPDATE_EPOCHS": E, "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"],
                    "GNN_HIDDEN_DIM": H, "GNN_NUM_MESSAGE_PASSING_STEPS": L, "micro_batch": learner.micro,
                    "parallelism": f"dp{world} (env shards; RCCL gradient all-reduce per minibatch)"},
-        "roofline": {"bound": "mfma", "kernel": dom["kernel"], "achieved": dom["tflops_fp32_equiv"],
-                     "peak": dom["peak"], "unit": "TFLOP/s (fp32-equivalent)", "frac": dom["frac"], "traffic": None,
-                     "kernel_ms": dom["ms_avg"], "launches": dom["launches"], "peak_basis": dom["peak_basis"],
-                     "note": "dominant matrix kernel of the timed cycle: algorithmic fp32 FLOPs (2*R*3H*(H+Kx) per "
-                             "GRU call, 2*M*N*K per GEMM) / its launches' summed duration (HIP events on the launch "
-                             "stream); rocprofv3 trace of the same leg, timed-cycle slice: profiles/r02_mappo_uf100-430_slice.json"},
+        "roofline": mappo_roofline(dom),
         "kernels": kernels,
         "issued_gemm_tflops_over_cycle": gemm_tflops,
-        "dtype": "f32 (fp32 accumulate; bf16x3 split MFMAs for the dominant products)",
+        "dtype": "f32 (fp32 accumulate; fp16x2 split MFMAs for the dominant products, bf16x3 where fp16's range "
+                 "does not hold)",
         "solve_rate": met["solve_rate"],
         "peak_hbm_gb": torch.cuda.max_memory_allocated() / 1e9,
     }

@@ -755,10 +755,26 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
                                                   0);
 }
 
+// ST = true: the activations go through LDS as well.  Each step's [128 rows][32 k] fp32 tile (16 KiB) is
+// fetched by LDS-DMA three steps ahead into one of three slots ([row][8 chunks of 16 B], chunk c of row
+// r at slot c ^ ((r >> 1) & 5): conflict-free ds_read_b128 for the register-A lane map), and split from
+// LDS in the middle of the step before its use.  With no registers in flight across steps, the step end
+// waits only for the next step's weights and the activations of step s + 2 (vmcnt(2)): the activation
+// fetches get 2.5 steps of lead instead of one.  ST = false: activations loaded to registers by asm one
+// step ahead and drained at every step end (see the note at the wait).  LDS: 96 KiB of weights + 48 KiB.
+// diagnostic ablations of the staged form (timing only, wrong results; never set in the product build):
+// bit 0 no weight DMA after the prologue, 1 no activation DMA after it, 2 no MFMAs, 3 no weight
+// fragment reads (registers reused), 4 no split
+#ifndef MSAT_GRU_ABL
+#define MSAT_GRU_ABL 0
+#endif
+template <bool ST>
 __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
     constexpr int H = 128, IMG = H * 4;  // uint4 per (plane, gate) image: 128 units x 4 chunks = 8 KiB
     constexpr int NI = 6;                // (plane, gate) images per step
     __shared__ uint4 Bs[2 * NI * IMG];  // 96 KiB, double-buffered
+    constexpr int ASL = 128 * 8;         // uint4 per activation slot (16 KiB)
+    __shared__ uint4 As[ST ? 3 * ASL : 1];
     const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int row0 = tile * 128, wr = 16 * w;
@@ -833,19 +849,73 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         f[1] = sp.p[1];
     };
     uint4 fas[2][2];  // split activations of step s in fas[s & 1]
-    aload(0, ras[0]);
-    if (ns > 1) aload(1, ras[1]);
-    issueW(0, 0);
-    await0(ras[0]);
-    await0(ras[1]);
-    asplit(0, ras[0], fas[0]);
-    barrier_lds();
+    // ST: activation DMA, 16 wave-instructions (1 KiB = 8 rows x 8 chunks) per step, 2 per wave;
+    // instruction e of wave w: rows 8 x .. 8 x + 7 (x = 2 w + e), lane -> row 8 x + (lane >> 3), LDS slot
+    // lane & 7 holding chunk (lane & 7) ^ ((row >> 1) & 5).  Rows past R read row R - 1; k past Kx read
+    // a valid address (zeroed at the split).
+    const float *dsrc[2];  // per instruction: this lane's source row base, set per step below
+    int dchunk[2], drow[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int r = 8 * (2 * w + e) + (lane >> 3);
+        drow[e] = r;
+        dchunk[e] = (lane & 7) ^ ((r >> 1) & 5);
+        dsrc[e] = nullptr;
+    }
+    auto issueA = [&](int st) {
+        if constexpr (ST) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int rr = row0 + drow[e], rc = rr < a.R ? rr : a.R - 1;
+                const float *src;
+                if (st < nsh) {
+                    src = hp + (size_t)rc * a.ldp + 32 * st + 4 * dchunk[e];
+                } else {
+                    const int kx = (st - nsh) * 32 + 4 * dchunk[e];
+                    if (kx < w0) src = sg0 + (size_t)rc * a.seg_ld[0] + kx;
+                    else if (kx < w01) src = sg1 + (size_t)rc * a.seg_ld[1] + (kx - w0);
+                    else if (kx < kx_end) src = sg2 + (size_t)rc * a.seg_ld[2] + (kx - w01);
+                    else src = hp + (size_t)rc * a.ldp;  // padding k: any valid row, zeroed at the split
+                }
+                glds16_async(src, &As[(st % 3) * ASL + 64 * (2 * w + e)]);
+            }
+        }
+    };
+    auto lsplit = [&](int st, uint4 (&f)[2]) {  // ST: split step st's activations from its LDS slot
+        const int r = wr + l16, sw = (r >> 1) & 5;
+        const uint4 *row = &As[(st % 3) * ASL + 8 * r];
+        f4v v[2];
+        v[0] = __builtin_bit_cast(f4v, row[(2 * g) ^ sw]);
+        v[1] = __builtin_bit_cast(f4v, row[(2 * g + 1) ^ sw]);
+        asplit(st, v, f);
+    };
+    if constexpr (ST) {
+        issueA(0);
+        if (ns > 1) issueA(1);
+        if (ns > 2) issueA(2);
+        issueW(0, 0);
+        wait_vmcnt<0>();
+        barrier_lds();
+        lsplit(0, fas[0]);
+    } else {
+        aload(0, ras[0]);
+        if (ns > 1) aload(1, ras[1]);
+        issueW(0, 0);
+        await0(ras[0]);
+        await0(ras[1]);
+        asplit(0, ras[0], fas[0]);
+        barrier_lds();
+    }
     auto pstep = [&](int st, auto hidc, auto parc) {
         constexpr bool hid = decltype(hidc)::value;
         constexpr int PB = decltype(parc)::value;  // st & 1
         const int buf = PB;
-        if (st + 1 < ns) issueW(st + 1, buf ^ 1);
-        if (st + 2 < ns) aload(st + 2, ras[PB]);
+        if (!(ST && (MSAT_GRU_ABL & 1)) && st + 1 < ns) issueW(st + 1, buf ^ 1);
+        if constexpr (ST) {
+            if (!(MSAT_GRU_ABL & 2) && st + 3 < ns) issueA(st + 3);
+        } else {
+            if (st + 2 < ns) aload(st + 2, ras[PB]);
+        }
         // weight fragments carried across the 24 (gate, column tile) blocks: each plane is re-read
         // for the next block as soon as its last MFMA here has issued, so the reads fly under the
         // MFMAs instead of each block waiting for its own reads (at 255 VGPRs the compiler had
@@ -862,21 +932,35 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
                 const int gt = n >> 3, j = n & 7;
                 const int G = gt < 2 ? gt : (hid ? 3 : 2);
                 f32x4g c = acc[G][j];
-                c = h2mma(fa[0], b1, c);  // a1 b2
-                if (n + 1 < 24) b1 = bfrag(n + 1, 1);
-                c = h2mma(fa[1], b0, c);  // a2 b1
-                c = h2mma(fa[0], b0, c);  // a1 b1
-                if (n + 1 < 24) b0 = bfrag(n + 1, 0);
+                constexpr bool nomma = ST && (MSAT_GRU_ABL & 4), noread = ST && (MSAT_GRU_ABL & 8);
+                if (!nomma) c = h2mma(fa[0], b1, c);  // a1 b2
+                if (!noread && n + 1 < 24) b1 = bfrag(n + 1, 1);
+                if (!nomma) c = h2mma(fa[1], b0, c);  // a2 b1
+                if (!nomma) c = h2mma(fa[0], b0, c);  // a1 b1
+                if (nomma) c += __builtin_bit_cast(f32x4g, b0 ^ b1);
+                if (!noread && n + 1 < 24) b0 = bfrag(n + 1, 0);
                 acc[G][j] = c;
-                if (n == 7) asplit(st + 1, ras[PB ^ 1], fas[PB ^ 1]);
+                if (n == 7) {
+                    if constexpr (ST) {
+                        if (!(MSAT_GRU_ABL & 16) && st + 1 < ns) lsplit(st + 1, fas[PB ^ 1]);
+                    } else {
+                        asplit(st + 1, ras[PB ^ 1], fas[PB ^ 1]);
+                    }
+                }
                 __builtin_amdgcn_sched_barrier(0);  // keep the blocks in order (the reads lead by one)
             }
         }
-        // Every asm load must complete within the step that issued it: hipcc treats an asm output as
-        // ready at the asm and reuses or moves its registers at the loop back-edge (leaving the step-s+2
-        // activations in flight across it, vmcnt(2) here, faulted: the late data landed in registers the
-        // latch block had reassigned to index arithmetic).
-        await0(ras[PB]);
+        if constexpr (ST) {
+            // W(st + 1) and A(st + 2) landed (A(st + 3), issued last, may fly); no registers in flight
+            if (st + 3 < ns) wait_vmcnt<2>();
+            else wait_vmcnt<0>();
+        } else {
+            // Every asm load must complete within the step that issued it: hipcc treats an asm output as
+            // ready at the asm and reuses or moves its registers at the loop back-edge (leaving the
+            // step-s+2 activations in flight across it, vmcnt(2) here, faulted: the late data landed in
+            // registers the latch block had reassigned to index arithmetic).
+            await0(ras[PB]);
+        }
         barrier_lds();
     };
     {
@@ -995,7 +1079,11 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
 }
 
 __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2r_kernel(GruX3rArgs a) {
-    gru_h2r_tile(a, blockIdx.x);
+    gru_h2r_tile<false>(a, blockIdx.x);
+}
+
+__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2s_kernel(GruX3rArgs a) {
+    gru_h2r_tile<true>(a, blockIdx.x);
 }
 
 // bf16x3 register-A kernel (the template above is fp16x2-only: instantiated for bf16x3 it computed
@@ -1666,8 +1754,14 @@ extern "C" int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w
     a.flags = tile_flags;
     a.wbad = wbad;
     const int tiles = (R + 127) / 128;
-    hipLaunchKernelGGL(gru_ln_fused_fwd_h2r_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
-    rc = check_launch("gru_ln_fused_fwd_h2r_kernel");
+    const char *e = getenv("MARLSAT_GRU_H2S");  // 0: activations to registers (round-1 form), A/B
+    if (e && e[0] == '0') {
+        hipLaunchKernelGGL(gru_ln_fused_fwd_h2r_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
+        rc = check_launch("gru_ln_fused_fwd_h2r_kernel");
+    } else {
+        hipLaunchKernelGGL(gru_ln_fused_fwd_h2s_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
+        rc = check_launch("gru_ln_fused_fwd_h2s_kernel");
+    }
     if (rc) return rc;
     a.wiT = reinterpret_cast<const uint16_t *>(wiT_x3);
     a.whT = reinterpret_cast<const uint16_t *>(whT_x3);

@@ -134,7 +134,9 @@ class GNNActorCritic:
     # {label: [(start event, end event, fp32-equivalent algorithmic FLOPs)]} on the launch stream
     ktimer: Optional[dict] = None
 
-    def _timed(self, label: str, flop: float, call):
+    def _timed(self, label: str, flop: float, call, nbytes: float = 0.0):
+        """Run `call`; under bench.py's ktimer record (start, end, algorithmic fp32 FLOPs, algorithmic HBM
+        bytes: operands read once + results written, no re-reads or workspaces)."""
         kt = GNNActorCritic.ktimer
         if kt is None:
             return call()
@@ -142,13 +144,21 @@ class GNNActorCritic:
         e0.record()
         r = call()
         e1.record()
-        kt.setdefault(label, []).append((e0, e1, float(flop)))
+        kt.setdefault(label, []).append((e0, e1, float(flop), float(nbytes)))
         return r
+
+    @staticmethod
+    def _span(p0: int, p1: int, width: int, ld: int) -> int:
+        """Floats per row read by two row windows [p, p + width) (byte pointers) of one row-major buffer
+        with ld floats per row: their union if they overlap within a row, else both."""
+        lo, hi = min(p0, p1), max(p0, p1) + 4 * width
+        return (hi - lo) // 4 if hi - lo <= 4 * ld else 2 * width
 
     def _gemm(self, A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc=0):
         GNNActorCritic.flops += 2 * M * N * K
         self._timed("msat_gemm (fp32 MFMA)", 2.0 * M * N * K, lambda: _chk(
-            L_.msat_gemm(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, self.stream), "msat_gemm"))
+            L_.msat_gemm(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, self.stream), "msat_gemm"),
+            4.0 * (M * K + N * K + M * N * (1 + acc)))
 
     def _gemm64(self, A, lda, transA, B, ldb, transB, C, ldc, M, N, K, acc=0):
         """fp64-accumulated small product, one rounding per element (the folded weights, gemm.hip)."""
@@ -191,10 +201,11 @@ class GNNActorCritic:
             return
         fl = 2.0 * M * K * (p0[7] + p1[7])
         GNNActorCritic.flops += fl
+        nb = 4.0 * M * (self._span(p0[0], p1[0], K, p0[1]) + p0[7] * (1 + p0[8]) + p1[7] * (1 + p1[8]) + 1)
         self._timed("gemm_h2r16_kernel (dgrad, fp16x2)", fl, lambda: _chk(L_.msat_gemm_h2_dual(
             p0[0], p0[1], p0[2].data_ptr(), p0[3].data_ptr(), p0[4], p0[5], p0[6], p0[7], p0[8],
             p1[0], p1[1], p1[2].data_ptr(), p1[3].data_ptr(), p1[4], p1[5], p1[6], p1[7], p1[8],
-            rexp.data_ptr(), M, K, self.stream), "msat_gemm_h2_dual"))
+            rexp.data_ptr(), M, K, self.stream), "msat_gemm_h2_dual"), nb)
 
     def _wgrad_h2_dual(self, p0, p1, rexp, M, acc=1):
         """p = (A, lda, G, ldg, W, ldw, K, N, rot): both W[:, (n + rot) % N] (+)= (A^T G)[:, n] over the same M
@@ -204,8 +215,9 @@ class GNNActorCritic:
         fl = 2.0 * M * (p0[6] * p0[7] + p1[6] * p1[7])
         GNNActorCritic.flops += fl
         ws = self.scr.get_ws(int(L_.msat_gemm_wgrad_dual_workspace_bytes(M, p0[6], p0[7], p1[6], p1[7])))
+        nb = 4.0 * M * (p0[6] + p1[6] + self._span(p0[2], p1[2], p0[7], p0[3]) + 1)  # A rows, G rows, rexp
         self._timed("wgrad_w_kernel<2> + fixup + reduce (fp16x2)", fl, lambda: _chk(L_.msat_gemm_wgrad_h2_dual(
-            *p0, *p1, rexp.data_ptr(), M, acc, ws.data_ptr(), self.stream), "msat_gemm_wgrad_h2_dual"))
+            *p0, *p1, rexp.data_ptr(), M, acc, ws.data_ptr(), self.stream), "msat_gemm_wgrad_h2_dual"), nb)
 
     def _split_weights_f16(self, mats):
         """fp16x2 planes (2^10 W, msat_split_f16x2_rot) of each block of `mats` (as _split_weights):
@@ -229,14 +241,15 @@ class GNNActorCritic:
             GNNActorCritic.flops += 2 * M * N * K
             self._timed("gemm_h2r16_kernel (dgrad, fp16x2)", 2.0 * M * N * K, lambda: _chk(
                 L_.msat_gemm_h2(A, lda, rexp.data_ptr(), p2.data_ptr(), planes.data_ptr(), wbad, C, ldc, None, M, N,
-                                K, acc, self.stream), "msat_gemm_h2"))
+                                K, acc, self.stream), "msat_gemm_h2"), 4.0 * M * (K + N * (1 + acc) + 1))
             return
         if planes is None:
             self._gemm(A, lda, Wm.data_ptr(), K, 1, C, ldc, None, M, N, K, acc)
             return
         GNNActorCritic.flops += 2 * M * N * K
         self._timed("gemm_x3r16_kernel (dgrad, bf16x3)", 2.0 * M * N * K, lambda: _chk(
-            L_.msat_gemm_x3(A, lda, planes.data_ptr(), C, ldc, None, M, N, K, acc, self.stream), "msat_gemm_x3"))
+            L_.msat_gemm_x3(A, lda, planes.data_ptr(), C, ldc, None, M, N, K, acc, self.stream), "msat_gemm_x3"),
+            4.0 * M * (K + N * (1 + acc)))
 
     def _wgrad(self, A, lda, G, ldg, W, ldw, M, K, N, acc=1, rot=0):
         """W[:, (n + rot) % N] (+)= (A^T G)[:, n] (rot: the packed rows' gate-block rotation)."""
@@ -252,7 +265,7 @@ class GNNActorCritic:
             label = "wgrad_x3_kernel + reduce (bf16x3)"
         self._timed(label, 2.0 * M * N * K, lambda: _chk(
             L_.msat_gemm_wgrad_rot(A, lda, G, ldg, W, ldw, M, K, N, rot, acc, ws.data_ptr(), self.stream),
-            "msat_gemm_wgrad_rot"))
+            "msat_gemm_wgrad_rot"), 4.0 * M * (K + N))
 
     # fp16x2 whole-row weight gradients of the GRU backward's packed rows (gemm_x3.hip wgrad_w_kernel<2>):
     # the backward writes each row's scale exponent, the kernel scales G per row split
@@ -267,7 +280,7 @@ class GNNActorCritic:
         self._timed("wgrad_w_kernel<2> + fixup + reduce (fp16x2)", 2.0 * M * N * K, lambda: _chk(
             L_.msat_gemm_wgrad_h2(A, lda, G, ldg, rexp.data_ptr(), W, ldw, M, K, N, rot, acc, ws.data_ptr(),
                                   self.stream),
-            "msat_gemm_wgrad_h2"))
+            "msat_gemm_wgrad_h2"), 4.0 * M * (K + N + 1))
 
     def _colsum(self, G, ldg, M, N, out, acc=1):
         if M == 0:
@@ -336,7 +349,8 @@ class GNNActorCritic:
         if isinstance(wt, dict) and wt.get("h2"):  # fp16x2 register-A kernel + bf16x3 fixup of flagged tiles
             h2wi, h2wh, wbad = wt["h2"]
             flags = self.scr.get_flags((R + 127) // 128)
-            self._timed("gru_ln_fused_fwd_h2r_kernel (fp16x2, + x3r fixup launch)", 2.0 * R * 3 * H * (H + kx), lambda: _chk(
+            nb = 4.0 * R * (kx + 2 * H + (4 * H if g4 is not None else 0))  # x, h in; h' (+ tape) out
+            self._timed("gru_ln_fused_fwd_h2s_kernel (fp16x2, + x3r fixup launch)", 2.0 * R * 3 * H * (H + kx), lambda: _chk(
                 L_.msat_gru_ln_fused_fwd_h2r(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
                                              h2wi.data_ptr(), h2wh.data_ptr(), wt["wi"][0].data_ptr(),
                                              wt["wh"].data_ptr(), wt["wi"][1], self.p(f"enc.{cell}_bi").data_ptr(),
@@ -344,7 +358,7 @@ class GNNActorCritic:
                                              self._ptr(ln_row, H), out.data_ptr(), H,
                                              g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, flags.data_ptr(),
                                              wbad, self.stream),
-                "msat_gru_ln_fused_fwd_h2r"))
+                "msat_gru_ln_fused_fwd_h2r"), nb)
             return
         if isinstance(wt, dict) and wt.get("x3r"):  # register-A kernel: W^T planes {"wi": (planes, kxp), "wh"}
             self._timed("gru_ln_fused_fwd_x3r_kernel (bf16x3)", 2.0 * R * 3 * H * (H + kx), lambda: _chk(
@@ -354,7 +368,7 @@ class GNNActorCritic:
                                              self.p(f"enc.{cell}_bh").data_ptr(), self._ptr(ln_row),
                                              self._ptr(ln_row, H), out.data_ptr(), H,
                                              g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
-                "msat_gru_ln_fused_fwd_x3r"))
+                "msat_gru_ln_fused_fwd_x3r"), 4.0 * R * (kx + 2 * H + (4 * H if g4 is not None else 0)))
             return
         if isinstance(wt, dict):  # bf16x3 planes {"wi": (planes, kxp), "wh": planes}
             _chk(L_.msat_gru_ln_fused_fwd_x3(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,

@@ -15,6 +15,7 @@ bench = json.loads(line)["mappo"]
 ROCPROF_NAMES = {  # bench label -> rocprof kernel names whose launches the bench's event pair brackets
     "gru_ln_fused_fwd_x3r_kernel (bf16x3)": ["gru_ln_fused_fwd_x3r_kernel"],
     "gru_ln_fused_fwd_h2r_kernel (fp16x2, + x3r fixup launch)": ["gru_ln_fused_fwd_h2r_kernel", "gru_ln_fused_fwd_x3r_kernel"],
+    "gru_ln_fused_fwd_h2s_kernel (fp16x2, + x3r fixup launch)": ["gru_ln_fused_fwd_h2s_kernel", "gru_ln_fused_fwd_x3r_kernel"],
     "gemm_x3r16_kernel (dgrad, bf16x3)": ["gemm_x3r16_kernel"],
     "wgrad_x3_kernel + reduce (bf16x3)": ["wgrad_x3_kernel", "wgrad_reduce4_kernel"],
     "wgrad_w_kernel<3> + reduce (bf16x3)": ["wgrad_w_kernel<3", "wgrad_reduce4_kernel"],
@@ -34,7 +35,8 @@ for k in bench["kernels"]:
     for nm in names:
         rows = sorted(v for key, vals in launches.items() if nm in key for v in vals)
         last = rows[-n:]
-        tot += sum(e - s for s, e in last) / len(last) / 1e6
+        if last:
+            tot += sum(e - s for s, e in last) / len(last) / 1e6
     res["kernels"].append({"kernel": k["kernel"], "launches": n, "bench_event_ms_avg": k["ms_avg"],
                            "rocprof_ms_avg_last_n": tot, "ratio": k["ms_avg"] / tot,
                            "bench_tflops_fp32_equiv": k["tflops_fp32_equiv"], "bench_frac": k["frac"]})
