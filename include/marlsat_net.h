@@ -254,6 +254,21 @@ int msat_ppo_loss(const float *logits, int32_t S, int32_t A, int32_t M, int32_t 
 int msat_adam(float *params, const float *grads, float *m, float *v, size_t n, float lr, float b1, float b2,
               float eps, int32_t count, float grad_scale, void *stream);
 
+/* ---- learner glue (learner:562-592 minibatching, :661-719 metrics) ---- */
+/* out[0..N) = a keyed pseudo-random permutation of [0, N) (4-round Feistel + cycle walking), for the
+ * PPO epoch's minibatch rows (replaces jax.random.permutation, learner:576; deterministic in
+ * (seed, counter)). */
+int msat_permutation(int32_t N, uint64_t seed, uint64_t counter, int32_t *out, void *stream);
+/* dst[f][s] = src[f][idx[s]] for nfields <= 8 fields of row_bytes[f] bytes per row (the micro-batch's
+ * transition rows, learner:597-602); src / dst / row_bytes are host arrays of device pointers. */
+int msat_gather_rows(const int32_t *idx, int32_t S, int32_t nfields, const void *const *src, void *const *dst,
+                     const int32_t *row_bytes, void *stream);
+/* fp64 cycle sums over N transitions (learner:661-719): out[9] = sum reward, sum done, sum solved&done,
+ * sum unsat*done, sum episode_step*(solved&done), sum tg, sum tg^2, sum d, sum d^2 (d = tg - vpred). */
+int msat_cycle_metrics(int32_t N, const float *reward, const uint8_t *done, const uint8_t *solved,
+                       const int32_t *num_unsatisfied, const int32_t *episode_step, const float *targets,
+                       const float *vpred, double *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

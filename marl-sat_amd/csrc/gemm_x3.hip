@@ -579,6 +579,9 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
 // 16x16x32 block instead of six bf16.  If the weight split overflowed (*wbad), the kernel runs the
 // bf16x3 body on the bf16x3 planes instead (same grid and LDS).
 constexpr int kDgW = 10;  // weight scale 2^10: |W| < 32 fits
+#ifndef MSAT_DG_PF
+#define MSAT_DG_PF 2
+#endif
 
 template <int RT, int NP>
 __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int lda, const int *__restrict__ rexp,
@@ -621,8 +624,13 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
     for (int i = 0; i < RT; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
-    float4 ra[RT][2];
-    auto loadA = [&](int d) {
+    // activations two double slabs ahead in two register sets (plain loads: hipcc tracks them and
+    // waits for A(d) just before its split; its count ignores the asm weight DMAs, which only makes
+    // that wait stricter, and W(d) has landed by then anyway)
+    // the bf16x3 body keeps one set (its split needs the registers); MSAT_DG_PF=1: one set for both (A/B)
+    constexpr int PF = (NP == 2 && MSAT_DG_PF == 2) ? 2 : 1;
+    float4 ras[PF][RT][2];
+    auto loadA = [&](int d, float4 (&ra)[RT][2]) {
 #pragma unroll
         for (int i = 0; i < RT; ++i)
 #pragma unroll
@@ -630,11 +638,12 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
     };
     const int slot = g ^ x3swz16((l16 >> 2) & 3);
     const int nd = K / 32;
-    loadA(0);
+    loadA(0, ras[0]);
+    if (PF == 2 && nd > 1) loadA(1, ras[PF - 1]);
     issueW(0, 0);
     wait_vmcnt<0>();
     barrier_lds();
-    for (int d = 0; d < nd; ++d) {
+    auto step = [&](int d, float4 (&ra)[RT][2]) {
         const int buf = d & 1;
         uint4 fa[RT][NP];
 #pragma unroll
@@ -655,7 +664,7 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
         __builtin_amdgcn_sched_barrier(0);
         const bool more = d + 1 < nd;
         if (more) issueW(d + 1, buf ^ 1);
-        if (more) loadA(d + 1);
+        if (d + PF < nd) loadA(d + PF, ra);  // this set was just split
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -689,9 +698,20 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (more) wait_vmcnt<2 * RT>();
+        // W(d + 1) landed; A(d + PF), issued after it, may fly
+        if (d + PF < nd) wait_vmcnt<2 * RT>();
         else wait_vmcnt<0>();
         barrier_lds();
+    };
+    if constexpr (PF == 2) {
+        int d = 0;
+        for (; d + 1 < nd; d += 2) {
+            step(d, ras[0]);
+            step(d + 1, ras[PF - 1]);
+        }
+        if (d < nd) step(d, ras[0]);
+    } else {
+        for (int d = 0; d < nd; ++d) step(d, ras[0]);
     }
     // fp16x2: rescale each output row (C/D map: row 4 (lane >> 4) + reg of the tile) by 2^-(e + kDgW)
     if constexpr (NP == 2) {

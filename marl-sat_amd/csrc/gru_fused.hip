@@ -1148,7 +1148,7 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[G][j] = f32x4g{};
     const int slot = g ^ gswz16((l16 >> 2) & 3);
-    auto step = [&](int s, auto hidc) {
+    [[maybe_unused]] auto step = [&](int s, auto hidc) {  // the MSAT_GRU_X3R_PIPE = 0 form
         constexpr bool hid = decltype(hidc)::value;
         const int buf = s & 1;
         float4 v0 = ra[0], v1 = ra[1];

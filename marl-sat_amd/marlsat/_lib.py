@@ -124,6 +124,9 @@ def _load():
     sig["msat_gemm_x3"] = (I, [P, I, P, P, I, P, I, I, I, I, P])
     sig["msat_split_f16x2_rot"] = (I, [P, I, I, I, I, P, P, P])
     sig["msat_gemm_h2"] = (I, [P, I, P, P, P, P, P, I, P, I, I, I, I, P])
+    sig["msat_permutation"] = (I, [I, U, U, P, P])
+    sig["msat_gather_rows"] = (I, [P, I, I, P, P, P, P])
+    sig["msat_cycle_metrics"] = (I, [I, P, P, P, P, P, P, P, P, P])
     sig["msat_gemm_h2_dual"] = (I, [P, I, P, P, P, P, I, I, I, P, I, P, P, P, P, I, I, I, P, I, I, P])
     sig["msat_gemm_wgrad_dual_workspace_bytes"] = (c_size_t, [I, I, I, I, I])
     sig["msat_gemm_wgrad_h2_dual"] = (I, [P, I, P, I, P, I, I, I, I, P, I, P, I, P, I, I, I, I, P, I, I, P, P])
@@ -207,6 +210,9 @@ EXPORTED = (
     "msat_gemm_x3",
     "msat_split_f16x2_rot",
     "msat_gemm_h2",
+    "msat_permutation",
+    "msat_gather_rows",
+    "msat_cycle_metrics",
     "msat_gemm_h2_dual",
     "msat_gemm_wgrad_dual_workspace_bytes",
     "msat_gemm_wgrad_h2_dual",

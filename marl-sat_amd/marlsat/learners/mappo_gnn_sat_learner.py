@@ -264,21 +264,15 @@ class MAPPOLearner:
         ``idx``; ``sums`` (3,) fp64 accumulates (value, actor, entropy) row sums.  Loss means divide by
         ``mb_size`` (the minibatch size), so micro-batch gradients add up to the minibatch's."""
         c, net, dev = self.cfg, self.net, self.device
-        N = self.T * self.B
-        flat = {k: v.reshape((N,) + tuple(v.shape[2:])) for k, v in self.tr.items()}
-        adv, tgt = self.adv.reshape(N), self.targets.reshape(N)
         A, M = self.A, self.M
+        idx = idx.to(torch.int32)
         net.grads.zero_()
         for m0 in range(0, idx.numel(), self.micro):
             mi = idx[m0:m0 + self.micro]
             S = mi.numel()
-            gb = self._batch(flat["pidx"][mi], flat["x"][mi])
+            pidx, x, act, olp, g_, vold, tg = self.gather_rows(mi)
+            gb = self._batch(pidx, x)
             logits, value, state = net.forward(gb, save=True)
-            act = flat["action"][mi].contiguous()
-            olp = flat["log_prob"][mi].contiguous()
-            g_ = adv[mi].contiguous()
-            vold = flat["value"][mi].contiguous()
-            tg = tgt[mi].contiguous()
             dlog = torch.empty_like(logits)
             dval = torch.empty_like(value)
             rows = torch.empty((2 * S * A + S,), device=dev)
@@ -290,6 +284,29 @@ class MAPPOLearner:
             net.backward(gb, state, dlog, dval)
             del state
 
+    def gather_rows(self, idx: torch.Tensor):
+        """The transition rows ``idx`` (int32, device) of the flat (T*B) buffers, in one launch
+        (msat_gather_rows): (pidx, x, action, log_prob, advantage, value, target)."""
+        S, dev = idx.numel(), self.device
+        srcs = [self.tr["pidx"], self.tr["x"], self.tr["action"], self.tr["log_prob"], self.adv, self.tr["value"],
+                self.targets]
+        outs = [torch.empty((S,) + tuple(t.shape[2:]), dtype=t.dtype, device=dev) for t in srcs]
+        n = len(srcs)
+        src = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
+        dst = (ctypes.c_void_p * n)(*[t.data_ptr() for t in outs])
+        rb = (ctypes.c_int32 * n)(*[t[0, 0].numel() * t.element_size() for t in srcs])
+        _lib.check(L_.msat_gather_rows(idx.data_ptr(), S, n, src, dst, rb, _lib.stream_ptr(dev)), "msat_gather_rows")
+        return outs
+
+    def permutation(self, generator: torch.Generator) -> torch.Tensor:
+        """A pseudo-random permutation of the T*B transition rows (learner:576), keyed from the host
+        generator's stream and drawn on the device (msat_permutation)."""
+        N = self.T * self.B
+        seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator))
+        perm = torch.empty((N,), dtype=torch.int32, device=self.device)
+        _lib.check(L_.msat_permutation(N, seed, 0, perm.data_ptr(), _lib.stream_ptr(self.device)), "msat_permutation")
+        return perm
+
     def ppo_update(self, update_idx: int, generator: torch.Generator):
         c, net, dev = self.cfg, self.net, self.device
         N, MB, E = self.T * self.B, self.MB, int(c["UPDATE_EPOCHS"])
@@ -298,7 +315,7 @@ class MAPPOLearner:
         A, M = self.A, self.M
         n_ent = MB * A * (M if self.mode == 1 else 1)
         for e in range(E):
-            perm = torch.randperm(N, generator=generator, device="cpu").to(dev)
+            perm = self.permutation(generator)
             for k in range(self.n_minibatches):
                 idx = perm[k * MB:(k + 1) * MB]
                 self.minibatch_grad(idx, ent, losses[e, k], MB)
@@ -317,23 +334,20 @@ class MAPPOLearner:
     # ------------------------------------------------------------ metrics ----
     def metrics(self, losses, ent):
         tr, dev = self.tr, self.device
-        done = tr["done"].double()
-        solved = (tr["solved"].bool() & tr["done"].bool()).double()
-        sums = torch.stack([
-            tr["reward"].double().sum(0).sum(), torch.tensor(float(self.B), device=dev, dtype=torch.float64),
-            done.sum(), solved.sum(), (tr["num_unsatisfied"].double() * done).sum(),
-            (tr["episode_step"].double() * solved).sum(),
-        ])
         N = self.T * self.B
-        vpred = self.critic_values(tr["pidx"].reshape(N), tr["x"].reshape(N, -1)).double()
-        tg = self.targets.reshape(N).double()
-        d = tg - vpred
-        ev = torch.stack([tg.sum(), (tg * tg).sum(), d.sum(), (d * d).sum(),
-                          torch.tensor(float(N), device=dev, dtype=torch.float64)])
-        allreduce_sums(sums, self.dist)
-        allreduce_sums(ev, self.dist)
-        s = sums.tolist()
-        t1, t2, d1, d2, n = ev.tolist()
+        vpred = self.critic_values(tr["pidx"].reshape(N), tr["x"].reshape(N, -1))
+        out = torch.empty((11,), dtype=torch.float64, device=dev)
+        # out[0..9) = sums over the transitions (msat_cycle_metrics), then the env and row counts
+        _lib.check(L_.msat_cycle_metrics(N, tr["reward"].data_ptr(), tr["done"].data_ptr(), tr["solved"].data_ptr(),
+                                         tr["num_unsatisfied"].data_ptr(), tr["episode_step"].data_ptr(),
+                                         self.targets.data_ptr(), vpred.data_ptr(), out.data_ptr(),
+                                         _lib.stream_ptr(dev)), "msat_cycle_metrics")
+        out[9] = float(self.B)
+        out[10] = float(N)
+        allreduce_sums(out, self.dist)
+        o = out.tolist()
+        s = [o[0], o[9], o[1], o[2], o[3], o[4]]  # reward, envs, done, solved, unsat*done, steps*solved
+        t1, t2, d1, d2, n = o[5], o[6], o[7], o[8], o[10]
         var_t = t2 / n - (t1 / n) ** 2
         var_d = d2 / n - (d1 / n) ** 2
         lc = losses.cpu().numpy()

@@ -72,7 +72,7 @@ def test_train_cycle_matches_oracle_replay(mode):
     np.testing.assert_allclose(learner.targets.cpu().numpy(), tgt, rtol=1e-5, atol=1e-6)
     adv_n, _, _ = om.normalize(adv)
     np.testing.assert_allclose(learner.adv.cpu().numpy(), adv_n, rtol=1e-4, atol=1e-5)
-    # PPO epochs with the same permutations (same CPU generator stream)
+    # PPO epochs with the same permutations (same host generator stream -> same device permutation keys)
     g2 = torch.Generator().manual_seed(123)
     state = {"count": 0, "m": {k: torch.zeros_like(v) for k, v in P.items()},
              "v": {k: torch.zeros_like(v) for k, v in P.items()}}
@@ -86,7 +86,7 @@ def test_train_cycle_matches_oracle_replay(mode):
     gmax = {k: torch.zeros_like(v) for k, v in P.items()}  # per-element max |grad| over the Adam steps
     lr_sum = 0.0
     for e in range(cfg["UPDATE_EPOCHS"]):
-        perm = torch.randperm(T * B, generator=g2).numpy()
+        perm = learner.permutation(g2).cpu().numpy()  # the learner's device permutation, same key stream
         for k in range((T * B) // cfg["MINIBATCH_SIZE"]):
             idx = perm[k * 8:(k + 1) * 8]
             mb = {kk: vv[idx] for kk, vv in full.items()}
