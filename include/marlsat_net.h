@@ -263,6 +263,11 @@ int msat_permutation(int32_t N, uint64_t seed, uint64_t counter, int32_t *out, v
  * transition rows, learner:597-602); src / dst / row_bytes are host arrays of device pointers. */
 int msat_gather_rows(const int32_t *idx, int32_t S, int32_t nfields, const void *const *src, void *const *dst,
                      const int32_t *row_bytes, void *stream);
+/* Row bases of a graph batch (learner:148-195 batch assembly): per sample s of instance inst[s],
+ * bases[s] = exclusive prefix sums of the instances' (var rows, clause rows, incidences) counts
+ * nv / nc / ne, totals[3] = their sums (the batch's Nv, Nc, nnz). */
+int msat_graph_bases(int32_t S, const int32_t *inst, const int32_t *nv, const int32_t *nc, const int32_t *ne,
+                     int32_t *bases, int32_t *totals, void *stream);
 /* fp64 cycle sums over N transitions (learner:661-719): out[9] = sum reward, sum done, sum solved&done,
  * sum unsat*done, sum episode_step*(solved&done), sum tg, sum tg^2, sum d, sum d^2 (d = tg - vpred). */
 int msat_cycle_metrics(int32_t N, const float *reward, const uint8_t *done, const uint8_t *solved,

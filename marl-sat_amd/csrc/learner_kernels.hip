@@ -1,7 +1,7 @@
-// Learner glue on the device (learner:562-719 around the network calls): the PPO epoch's row
-// permutation, the micro-batch row gather and the cycle metrics.  They replaced torch ops
-// (randperm on the host + copy, index kernels, fp64 reductions) so that nothing on the timed MAPPO
-// path computes outside this library.
+// Learner glue on the device (learner:148-195, 562-719 around the network calls): the PPO epoch's
+// row permutation, the micro-batch row gather, the graph batch's row bases and the cycle metrics.
+// They replaced torch ops (randperm on the host + copy, index kernels, cumsum, fp64 reductions) so
+// that nothing on the timed MAPPO path computes outside this library.
 #include <stdint.h>
 
 #include "common.h"
@@ -118,6 +118,58 @@ __global__ void __launch_bounds__(kMetT) cycle_metrics_kernel(int N, const float
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row bases of a graph batch: for samples s < S of instances inst[s], with per-instance row counts
+// (var rows, clause rows, incidences) nv[i], nc[i], ne[i], bases[s] = exclusive prefix sums (S, 3) and
+// totals[3] = the sums.  One workgroup (the batch is at most a few ten thousand samples): each thread
+// sums a contiguous chunk, the chunk sums are scanned in LDS, then every chunk is re-walked.
+constexpr int kScanT = 1024;
+
+__global__ void __launch_bounds__(kScanT) graph_bases_kernel(int S, const int32_t *__restrict__ inst,
+                                                             const int32_t *__restrict__ nv,
+                                                             const int32_t *__restrict__ nc,
+                                                             const int32_t *__restrict__ ne,
+                                                             int32_t *__restrict__ bases, int32_t *__restrict__ totals) {
+    __shared__ long long sc[3][kScanT];
+    const int t = threadIdx.x, per = (S + kScanT - 1) / kScanT;
+    const int b = min(S, t * per), e = min(S, b + per);
+    long long a[3] = {0, 0, 0};
+    for (int s = b; s < e; ++s) {
+        const int i = inst[s];
+        a[0] += nv[i];
+        a[1] += nc[i];
+        a[2] += ne[i];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) sc[q][t] = a[q];
+    __syncthreads();
+    for (int o = 1; o < kScanT; o <<= 1) {  // Hillis-Steele inclusive scan of the chunk sums
+        long long v[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v[q] = t >= o ? sc[q][t - o] : 0;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 3; ++q) sc[q][t] += v[q];
+        __syncthreads();
+    }
+    long long run[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) run[q] = sc[q][t] - a[q];  // exclusive base of this chunk
+    for (int s = b; s < e; ++s) {
+        const int i = inst[s];
+        bases[3 * s] = (int32_t)run[0];
+        bases[3 * s + 1] = (int32_t)run[1];
+        bases[3 * s + 2] = (int32_t)run[2];
+        run[0] += nv[i];
+        run[1] += nc[i];
+        run[2] += ne[i];
+    }
+    if (t == kScanT - 1) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) totals[q] = (int32_t)min(sc[q][t], (long long)INT32_MAX);
+    }
+}
+
 __host__ inline uint64_t splitmix64(uint64_t &s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -173,4 +225,12 @@ extern "C" int msat_cycle_metrics(int32_t N, const float *reward, const uint8_t 
     hipLaunchKernelGGL(cycle_metrics_kernel, dim3(1), dim3(kMetT), 0, (hipStream_t)stream, N, reward, done, solved,
                        num_unsatisfied, episode_step, targets, vpred, out);
     return check_launch("cycle_metrics_kernel");
+}
+
+extern "C" int msat_graph_bases(int32_t S, const int32_t *inst, const int32_t *nv, const int32_t *nc, const int32_t *ne,
+                                int32_t *bases, int32_t *totals, void *stream) {
+    MSAT_REQUIRE(S >= 0 && totals && (S == 0 || (inst && nv && nc && ne && bases)), "graph_bases: bad args");
+    hipLaunchKernelGGL(graph_bases_kernel, dim3(1), dim3(kScanT), 0, (hipStream_t)stream, S, inst, nv, nc, ne, bases,
+                       totals);
+    return check_launch("graph_bases_kernel");
 }

@@ -127,6 +127,7 @@ def _load():
     sig["msat_permutation"] = (I, [I, U, U, P, P])
     sig["msat_gather_rows"] = (I, [P, I, I, P, P, P, P])
     sig["msat_cycle_metrics"] = (I, [I, P, P, P, P, P, P, P, P, P])
+    sig["msat_graph_bases"] = (I, [I, P, P, P, P, P, P, P])
     sig["msat_gemm_h2_dual"] = (I, [P, I, P, P, P, P, I, I, I, P, I, P, P, P, P, I, I, I, P, I, I, P])
     sig["msat_gemm_wgrad_dual_workspace_bytes"] = (c_size_t, [I, I, I, I, I])
     sig["msat_gemm_wgrad_h2_dual"] = (I, [P, I, P, I, P, I, I, I, I, P, I, P, I, P, I, I, I, I, P, I, I, P, P])
@@ -213,6 +214,7 @@ EXPORTED = (
     "msat_permutation",
     "msat_gather_rows",
     "msat_cycle_metrics",
+    "msat_graph_bases",
     "msat_gemm_h2_dual",
     "msat_gemm_wgrad_dual_workspace_bytes",
     "msat_gemm_wgrad_h2_dual",

@@ -177,14 +177,15 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
     """Instantiate the templates for samples (inst (S,), x (S,V) uint8) on the device."""
     S = int(inst.shape[0])
     G = 1 if critic_only else tpl.G
-    il = inst.long()
-    nvs = (tpl.crit_v if critic_only else tpl.full_v)[il]
-    ncs = (tpl.crit_c if critic_only else tpl.full_c)[il]
-    nes = (tpl.crit_e if critic_only else tpl.full_e)[il]
-    cat0 = lambda t: torch.cat([torch.zeros(1, dtype=torch.int64, device=t.device), torch.cumsum(t.long(), 0)])
-    vb, cb, eb = cat0(nvs), cat0(ncs), cat0(nes)
-    Nv, Nc, nnz = (int(t) for t in torch.stack([vb[-1], cb[-1], eb[-1]]).tolist())
     dev = inst.device
+    inst = inst.to(torch.int32).contiguous()
+    # per-sample row bases (exclusive scans of the instances' row counts) and the batch totals
+    sb = torch.empty((max(S, 1), 3), dtype=torch.int32, device=dev)
+    tot = torch.empty((3,), dtype=torch.int32, device=dev)
+    tv, tc, te = (tpl.crit_v, tpl.crit_c, tpl.crit_e) if critic_only else (tpl.full_v, tpl.full_c, tpl.full_e)
+    _lib.check(_lib.lib.msat_graph_bases(S, inst.data_ptr(), tv.data_ptr(), tc.data_ptr(), te.data_ptr(), sb.data_ptr(),
+                                         tot.data_ptr(), _lib.stream_ptr(dev)), "msat_graph_bases")
+    Nv, Nc, nnz = tot.tolist()  # sizes the outputs (one small device -> host read)
     out = GraphBatch(S, G, Nv, Nc, nnz,
                      torch.empty((Nv, 8), dtype=torch.float32, device=dev),
                      torch.empty((Nc, 3), dtype=torch.float32, device=dev),
@@ -198,7 +199,6 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
                      torch.empty((S * G,), dtype=torch.int32, device=dev))
     V = x.shape[1]
     C = pool_packed.shape[1]
-    sb = torch.stack([vb[:-1], cb[:-1], eb[:-1]], 1).to(torch.int32).contiguous()  # (S, 3)
     _lib.check(_lib.lib.msat_assemble_graph_batch(
         S, G, tpl.A, V, C, inst.data_ptr(), x.data_ptr(), svf.data_ptr(), pool_packed.data_ptr(), sb.data_ptr(),
         tpl.vgid.data_ptr(), tpl.cgid.data_ptr(), tpl.slots.data_ptr(), tpl.ptr.data_ptr(), tpl.inc.data_ptr(),

@@ -85,3 +85,23 @@ def test_cycle_metrics_match_numpy():
     ref = [reward.astype(np.float64).sum(), dn.sum(), sv.sum(), (unsat * dn).sum(), (steps * sv).sum(), t.sum(),
            (t * t).sum(), d.sum(), (d * d).sum()]
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("S", [0, 1, 5, 1023, 1024, 1025, 32768, 40001])
+def test_graph_bases_match_cumsum(S):
+    from marlsat import _lib
+
+    rng = np.random.default_rng(S)
+    n_inst = 37
+    counts = [rng.integers(0, 3000, n_inst).astype(np.int32) for _ in range(3)]
+    inst = rng.integers(0, n_inst, S).astype(np.int32)
+    dc = [torch.from_numpy(c).cuda() for c in counts]
+    di = torch.from_numpy(inst).cuda()
+    bases = torch.empty((max(S, 1), 3), dtype=torch.int32, device="cuda")
+    tot = torch.empty(3, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.msat_graph_bases(S, di.data_ptr(), *[c.data_ptr() for c in dc], bases.data_ptr(),
+                                         tot.data_ptr(), _lib.stream_ptr()), "graph_bases")
+    per = np.stack([c[inst] for c in counts], 1).astype(np.int64)
+    ref = np.cumsum(per, 0) - per
+    assert np.array_equal(bases.cpu().numpy()[:S], ref)
+    assert np.array_equal(tot.cpu().numpy(), per.sum(0))
