@@ -131,6 +131,18 @@ def load_pmc_traffic(workload: str):
     return None, None
 
 
+def load_gru_pmc_ratio():
+    """PMC HBM bytes / algorithmic bytes of the GRU forward (profiles/r02_pmc_gru.json: FETCH_SIZE x 2 +
+    WRITE_SIZE per launch on the clause and var training shapes, profiles/pmc_gru_traffic.sh)."""
+    f = os.path.join(ROOT, "profiles", "r02_pmc_gru.json")
+    try:
+        d = json.load(open(f))
+        r = [v["pmc_over_algorithmic"] for v in d.values()]
+        return sum(r) / len(r), os.path.basename(f)
+    except Exception:
+        return None, None
+
+
 # ------------------------------------------------------------------ MAPPO ----
 def mappo_cpu_baseline(workload: str, budget_s: float = 10.0, batch: int = 8):
     """PPO minibatch forward + backward of the reference network restated in torch (oracle/net.py:
@@ -223,10 +235,15 @@ def mappo_roofline(dom: dict) -> dict:
     HBM-bound: achieved = algorithmic GB/s vs 8 TB/s; MFMA-bound: fp32-equivalent TF/s vs the ceiling.
     Both views are carried either way."""
     hbm = dom.get("bound") == "hbm"
+    ratio, src = load_gru_pmc_ratio() if "gru_ln_fused_fwd_h2s" in dom["kernel"] else (None, None)
+    alg = dom.get("algorithmic_bytes_avg")
     r = {"bound": "hbm" if hbm else "mfma", "kernel": dom["kernel"],
          "achieved": dom["hbm_GBps"] if hbm else dom["tflops_fp32_equiv"],
          "peak": HBM_PEAK_GBS if hbm else dom["peak"], "unit": "GB/s" if hbm else "TFLOP/s (fp32-equivalent)",
-         "frac": dom["hbm_frac"] if hbm else dom["frac"], "traffic": None,
+         "frac": dom["hbm_frac"] if hbm else dom["frac"],
+         "traffic": ratio * alg if ratio and alg else None,
+         "traffic_source": (f"{src}: PMC bytes = {ratio:.3f} x algorithmic on the clause / var training shapes"
+                            if ratio else None),
          "kernel_ms": dom["ms_avg"], "launches": dom["launches"],
          "algorithmic_bytes_per_launch": dom.get("algorithmic_bytes_avg"),
          "mfma": {"achieved_tflops_fp32_equiv": dom["tflops_fp32_equiv"], "peak": dom["peak"], "frac": dom["frac"],
