@@ -253,6 +253,12 @@ int msat_ppo_loss(const float *logits, int32_t S, int32_t A, int32_t M, int32_t 
                   float *dlogits, float *dvalue, float *row_terms, double *loss_sums, void *stream);
 int msat_adam(float *params, const float *grads, float *m, float *v, size_t n, float lr, float b1, float b2,
               float eps, int32_t count, float grad_scale, void *stream);
+/* Collectives: no msat_comm_init / msat_allreduce (SURVEY.md 8(b) sketched them).  The gradient is ONE
+ * flat fp32 buffer (the grads of every parameter, 16-B aligned tensors), so the host all-reduces it with
+ * RCCL in place (sum; marlsat/learners/collectives.py uses torch.distributed, whose "nccl" backend is
+ * RCCL on ROCm) and passes grad_scale = 1 / world to msat_adam (learner:647-650).  A host binding in
+ * another language calls ncclAllReduce on the same buffer and stream; nothing in this library keeps a
+ * communicator. */
 
 /* ---- learner glue (learner:562-592 minibatching, :661-719 metrics) ---- */
 /* out[0..N) = a keyed pseudo-random permutation of [0, N) (4-round Feistel + cycle walking), for the
