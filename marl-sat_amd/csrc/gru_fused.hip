@@ -764,7 +764,7 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 // step ahead and drained at every step end (see the note at the wait).  LDS: 96 KiB of weights + 48 KiB.
 // diagnostic ablations of the staged form (timing only, wrong results; never set in the product build):
 // bit 0 no weight DMA after the prologue, 1 no activation DMA after it, 2 no MFMAs, 3 no weight
-// fragment reads (registers reused), 4 no split
+// fragment reads (registers reused), 4 no split, 5 no step-end barrier, 6 no step-end vmcnt wait
 #ifndef MSAT_GRU_ABL
 #define MSAT_GRU_ABL 0
 #endif
@@ -952,8 +952,10 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         }
         if constexpr (ST) {
             // W(st + 1) and A(st + 2) landed (A(st + 3), issued last, may fly); no registers in flight
-            if (st + 3 < ns) wait_vmcnt<2>();
-            else wait_vmcnt<0>();
+            if (!(MSAT_GRU_ABL & 64)) {
+                if (st + 3 < ns) wait_vmcnt<2>();
+                else wait_vmcnt<0>();
+            }
         } else {
             // Every asm load must complete within the step that issued it: hipcc treats an asm output as
             // ready at the asm and reuses or moves its registers at the loop back-edge (leaving the
@@ -961,7 +963,7 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
             // registers the latch block had reassigned to index arithmetic).
             await0(ras[PB]);
         }
-        barrier_lds();
+        if (!(ST && (MSAT_GRU_ABL & 32))) barrier_lds();
     };
     {
         int st = 0;
