@@ -768,18 +768,26 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 #ifndef MSAT_GRU_ABL
 #define MSAT_GRU_ABL 0
 #endif
-template <bool ST>
+// NW waves (16 rows each) per workgroup, WB weight buffers.  <ST, 8, 2>: 128-row tiles, one workgroup
+// per CU (147 KiB of LDS).  <true, 4, 1> ("ping-pong"): 64-row tiles, weights single-buffered, 72 KiB,
+// two workgroups per CU, so one's DMA waits, barriers and epilogue run beside the other's MFMAs; its
+// range flags go to the 128-row tile the x3r fixup launch indexes (pre-zeroed, written only on overflow).
+template <bool ST, int NW = 8, int WB = 2>
 __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
     constexpr int H = 128, IMG = H * 4;  // uint4 per (plane, gate) image: 128 units x 4 chunks = 8 KiB
     constexpr int NI = 6;                // (plane, gate) images per step
-    __shared__ uint4 Bs[2 * NI * IMG];  // 96 KiB, double-buffered
-    constexpr int ASL = 128 * 8;         // uint4 per activation slot (16 KiB)
+    constexpr int NIW = 8 * NI / NW;     // weight DMA instructions per wave and step
+    constexpr int TR = 16 * NW;          // tile rows
+    static_assert(WB == 2 || ST, "single-buffered weights need the LDS-staged activations");
+    __shared__ uint4 Bs[WB * NI * IMG];  // 48 KiB per buffer
+    constexpr int ASL = TR * 8;          // uint4 per activation slot (128 B per row)
     __shared__ uint4 As[ST ? 3 * ASL : 1];
     const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int row0 = tile * 128, wr = 16 * w;
+    const int row0 = tile * TR, wr = 16 * w;
+    int *const flag = a.flags + (NW == 8 ? tile : tile >> 1);
     if (a.wbad[0] | a.wbad[1]) {  // weights out of fp16 range: the bf16x3 launch does every tile
-        if (t == 0) a.flags[tile] = 1;
+        if (t == 0) *flag = 1;
         return;
     }
     const int arow = row0 + wr + l16, arc = arow < a.R ? arow : a.R - 1;
@@ -802,8 +810,8 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         const int k0 = hid ? 32 * s : 32 * (s - nsh);
         const unsigned voff = lpart * (unsigned)Kp + chb;
 #pragma unroll
-        for (int e = 0; e < NI; ++e) {
-            const int x = NI * w + e, img = x >> 3, p = x & 7, q = img / 3, gt = img - 3 * q;
+        for (int e = 0; e < NIW; ++e) {
+            const int x = NIW * w + e, img = x >> 3, p = x & 7, q = img / 3, gt = img - 3 * q;
             const uint16_t *base = W + ((size_t)q * 3 * H + gt * H + 16 * p) * Kp + k0;
             glds16_async_s(base, voff, &Bs[(buf * NI + img) * IMG + 64 * p]);
         }
@@ -909,10 +917,10 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
     auto pstep = [&](int st, auto hidc, auto parc) {
         constexpr bool hid = decltype(hidc)::value;
         constexpr int PB = decltype(parc)::value;  // st & 1
-        const int buf = PB;
-        if (!(ST && (MSAT_GRU_ABL & 1)) && st + 1 < ns) issueW(st + 1, buf ^ 1);
+        const int buf = WB == 2 ? PB : 0;
+        if (WB == 2 && !(ST && (MSAT_GRU_ABL & 1)) && st + 1 < ns) issueW(st + 1, buf ^ 1);
         if constexpr (ST) {
-            if (!(MSAT_GRU_ABL & 2) && st + 3 < ns) issueA(st + 3);
+            if (WB == 2 && !(MSAT_GRU_ABL & 2) && st + 3 < ns) issueA(st + 3);
         } else {
             if (st + 2 < ns) aload(st + 2, ras[PB]);
         }
@@ -950,6 +958,12 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
                 __builtin_amdgcn_sched_barrier(0);  // keep the blocks in order (the reads lead by one)
             }
         }
+        if constexpr (ST && WB == 1) {
+            // single weight buffer: every wave is done with W(st) before W(st + 1) overwrites it
+            barrier_lds();
+            if (st + 1 < ns) issueW(st + 1, 0);
+            if (st + 3 < ns) issueA(st + 3);
+        }
         if constexpr (ST) {
             // W(st + 1) and A(st + 2) landed (A(st + 3), issued last, may fly); no registers in flight
             if (!(MSAT_GRU_ABL & 64)) {
@@ -982,7 +996,7 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
     }
     {  // range check: |a| < 2^15 keeps a1 = fp16(a) finite with margin
         const int bad = __syncthreads_or(!(amax < 32768.0f));
-        if (t == 0) a.flags[tile] = bad;
+        if (t == 0 && (NW == 8 || bad)) *flag = bad;
         if (bad) return;
     }
 
@@ -1086,6 +1100,10 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2r_kernel(GruX3rArgs
 
 __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2s_kernel(GruX3rArgs a) {
     gru_h2r_tile<true>(a, blockIdx.x);
+}
+
+__global__ void __launch_bounds__(256, 2) gru_ln_fused_fwd_h2p_kernel(GruX3rArgs a) {
+    gru_h2r_tile<true, 4, 1>(a, blockIdx.x);
 }
 
 // bf16x3 register-A kernel (the template above is fp16x2-only: instantiated for bf16x3 it computed
@@ -1757,7 +1775,13 @@ extern "C" int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w
     a.wbad = wbad;
     const int tiles = (R + 127) / 128;
     const char *e = getenv("MARLSAT_GRU_H2S");  // 0: activations to registers (round-1 form), A/B
-    if (e && e[0] == '0') {
+    const char *pp = getenv("MARLSAT_GRU_H2P");  // 1: 64-row ping-pong tiles (two workgroups per CU)
+    if (pp && pp[0] == '1') {
+        if (hipMemsetAsync(tile_flags, 0, sizeof(int32_t) * tiles, (hipStream_t)stream) != hipSuccess)
+            return check_launch("gru h2p flags memset");
+        hipLaunchKernelGGL(gru_ln_fused_fwd_h2p_kernel, dim3((R + 63) / 64), dim3(256), 0, (hipStream_t)stream, a);
+        rc = check_launch("gru_ln_fused_fwd_h2p_kernel");
+    } else if (e && e[0] == '0') {
         hipLaunchKernelGGL(gru_ln_fused_fwd_h2r_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
         rc = check_launch("gru_ln_fused_fwd_h2r_kernel");
     } else {
