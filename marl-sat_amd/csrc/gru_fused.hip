@@ -772,6 +772,9 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 // per CU (147 KiB of LDS).  <true, 4, 1> ("ping-pong"): 64-row tiles, weights single-buffered, 72 KiB,
 // two workgroups per CU, so one's DMA waits, barriers and epilogue run beside the other's MFMAs; its
 // range flags go to the 128-row tile the x3r fixup launch indexes (pre-zeroed, written only on overflow).
+#ifndef MSAT_GRU_LA2
+#define MSAT_GRU_LA2 1
+#endif
 template <bool ST, int NW = 8, int WB = 2>
 __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
     constexpr int H = 128, IMG = H * 4;  // uint4 per (plane, gate) image: 128 units x 4 chunks = 8 KiB
@@ -934,19 +937,30 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         };
         uint4 (&fa)[2] = fas[PB];
         {
-            uint4 b0 = bfrag(0, 0), b1 = bfrag(0, 1);
+            // ST: fragments two blocks ahead in two alternating register sets (block n uses set n & 1;
+            // each plane's register is refilled for block n + 2 right after its last MFMA in block n);
+            // otherwise one block ahead in one set
+            constexpr int LA = (ST && MSAT_GRU_LA2) ? 2 : 1;
+            uint4 bb[LA][2];
+            bb[0][0] = bfrag(0, 0);
+            bb[0][1] = bfrag(0, 1);
+            if (LA == 2) {
+                bb[LA - 1][0] = bfrag(1, 0);
+                bb[LA - 1][1] = bfrag(1, 1);
+            }
 #pragma unroll
             for (int n = 0; n < 24; ++n) {
                 const int gt = n >> 3, j = n & 7;
                 const int G = gt < 2 ? gt : (hid ? 3 : 2);
+                uint4 &b0 = bb[n % LA][0], &b1 = bb[n % LA][1];
                 f32x4g c = acc[G][j];
                 constexpr bool nomma = ST && (MSAT_GRU_ABL & 4), noread = ST && (MSAT_GRU_ABL & 8);
                 if (!nomma) c = h2mma(fa[0], b1, c);  // a1 b2
-                if (!noread && n + 1 < 24) b1 = bfrag(n + 1, 1);
+                if (!noread && n + LA < 24) b1 = bfrag(n + LA, 1);
                 if (!nomma) c = h2mma(fa[1], b0, c);  // a2 b1
                 if (!nomma) c = h2mma(fa[0], b0, c);  // a1 b1
                 if (nomma) c += __builtin_bit_cast(f32x4g, b0 ^ b1);
-                if (!noread && n + 1 < 24) b0 = bfrag(n + 1, 0);
+                if (!noread && n + LA < 24) b0 = bfrag(n + LA, 0);
                 acc[G][j] = c;
                 if (n == 7) {
                     if constexpr (ST) {
