@@ -1010,6 +1010,9 @@ wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ 
 #ifndef MSAT_WW_ABL
 #define MSAT_WW_ABL 0
 #endif
+#ifndef MSAT_WW_PF
+#define MSAT_WW_PF 2  // raw slab sets of the fp16x2 form (2, 3 or 4: measured equal or slower)
+#endif
 constexpr int kWWT = 512;
 constexpr int kWWN = 384;  // widest N
 
@@ -1142,15 +1145,21 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
             }
     };
     if (ns > 0) {
-        Stage R0, R1;
-        load(0, R0);
-        load(1 < ns ? 1 : 0, R1);
-        store(0, R0, 0);
+        // NPF register sets of raw slabs: at iteration s they hold slabs s + 1 .. s + NPF - 1 (in flight or
+        // landed) and the set of slab s (stored at the end of iteration s - 1) receives slab s + NPF.
+        // fp16x2: MSAT_WW_PF sets (three or four, 96-128 KiB in flight per CU, measured 1 % slower than
+        // two: the kernel is not latency-bound on its loads); bf16x3 keeps two (its split needs the
+        // registers).
+        constexpr int NPF = NP == 2 ? MSAT_WW_PF : 2;
+        Stage R[NPF];
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) load(k < ns ? k : ns - 1, R[k]);
+        store(0, R[0], 0);
         __syncthreads();
-        // Rn holds slab s + 1, Rf receives slab s + 2 (past the end: a repeated, never stored load)
+        // Rn holds slab s + 1, Rf receives slab s + NPF (past the end: a repeated, never stored load)
         auto iter = [&](int s, const Stage &Rn, Stage &Rf) {
             const int buf = s & 1;
-            if (!(MSAT_WW_ABL & 1)) load(s + 2 < ns ? s + 2 : ns - 1, Rf);
+            if (!(MSAT_WW_ABL & 1)) load(s + NPF < ns ? s + NPF : ns - 1, Rf);
             __builtin_amdgcn_sched_barrier(0);
             if (!(MSAT_WW_ABL & 2)) slab(buf);
             if constexpr (IL) {
@@ -1170,11 +1179,13 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
             __syncthreads();
         };
         int s = 0;
-        for (; s + 1 < ns; s += 2) {
-            iter(s, R1, R0);
-            iter(s + 1, R0, R1);
+        for (; s + NPF - 1 < ns; s += NPF) {
+#pragma unroll
+            for (int k = 0; k < NPF; ++k) iter(s + k, R[(k + 1) % NPF], R[k]);
         }
-        if (s < ns) iter(s, R1, R0);
+#pragma unroll
+        for (int k = 0; k < NPF - 1; ++k)
+            if (s + k < ns) iter(s + k, R[(k + 1) % NPF], R[k]);
     }
     if constexpr (NP == 2) {
         const int bad = __syncthreads_or(!(amax < 32768.0f));
