@@ -764,7 +764,8 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 // step ahead and drained at every step end (see the note at the wait).  LDS: 96 KiB of weights + 48 KiB.
 // diagnostic ablations of the staged form (timing only, wrong results; never set in the product build):
 // bit 0 no weight DMA after the prologue, 1 no activation DMA after it, 2 no MFMAs, 3 no weight
-// fragment reads (registers reused), 4 no split, 5 no step-end barrier, 6 no step-end vmcnt wait
+// fragment reads (registers reused), 4 no split, 5 no step-end barrier, 6 no step-end vmcnt wait,
+// 7 no epilogue, 8 one k step (prologue and epilogue alone)
 #ifndef MSAT_GRU_ABL
 #define MSAT_GRU_ABL 0
 #endif
@@ -774,6 +775,21 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 // range flags go to the 128-row tile the x3r fixup launch indexes (pre-zeroed, written only on overflow).
 #ifndef MSAT_GRU_LA2
 #define MSAT_GRU_LA2 1
+#endif
+#ifndef MSAT_GRU_STG
+#define MSAT_GRU_STG 2
+#endif
+#ifndef MSAT_GRU_DMA0
+#define MSAT_GRU_DMA0 -1
+#endif
+#ifndef MSAT_GRU_DMA1
+#define MSAT_GRU_DMA1 8
+#endif
+#ifndef MSAT_GRU_SPLH
+#define MSAT_GRU_SPLH 0
+#endif
+#ifndef MSAT_GRU_HVE
+#define MSAT_GRU_HVE 1
 #endif
 template <bool ST, int NW = 8, int WB = 2>
 __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
@@ -795,7 +811,8 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
     }
     const int arow = row0 + wr + l16, arc = arow < a.R ? arow : a.R - 1;
     constexpr int nsh = H / 32;
-    const int ns = nsh + a.kxp / 32;
+    // ablation bit 8: one step instead of ns (prologue + epilogue cost)
+    const int ns = (ST && (MSAT_GRU_ABL & 256)) ? 1 : nsh + a.kxp / 32;
     const float *const hp = a.hp, *const sg0 = a.seg[0], *const sg1 = a.seg[1], *const sg2 = a.seg[2];
     const int w0 = a.seg_w[0], w01 = a.seg_w[0] + a.seg_w[1], kx_end = a.Kx;
     const unsigned ro0 = (unsigned)arc * (unsigned)a.seg_ld[0], ro1 = (unsigned)arc * (unsigned)a.seg_ld[1],
@@ -900,6 +917,33 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         v[1] = __builtin_bit_cast(f4v, row[(2 * g + 1) ^ sw]);
         asplit(st, v, f);
     };
+    // half of lsplit: float4 e of the lane's 8 k, into dwords 2e, 2e + 1 of both planes (SPLH: the two
+    // halves run in different blocks of the step, so each VALU burst between MFMAs is half as long)
+    auto lsplit_h = [&](int st, uint4 (&f)[2], auto ec) {
+        constexpr int e = decltype(ec)::value;
+        const int r = wr + l16, sw = (r >> 1) & 5;
+        const uint4 *row = &As[(st % 3) * ASL + 8 * r];
+        const f4v zero = {0.f, 0.f, 0.f, 0.f};
+        const f4v raw = __builtin_bit_cast(f4v, row[(2 * g + e) ^ sw]);
+        const bool z = st >= nsh && (st - nsh) * 32 + 8 * g + 4 * e >= kx_end;
+        const float4 v = __builtin_bit_cast(float4, z ? zero : raw);
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        const float x[4] = {v.x, v.y, v.z, v.w};
+        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+        f16x4 h, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const _Float16 q = (_Float16)x[j];
+            h[j] = q;
+            l[j] = (_Float16)(x[j] - (float)q);
+        }
+        const uint2 hb = __builtin_bit_cast(uint2, h), lb = __builtin_bit_cast(uint2, l);
+        if constexpr (e == 0) {
+            f[0].x = hb.x, f[0].y = hb.y, f[1].x = lb.x, f[1].y = lb.y;
+        } else {
+            f[0].z = hb.x, f[0].w = hb.y, f[1].z = lb.x, f[1].w = lb.y;
+        }
+    };
     if constexpr (ST) {
         issueA(0);
         if (ns > 1) issueA(1);
@@ -917,14 +961,48 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         asplit(0, ras[0], fas[0]);
         barrier_lds();
     }
+    // HVE: the h values of the epilogue (h of each accumulator's (row, unit)) are fetched by LDS-DMA at
+    // the start of the last step, so their HBM latency runs under its MFMAs instead of at the epilogue
+    // (the rows' h passed through the activation slots in steps 0..3 and are long evicted).  In the last
+    // step the three activation slots and the other weight buffer are free: waves 0..5 put their 16 rows
+    // (8 KiB, [row][128]) in the slots, waves 6 and 7 in that buffer.
+    constexpr bool HVE = MSAT_GRU_HVE && ST && WB == 2 && NW == 8;
+    auto hbase = [&](int fb) -> float * {
+        return w < 6 ? reinterpret_cast<float *>(&As[512 * w]) : reinterpret_cast<float *>(&Bs[fb * NI * IMG + 512 * (w - 6)]);
+    };
+    auto issueH = [&](int fb, int z) {  // z = 0, passed from the step so nothing is hoisted into the loop
+        const uint4 *dst = reinterpret_cast<const uint4 *>(hbase(fb));
+        const float *sb = hp + (size_t)row0 * a.ldp;  // wave-uniform base, per-lane 32-bit offsets
+        const int rmax = a.R - 1 - row0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {  // rows wr + 2 e + (lane >> 5), float4 (lane & 31)
+            const int rr = wr + 2 * e + (lane >> 5) + z, rc = rr < rmax ? rr : rmax;
+            glds16_async_s(sb, 4u * ((unsigned)rc * (unsigned)a.ldp + 4u * (unsigned)(lane & 31)), dst + 64 * e);
+        }
+    };
     auto pstep = [&](int st, auto hidc, auto parc) {
         constexpr bool hid = decltype(hidc)::value;
         constexpr int PB = decltype(parc)::value;  // st & 1
         const int buf = WB == 2 ? PB : 0;
-        if (WB == 2 && !(ST && (MSAT_GRU_ABL & 1)) && st + 1 < ns) issueW(st + 1, buf ^ 1);
-        if constexpr (ST) {
-            if (WB == 2 && !(MSAT_GRU_ABL & 2) && st + 3 < ns) issueA(st + 3);
-        } else {
+        if (HVE && st + 1 == ns) issueH(buf ^ 1, ns - 1 - st);
+        // STG (stagger of SIMD partners: waves w and w + 4 share a SIMD): bit 0 moves waves 4..7's split
+        // to block 19, bit 1 (default) their DMA issue to before block MSAT_GRU_DMA1 = 8, so partners'
+        // DMA bursts do not coincide.  Measured (profiles/ab_gru_dma.sh, tape on): DMA at block 8 -2.9 %
+        // clause / -1.1 % var; blocks 4, 6, 10, 12, 16 -1..-2.5 %; delaying waves 0..3 too (4 / 16,
+        // 6 / 18) +2 %; the split stagger 0 .. +0.5 %.
+        constexpr bool stg_split = ST && WB == 2 && NW == 8 && (MSAT_GRU_STG & 1);
+        constexpr bool stg_dma = ST && WB == 2 && NW == 8;
+        // the block before which waves 0..3 / 4..7 issue the step's DMA (-1: at the step start)
+        constexpr int dma_n0 = MSAT_GRU_DMA0, dma_n1 = (MSAT_GRU_STG & 2) ? MSAT_GRU_DMA1 : MSAT_GRU_DMA0;
+        const bool late = w >= 4;
+        auto dma = [&]() {
+            if (WB == 2 && !(ST && (MSAT_GRU_ABL & 1)) && st + 1 < ns) issueW(st + 1, buf ^ 1);
+            if constexpr (ST) {
+                if (WB == 2 && !(MSAT_GRU_ABL & 2) && st + 3 < ns) issueA(st + 3);
+            }
+        };
+        if (!stg_dma || (late ? dma_n1 : dma_n0) < 0) dma();
+        if constexpr (!ST) {
             if (st + 2 < ns) aload(st + 2, ras[PB]);
         }
         // weight fragments carried across the 24 (gate, column tile) blocks: each plane is re-read
@@ -937,16 +1015,15 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         };
         uint4 (&fa)[2] = fas[PB];
         {
-            // ST: fragments two blocks ahead in two alternating register sets (block n uses set n & 1;
-            // each plane's register is refilled for block n + 2 right after its last MFMA in block n);
-            // otherwise one block ahead in one set
-            constexpr int LA = (ST && MSAT_GRU_LA2) ? 2 : 1;
+            // ST: fragments LA = MSAT_GRU_LA2 + 1 blocks ahead in LA rotating register sets (block n uses
+            // set n % LA; each plane's register is refilled for block n + LA right after its last MFMA in
+            // block n); otherwise one block ahead in one set
+            constexpr int LA = (ST && MSAT_GRU_LA2) ? MSAT_GRU_LA2 + 1 : 1;
             uint4 bb[LA][2];
-            bb[0][0] = bfrag(0, 0);
-            bb[0][1] = bfrag(0, 1);
-            if (LA == 2) {
-                bb[LA - 1][0] = bfrag(1, 0);
-                bb[LA - 1][1] = bfrag(1, 1);
+#pragma unroll
+            for (int q = 0; q < LA; ++q) {  // blocks 0 .. LA - 1
+                bb[q][0] = bfrag(q, 0);
+                bb[q][1] = bfrag(q, 1);
             }
 #pragma unroll
             for (int n = 0; n < 24; ++n) {
@@ -962,13 +1039,18 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
                 if (nomma) c += __builtin_bit_cast(f32x4g, b0 ^ b1);
                 if (!noread && n + LA < 24) b0 = bfrag(n + LA, 0);
                 acc[G][j] = c;
-                if (n == 7) {
-                    if constexpr (ST) {
-                        if (!(MSAT_GRU_ABL & 16) && st + 1 < ns) lsplit(st + 1, fas[PB ^ 1]);
-                    } else {
-                        asplit(st + 1, ras[PB ^ 1], fas[PB ^ 1]);
+                if (ST && MSAT_GRU_SPLH && (n == 7 || n == 15)) {
+                    if (!(MSAT_GRU_ABL & 16) && st + 1 < ns) {
+                        if (n == 7) lsplit_h(st + 1, fas[PB ^ 1], std::integral_constant<int, 0>{});
+                        else lsplit_h(st + 1, fas[PB ^ 1], std::integral_constant<int, 1>{});
                     }
+                } else if constexpr (ST) {
+                    if ((n == 7 && !(stg_split && late)) || (stg_split && n == 19 && late))
+                        if (!(MSAT_GRU_ABL & 16) && st + 1 < ns) lsplit(st + 1, fas[PB ^ 1]);
+                } else if (n == 7) {
+                    asplit(st + 1, ras[PB ^ 1], fas[PB ^ 1]);
                 }
+                if (stg_dma && n + 1 < 24 && n + 1 == (late ? dma_n1 : dma_n0)) dma();
                 __builtin_amdgcn_sched_barrier(0);  // keep the blocks in order (the reads lead by one)
             }
         }
@@ -1008,25 +1090,55 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         }
         if (st < ns) pstep(st, std::false_type{}, std::integral_constant<int, 0>{});
     }
-    {  // range check: |a| < 2^15 keeps a1 = fp16(a) finite with margin
-        const int bad = __syncthreads_or(!(amax < 32768.0f));
+    {  // range check: |a| < 2^15 keeps a1 = fp16(a) finite with margin.  A ballot per wave and an
+       // LDS-only barrier: __syncthreads_or's fence would also wait for the h DMA in flight.
+        __shared__ int wbadl[NW];
+        const bool wb = __ballot(!(amax < 32768.0f)) != 0;
+        if (lane == 0) wbadl[w] = wb;
+        barrier_lds();
+        int bad = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) bad |= wbadl[q];
         if (t == 0 && (NW == 8 || bad)) *flag = bad;
-        if (bad) return;
+        if (bad) {
+            wait_vmcnt<0>();  // no LDS-DMA may land after the workgroup's LDS is released
+            return;
+        }
     }
 
+    if (ST && (MSAT_GRU_ABL & 128)) {  // ablation bit 7: no epilogue (accumulators kept live)
+        if constexpr (HVE) wait_vmcnt<0>();
+        float v = 0.f;
+#pragma unroll
+        for (int G = 0; G < 4; ++G)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v += acc[G][j][0] + acc[G][j][1] + acc[G][j][2] + acc[G][j][3];
+        if (arow < a.R) a.out[(size_t)arow * a.ldo + lane] = v;
+        return;
+    }
     // ---- epilogue.  C/D map: unit u = 16 j + l16, row wr + 4 g + reg.
     float *stage = reinterpret_cast<float *>(Bs) + w * 16 * 132;  // [16 rows][132] per wave
     const bool tape = a.g4 != nullptr;
-    // h of each accumulator's (row, unit), loaded before the tape stores (vector-memory counts retire
-    // in issue order, so a load issued after them would wait for them)
     float hv[8][4];
+    if constexpr (HVE) {
+        wait_vmcnt<0>();  // this wave's own h rows have landed
+        const float *hl = hbase(((ns - 1) & 1) ^ 1);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = row0 + wr + 4 * g + r;
-            hv[j][r] = hp[(size_t)(row < a.R ? row : a.R - 1) * a.ldp + 16 * j + l16];
-        }
+            for (int r = 0; r < 4; ++r) hv[j][r] = hl[(4 * g + r) * H + 16 * j + l16];
+        barrier_lds();  // every wave has read its h before any wave's stage (over Bs) is written
+    } else {
+        // loaded before the tape stores (vector-memory counts retire in issue order, so a load issued
+        // after them would wait for them)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = row0 + wr + 4 * g + r;
+                hv[j][r] = hp[(size_t)(row < a.R ? row : a.R - 1) * a.ldp + 16 * j + l16];
+            }
+    }
     constexpr float sc = 1.0f / (float)(1 << kH2Shift);  // exact power of two
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
