@@ -788,6 +788,9 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 #ifndef MSAT_GRU_SPLH
 #define MSAT_GRU_SPLH 0
 #endif
+#ifndef MSAT_GRU_PKE
+#define MSAT_GRU_PKE 1
+#endif
 #ifndef MSAT_GRU_HVE
 #define MSAT_GRU_HVE 1
 #endif
@@ -1140,6 +1143,21 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
             }
     }
     constexpr float sc = 1.0f / (float)(1 << kH2Shift);  // exact power of two
+#if MSAT_GRU_PKE
+    // packed fp32 (v_pk_mul / v_pk_add on row pairs): no MFMAs run here, so the packed forms halve the
+    // epilogue's vector issue instead of competing with matrix work
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int u = 16 * j + l16;
+        const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
+        const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
+        const f32x4g s4 = {sc, sc, sc, sc};
+        acc[0][j] = acc[0][j] * s4 + f32x4g{br, br, br, br};
+        acc[1][j] = acc[1][j] * s4 + f32x4g{bz, bz, bz, bz};
+        acc[2][j] = acc[2][j] * s4 + f32x4g{bni, bni, bni, bni};
+        acc[3][j] = acc[3][j] * s4 + f32x4g{bnh, bnh, bnh, bnh};
+    }
+#else
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int u = 16 * j + l16;
@@ -1153,6 +1171,7 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
             acc[3][j][r] = acc[3][j][r] * sc + bnh;
         }
     }
+#endif
     // float4 rows of the wave's [16][128] stage -> dst (row stride ld), rows < R only.  The stage is
     // wave-private and a wave's LDS operations complete in issue order, so waiting for its own stage
     // writes (lgkmcnt) is the only ordering needed: no workgroup barrier, whose release fence would
@@ -1170,7 +1189,8 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
     };
     if (tape) {
         // pre-activations straight from the accumulators (16 lanes x 4 B per row segment; staging them
-        // through LDS as float4 rows measured 0-4 % slower)
+        // through LDS as float4 rows measured 0-4 % slower, float4 rows by a DPP 4 x 4 transpose inside
+        // each lane quad 5 % slower: profiles/r02_ab_gru_tq.log)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = row0 + wr + 4 * g + r;
@@ -1183,6 +1203,63 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
             }
         }
     }
+#if MSAT_GRU_PKE
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    constexpr float kL2E = 1.4426950408889634f;  // exp(x) = 2^(x log2 e), as __expf
+    auto exp2v = [](f2 x) { return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; };
+    auto rcpv = [](f2 x) { return f2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; };
+    const f2 one = {1.f, 1.f}, ml2e = {-kL2E, -kL2E}, m2l2e = {-2.f * kL2E, -2.f * kL2E}, two = {2.f, 2.f};
+    f2 s1v[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, s2v[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {  // rows 2p, 2p + 1
+            const f2 rp = {acc[0][j][2 * p], acc[0][j][2 * p + 1]}, zp = {acc[1][j][2 * p], acc[1][j][2 * p + 1]};
+            const f2 gi = {acc[2][j][2 * p], acc[2][j][2 * p + 1]}, gh = {acc[3][j][2 * p], acc[3][j][2 * p + 1]};
+            const f2 h = {hv[j][2 * p], hv[j][2 * p + 1]};
+            const f2 rg = rcpv(one + exp2v(rp * ml2e)), zg = rcpv(one + exp2v(zp * ml2e));
+            const f2 ng = two * rcpv(one + exp2v((gi + rg * gh) * m2l2e)) - one;  // tanh = 2 sigma(2x) - 1
+            const f2 hn = (one - zg) * ng + zg * h;
+            acc[0][j][2 * p] = hn.x;
+            acc[0][j][2 * p + 1] = hn.y;
+            s1v[p] += hn;
+            s2v[p] += hn * hn;
+        }
+    // sums over the 16 lanes of a row group (DPP row rotations and quad swaps, no LDS round trips)
+    auto row16 = [](float v) {
+        auto dpp = [](float x, auto ctl) {
+            return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x),
+                                                                         decltype(ctl)::value, 0xF, 0xF, false));
+        };
+        v += dpp(v, std::integral_constant<int, 0x128>{});  // row_ror:8
+        v += dpp(v, std::integral_constant<int, 0x124>{});  // row_ror:4
+        v += dpp(v, std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
+        v += dpp(v, std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
+        return v;
+    };
+    float mean[4], rs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float t1 = row16(r & 1 ? s1v[r >> 1].y : s1v[r >> 1].x);
+        const float t2 = row16(r & 1 ? s2v[r >> 1].y : s2v[r >> 1].x);
+        mean[r] = t1 / (float)H;
+        const float var = fmaxf(t2 / (float)H - mean[r] * mean[r], 0.0f);
+        rs[r] = rsqrtf(var + 1e-6f);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int u = 16 * j + l16;
+        const float scl = a.ln_scale[u], lb = a.ln_bias[u];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const f2 hn = {acc[0][j][2 * p], acc[0][j][2 * p + 1]};
+            const f2 y = (hn - f2{mean[2 * p], mean[2 * p + 1]}) * (f2{rs[2 * p], rs[2 * p + 1]} * f2{scl, scl}) +
+                         f2{lb, lb};
+            stage[(4 * g + 2 * p) * 132 + u] = y.x;
+            stage[(4 * g + 2 * p + 1) * 132 + u] = y.y;
+        }
+    }
+#else
     float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -1217,6 +1294,7 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         for (int r = 0; r < 4; ++r)
             stage[(4 * g + r) * 132 + u] = (acc[0][j][r] - mean[r]) * (rs[r] * scl) + lb;
     }
+#endif
     flush(a.out, a.ldo);
 }
 
