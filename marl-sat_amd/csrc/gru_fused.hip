@@ -1190,7 +1190,8 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
     if (tape) {
         // pre-activations straight from the accumulators (16 lanes x 4 B per row segment; staging them
         // through LDS as float4 rows measured 0-4 % slower, float4 rows by a DPP 4 x 4 transpose inside
-        // each lane quad 5 % slower: profiles/r02_ab_gru_tq.log)
+        // each lane quad 5 % slower: profiles/r02_ab_gru_tq.log; non-temporal stores +1.3 % clause / -1.3 % var,
+        // r02_ab_gru_nt.log)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = row0 + wr + 4 * g + r;
