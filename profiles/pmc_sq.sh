@@ -19,7 +19,7 @@ import csv, glob, collections
 acc = collections.defaultdict(list)
 for f in sorted(glob.glob("$OUT/p*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith("msat"):
+        if "msat::" in r["Kernel_Name"]:
             acc[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
 ks = sorted({k for k, _ in acc})
 for k in ks:
