@@ -999,7 +999,8 @@ wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ 
 // NP = 2: fp16x2 (three fp16 MFMAs).  G is scaled by 2^e with e the smallest row exponent of the
 // split (rexp, written by the GRU backward that produced G: every scaled row below 2^15, the
 // largest at full precision) and the partial by 2^-e (exact).  A is range-checked (|a| < 2^15): a
-// workgroup that loads anything outside sets flags[id] and stores nothing.
+// workgroup that loads anything outside sets flags[id] and stores nothing; G needs no check (a
+// non-finite G row stays non-finite through the fp16 products, as it would in fp32).
 //
 // IL: the split and LDS store of slab s + 1 are interleaved with slab s's MFMAs by scheduling groups
 // (one MFMA, then a few vector instructions; an LDS store every few MFMAs), so the split fills the
@@ -1081,10 +1082,20 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
     auto store = [&](int s, Stage r, int buf) {
         const bool mok = rb + s * 16 + srow < re;
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!(mok && kok)) r.a = z;
+        if constexpr (NP == 2) {
+            // rows past the split: zero A only (the product of a zero row is zero whatever G holds);
+            // columns past K or N read clamped, finite data and land in dW rows / columns that are
+            // never stored, so they need no zeroing; G is in fp16 range by construction (ge is the
+            // split's smallest row exponent), so only A is range-checked.  -4.7 % on the dual launch
+            // (profiles/r02_ab_wgrad_lean.log); the split by v_fma_mix{lo,hi}_f16 (two instructions per
+            // element pair instead of four) measured +0.3 % on top (r02_ab_wgrad_mix.log, not kept)
+            if (!mok) r.a = z;
+        } else {
+            if (!(mok && kok)) r.a = z;
 #pragma unroll
-        for (int u = 0; u < 3; ++u)
-            if (!(mok && nok[u])) r.g[u] = z;
+            for (int u = 0; u < 3; ++u)
+                if (!(mok && nok[u])) r.g[u] = z;
+        }
         if constexpr (NP == 3) {
             const Split4 xa = split4(r.a);
 #pragma unroll
@@ -1104,7 +1115,6 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
             for (int u = 0; u < 3; ++u) {
                 const float4 v = make_float4(ldexpf(r.g[u].x, ge), ldexpf(r.g[u].y, ge), ldexpf(r.g[u].z, ge),
                                              ldexpf(r.g[u].w, ge));
-                amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
                 const SplitH4 xg = splith4(v);
                 put(buf, 2 + u, xg.p[0]);
                 put(buf, 5 + u, xg.p[1]);

@@ -1226,16 +1226,26 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
             s1v[p] += hn;
             s2v[p] += hn * hn;
         }
-    // sums over the 16 lanes of a row group (DPP row rotations and quad swaps, no LDS round trips)
-    auto row16 = [](float v) {
+    // sums over the 16 lanes of a row group: the xor butterfly of __shfl_xor(v, 1 / 2 / 4 / 8, 16) (same
+    // association, so bit-identical sums) by DPP instead of LDS permutes -- quad swaps for 1 and 2,
+    // row shifts selected by the lane's bit for 4 and 8
+    auto row16 = [lane](float v) {
         auto dpp = [](float x, auto ctl) {
-            return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x),
-                                                                         decltype(ctl)::value, 0xF, 0xF, false));
+            return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), decltype(ctl)::value,
+                                                                      0xF, 0xF, true));
         };
-        v += dpp(v, std::integral_constant<int, 0x128>{});  // row_ror:8
-        v += dpp(v, std::integral_constant<int, 0x124>{});  // row_ror:4
-        v += dpp(v, std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
-        v += dpp(v, std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
+        v += dpp(v, std::integral_constant<int, 0xB1>{});  // quad_perm [1,0,3,2]: lane ^ 1
+        v += dpp(v, std::integral_constant<int, 0x4E>{});  // quad_perm [2,3,0,1]: lane ^ 2
+        {
+            const float up = dpp(v, std::integral_constant<int, 0x104>{});  // row_shl:4: lane + 4
+            const float dn = dpp(v, std::integral_constant<int, 0x114>{});  // row_shr:4: lane - 4
+            v += (lane & 4) ? dn : up;
+        }
+        {
+            const float up = dpp(v, std::integral_constant<int, 0x108>{});  // row_shl:8
+            const float dn = dpp(v, std::integral_constant<int, 0x118>{});  // row_shr:8
+            v += (lane & 8) ? dn : up;
+        }
         return v;
     };
     float mean[4], rs[4];
