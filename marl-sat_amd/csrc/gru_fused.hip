@@ -1321,6 +1321,7 @@ __global__ void __launch_bounds__(256, 2) gru_ln_fused_fwd_h2p_kernel(GruX3rArgs
     gru_h2r_tile<true, 4, 1>(a, blockIdx.x);
 }
 
+
 // bf16x3 register-A kernel (the template above is fp16x2-only: instantiated for bf16x3 it computed
 // wrong results; this is the round-1 kernel, unchanged).  Pipeline switches: activations loaded two
 // steps ahead by asm, weight fragments carried across column blocks, tape stored from the accumulators.
