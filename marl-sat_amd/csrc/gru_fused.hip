@@ -846,11 +846,11 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         for (int j = 0; j < 8; ++j) acc[G][j] = f32x4g{};
     const int slot = g ^ gswz16((l16 >> 2) & 3);
     float amax = 0.f;  // largest |activation| this lane split (range check)
-    // Activation loads by asm (invisible to hipcc's wait insertion) two steps ahead into alternating
-    // register sets; the split of step s + 1 runs among step s's MFMAs; one vmcnt(0) + barrier per
-    // step (the weights of s + 1 and the activations of s + 2, both issued at the start of step s,
-    // have landed).  The wait names the set just loaded as an in/out operand, so no use of it is
-    // scheduled above the wait.
+    // Activation loads one or two steps ahead into alternating register sets (plain loads, tracked by
+    // hipcc); the split of step s + 1 runs among step s's MFMAs; one vmcnt(0) + barrier per step.
+    // These were asm loads once: hipcc treats an asm output as ready at the asm and may copy or move
+    // its registers before the data lands (it did once the x3r body was inlined into a second kernel:
+    // rows of garbage), so register loads stay visible to the compiler; only LDS-DMA is asm.
     typedef float f4v __attribute__((ext_vector_type(4)));
     f4v ras[2][2];  // [set = step & 1][half]
     auto aptr = [&](int st, int e) -> const float * {
@@ -863,9 +863,10 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
     };
     auto aload = [&](int st, f4v (&r)[2]) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[e]) : "v"(aptr(st, e)) : "memory");
+        for (int e = 0; e < 2; ++e) r[e] = *reinterpret_cast<const f4v *>(aptr(st, e));
     };
-    auto await0 = [&](f4v (&r)[2]) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]) :: "memory"); };
+    // all vector memory of this wave (the weight DMA, which hipcc cannot see, and the activation loads)
+    auto await0 = [&](f4v (&)[2]) { wait_vmcnt<0>(); };
     auto asplit = [&](int st, const f4v (&r)[2], uint4 (&f)[2]) {  // branch-free (selects)
         const int kx = (st - nsh) * 32 + 8 * g;
         const bool z0 = st >= nsh && kx >= kx_end, z1 = st >= nsh && kx + 4 >= kx_end;
@@ -1431,11 +1432,10 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
         barrier_lds();
     };
 #if MSAT_GRU_X3R_PIPE
-    // Pipelined form: activation loads by asm (invisible to hipcc's wait insertion) two steps
-    // ahead into alternating register sets; the split of step s + 1 runs among step s's MFMAs;
-    // one vmcnt(0) + barrier per step (the weights of s + 1 and the activations of s + 2, both
-    // issued at the start of step s, have landed).  The wait names the set just loaded as an
-    // in/out operand, so no use of it is scheduled above the wait.
+    // Pipelined form: activation loads two steps ahead into alternating register sets (plain loads,
+    // tracked by hipcc: see the note in gru_h2r_tile); the split of step s + 1 runs among step s's
+    // MFMAs; one vmcnt(0) + barrier per step (the weights of s + 1 and the activations of s + 2, both
+    // issued at the start of step s, have landed).
     typedef float f4v __attribute__((ext_vector_type(4)));
     f4v ras[2][2];  // [set = step & 1][half]
     auto aptr = [&](int st, int e) -> const float * {
@@ -1448,9 +1448,10 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
     };
     auto aload = [&](int st, f4v (&r)[2]) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[e]) : "v"(aptr(st, e)) : "memory");
+        for (int e = 0; e < 2; ++e) r[e] = *reinterpret_cast<const f4v *>(aptr(st, e));
     };
-    auto await0 = [&](f4v (&r)[2]) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]) :: "memory"); };
+    // all vector memory of this wave (the weight DMA, which hipcc cannot see, and the activation loads)
+    auto await0 = [&](f4v (&)[2]) { wait_vmcnt<0>(); };
     auto asplit = [&](int st, const f4v (&r)[2], bf16x8 (&f)[3]) {  // branch-free (selects)
         const int kx = (st - nsh) * 32 + 8 * g;
         const bool z0 = st >= nsh && kx >= kx_end, z1 = st >= nsh && kx + 4 >= kx_end;
