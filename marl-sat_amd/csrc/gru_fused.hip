@@ -1329,13 +1329,12 @@ __global__ void __launch_bounds__(256, 2) gru_ln_fused_fwd_h2p_kernel(GruX3rArgs
 #define MSAT_GRU_X3R_BPIPE 1
 #define MSAT_GRU_X3R_PIPE 1
 #define MSAT_GRU_TAPE_DIRECT 1
-__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs a) {
+__device__ __forceinline__ void gru_x3r_tile(const GruX3rArgs &a, int tile) {
     constexpr int H = 128, IMG = H * 4;  // uint4 per (plane, gate) image: 128 units x 4 chunks = 8 KiB
     __shared__ uint4 Bs[2][9][IMG];      // [buf][plane * 3 + gate], 144 KiB
-    if (a.flags && a.flags[blockIdx.x] == 0) return;  // fixup launch: only the tiles the fp16x2 kernel flagged
     const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int row0 = blockIdx.x * 128, wr = 16 * w;
+    const int row0 = tile * 128, wr = 16 * w;
     const int arow = row0 + wr + l16, arc = arow < a.R ? arow : a.R - 1;
     constexpr int nsh = H / 32;
     const int ns = nsh + a.kxp / 32;
@@ -1668,6 +1667,27 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs
             stage[(4 * g + r) * 132 + u] = (acc[0][j][r] - mean[r]) * (rs[r] * sc) + lb;
     }
     flush(a.out, a.ldo);
+}
+
+__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_kernel(GruX3rArgs a) { gru_x3r_tile(a, blockIdx.x); }
+
+// The bf16x3 fixup after an fp16x2 launch: recompute the tiles it flagged.  A few workgroups (one per
+// CU at most) scan the flags 64 tiles per load (lane i reads tile c0 + i * grid) and loop over the
+// flagged ones, instead of one workgroup per tile that reads its flag and exits (~17 us of dispatch
+// per launch when nothing is flagged, which is nearly always).  The mask is the same in every wave of
+// the workgroup, so the barrier between tiles is uniform.
+__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_x3r_fix_kernel(GruX3rArgs a, int ntiles) {
+    const int lane = threadIdx.x & 63;
+    for (int c0 = blockIdx.x; c0 < ntiles; c0 += 64 * gridDim.x) {
+        const int tl = c0 + lane * gridDim.x;
+        uint64_t m = __ballot(tl < ntiles && a.flags[tl] != 0);
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            gru_x3r_tile(a, c0 + b * gridDim.x);
+            __syncthreads();  // the next tile's DMA reuses the LDS the last one's epilogue read
+        }
+    }
 }
 
 // planes[q][n][k] = part q of (k < K ? W[k][n] : 0), n < N, k < Kp: the transposed, zero-padded
@@ -2009,6 +2029,7 @@ extern "C" int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w
     a.wiT = reinterpret_cast<const uint16_t *>(wiT_x3);
     a.whT = reinterpret_cast<const uint16_t *>(whT_x3);
     a.wbad = nullptr;
-    hipLaunchKernelGGL(gru_ln_fused_fwd_x3r_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
-    return check_launch("gru_ln_fused_fwd_x3r_kernel (fixup)");
+    hipLaunchKernelGGL(gru_ln_fused_fwd_x3r_fix_kernel, dim3(std::min(tiles, 256)), dim3(512), 0, (hipStream_t)stream,
+                       a, tiles);
+    return check_launch("gru_ln_fused_fwd_x3r_fix_kernel (fixup)");
 }

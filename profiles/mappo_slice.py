@@ -15,7 +15,7 @@ bench = json.loads(line)["mappo"]
 ROCPROF_NAMES = {  # bench label -> rocprof kernel names whose launches the bench's event pair brackets
     "gru_ln_fused_fwd_x3r_kernel (bf16x3)": ["gru_ln_fused_fwd_x3r_kernel"],
     "gru_ln_fused_fwd_h2r_kernel (fp16x2, + x3r fixup launch)": ["gru_ln_fused_fwd_h2r_kernel", "gru_ln_fused_fwd_x3r_kernel"],
-    "gru_ln_fused_fwd_h2s_kernel (fp16x2, + x3r fixup launch)": ["gru_ln_fused_fwd_h2s_kernel", "gru_ln_fused_fwd_x3r_kernel"],
+    "gru_ln_fused_fwd_h2s_kernel (fp16x2, + x3r fixup launch)": ["gru_ln_fused_fwd_h2s_kernel", "gru_ln_fused_fwd_x3r_fix_kernel"],
     "gemm_x3r16_kernel (dgrad, bf16x3)": ["gemm_x3r16_kernel"],
     "wgrad_x3_kernel + reduce (bf16x3)": ["wgrad_x3_kernel", "wgrad_reduce4_kernel"],
     "wgrad_w_kernel<3> + reduce (bf16x3)": ["wgrad_w_kernel<3", "wgrad_reduce4_kernel"],
