@@ -181,8 +181,11 @@ gru_ln_fwd_kernel(const float *__restrict__ Gi, int ldi, const float *__restrict
 // NF > 0: the partials also carry feature-weighted gate sums for the input-matrix rows of NF
 // per-row features (feat, ld ldf): part[block][NQ + 3k + g] = sum_rows feat[r][k] * dG_g[r]
 // (g = r, z, n gate) -- the weight gradient of those input rows without another pass over dGi.
+#ifndef MSAT_BWD_OCC6
+#define MSAT_BWD_OCC6 1  // workgroups per CU the NF = 6 (var cell) form is compiled for (1: no bound)
+#endif
 template <int PER, bool G4, int NQ = 2, int NF = 0>
-__global__ void __launch_bounds__(kRowThreads)
+__global__ void __launch_bounds__(kRowThreads, NF == 6 ? MSAT_BWD_OCC6 : 1)
 gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
                   const float *__restrict__ scale, float *__restrict__ dGi, int lddi, float *__restrict__ dGh, int lddh,
@@ -489,7 +492,10 @@ using namespace msat;
 
 static int grid_rows(long rows) { return (int)std::min<long>((rows + 3) / 4, 8192); }
 // GRU/LN backward: at most 1024 blocks (16 waves per CU), so its per-block LN partials stay small
-static int bwd_blocks(long rows) { return (int)std::min<long>((rows + 3) / 4, 1024); }
+#ifndef MSAT_BWD_MAXB
+#define MSAT_BWD_MAXB 1024  // GRU backward grid cap (partial-sum rows = blocks)
+#endif
+static int bwd_blocks(long rows) { return (int)std::min<long>((rows + 3) / 4, MSAT_BWD_MAXB); }
 constexpr int kPartRows = 16;  // rows per first-stage block when reducing LN partials
 
 
