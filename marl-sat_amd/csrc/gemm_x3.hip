@@ -1014,9 +1014,6 @@ wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ 
 #ifndef MSAT_WW_PF
 #define MSAT_WW_PF 2  // raw slab sets of the fp16x2 form (2, 3 or 4: measured equal or slower)
 #endif
-#ifndef MSAT_WW_STG
-#define MSAT_WW_STG 0
-#endif
 constexpr int kWWT = 512;
 constexpr int kWWN = 384;  // widest N
 
@@ -1170,13 +1167,11 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
         store(0, R[0], 0);
         __syncthreads();
         // Rn holds slab s + 1, Rf receives slab s + NPF (past the end: a repeated, never stored load)
-        // STG: waves 4..7 (the SIMD partners of waves 0..3, which run in lockstep with them between the
-        // barriers) issue their slab loads after the slab's MFMAs instead of before them.  Measured 5 %
-        // slower on the dual launch (profiles/r02_ab_wgrad_stg.log): off.
-        const bool late = MSAT_WW_STG && w >= 4;
+        // (a stagger of SIMD partners -- waves 4..7 issuing their loads after the slab's MFMAs --
+        // measured 5 % slower on the dual launch, profiles/r02_ab_wgrad_stg.log)
         auto iter = [&](int s, const Stage &Rn, Stage &Rf) {
             const int buf = s & 1;
-            if (!(MSAT_WW_ABL & 1) && !late) load(s + NPF < ns ? s + NPF : ns - 1, Rf);
+            if (!(MSAT_WW_ABL & 1)) load(s + NPF < ns ? s + NPF : ns - 1, Rf);
             __builtin_amdgcn_sched_barrier(0);
             if (!(MSAT_WW_ABL & 2)) slab(buf);
             if constexpr (IL) {
@@ -1192,10 +1187,6 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
             } else {
                 __builtin_amdgcn_sched_barrier(0);
                 store(s + 1, Rn, buf ^ 1);
-            }
-            if (MSAT_WW_STG) {
-                __builtin_amdgcn_sched_barrier(0);
-                if (!(MSAT_WW_ABL & 1) && late) load(s + NPF < ns ? s + NPF : ns - 1, Rf);
             }
             __syncthreads();
         };

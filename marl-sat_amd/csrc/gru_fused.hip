@@ -785,9 +785,6 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 #ifndef MSAT_GRU_DMA1
 #define MSAT_GRU_DMA1 8
 #endif
-#ifndef MSAT_GRU_SPLH
-#define MSAT_GRU_SPLH 0
-#endif
 #ifndef MSAT_GRU_PKE
 #define MSAT_GRU_PKE 1
 #endif
@@ -921,33 +918,6 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
         v[1] = __builtin_bit_cast(f4v, row[(2 * g + 1) ^ sw]);
         asplit(st, v, f);
     };
-    // half of lsplit: float4 e of the lane's 8 k, into dwords 2e, 2e + 1 of both planes (SPLH: the two
-    // halves run in different blocks of the step, so each VALU burst between MFMAs is half as long)
-    auto lsplit_h = [&](int st, uint4 (&f)[2], auto ec) {
-        constexpr int e = decltype(ec)::value;
-        const int r = wr + l16, sw = (r >> 1) & 5;
-        const uint4 *row = &As[(st % 3) * ASL + 8 * r];
-        const f4v zero = {0.f, 0.f, 0.f, 0.f};
-        const f4v raw = __builtin_bit_cast(f4v, row[(2 * g + e) ^ sw]);
-        const bool z = st >= nsh && (st - nsh) * 32 + 8 * g + 4 * e >= kx_end;
-        const float4 v = __builtin_bit_cast(float4, z ? zero : raw);
-        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-        const float x[4] = {v.x, v.y, v.z, v.w};
-        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-        f16x4 h, l;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const _Float16 q = (_Float16)x[j];
-            h[j] = q;
-            l[j] = (_Float16)(x[j] - (float)q);
-        }
-        const uint2 hb = __builtin_bit_cast(uint2, h), lb = __builtin_bit_cast(uint2, l);
-        if constexpr (e == 0) {
-            f[0].x = hb.x, f[0].y = hb.y, f[1].x = lb.x, f[1].y = lb.y;
-        } else {
-            f[0].z = hb.x, f[0].w = hb.y, f[1].z = lb.x, f[1].w = lb.y;
-        }
-    };
     if constexpr (ST) {
         issueA(0);
         if (ns > 1) issueA(1);
@@ -1043,12 +1013,7 @@ __device__ __forceinline__ void gru_h2r_tile(const GruX3rArgs &a, int tile) {
                 if (nomma) c += __builtin_bit_cast(f32x4g, b0 ^ b1);
                 if (!noread && n + LA < 24) b0 = bfrag(n + LA, 0);
                 acc[G][j] = c;
-                if (ST && MSAT_GRU_SPLH && (n == 7 || n == 15)) {
-                    if (!(MSAT_GRU_ABL & 16) && st + 1 < ns) {
-                        if (n == 7) lsplit_h(st + 1, fas[PB ^ 1], std::integral_constant<int, 0>{});
-                        else lsplit_h(st + 1, fas[PB ^ 1], std::integral_constant<int, 1>{});
-                    }
-                } else if constexpr (ST) {
+                if constexpr (ST) {
                     if ((n == 7 && !(stg_split && late)) || (stg_split && n == 19 && late))
                         if (!(MSAT_GRU_ABL & 16) && st + 1 < ns) lsplit(st + 1, fas[PB ^ 1]);
                 } else if (n == 7) {

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The split-halves switch MSAT_GRU_SPLH was removed after this measurement: profiles/r02_ab_gru_la.log.)
 # GRU forward (LDS-staged fp16x2) variants, alternating on one box, tape on: fragment lookahead 3 / 4
 # blocks (ab/la3, la4; current 2) and the activation split in two halves (ab/splh, splhla3).
 set -eo pipefail
