@@ -80,6 +80,19 @@ __global__ void __launch_bounds__(256) obs_expand_rows_kernel(int4 *__restrict__
         }
     }
 }
+// pattern 3: one workgroup per env writes its A obs rows of D16 x 16 B, env-major ([E][A][D], the
+// product layout) or agent-major ([A][E][D]: agent a's rows of all envs contiguous)
+template <int NT>
+__global__ void __launch_bounds__(NT) fill_rows_kernel(int4 *__restrict__ dst, int E, int A, int D16, int amajor,
+                                                       int value) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i v = {value, value, value, value};
+    for (int e = blockIdx.x; e < E; e += gridDim.x)
+        for (int a = 0; a < A; ++a) {
+            const size_t row = amajor ? (size_t)a * E + e : (size_t)e * A + a;
+            for (int i = threadIdx.x; i < D16; i += NT) *reinterpret_cast<v4i *>(dst + row * D16 + i) = v;
+        }
+}
 }  // namespace msat
 
 extern "C" int msat_debug_obs_expand(void *dst, int32_t E, int32_t A, int32_t D, const int32_t *inst,
@@ -124,4 +137,16 @@ extern "C" int msat_debug_fill(void *dst, size_t bytes, int32_t value, int32_t n
         hipLaunchKernelGGL(msat::fill_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (int4 *)dst, n16,
                            value);
     return msat::check_launch("fill_kernel");
+}
+
+extern "C" int msat_debug_fill_rows(void *dst, int32_t E, int32_t A, int32_t D16, int32_t amajor, int32_t value,
+                                    int32_t threads, int32_t grid, void *stream) {
+    MSAT_REQUIRE(dst && E > 0 && A > 0 && D16 > 0 && grid > 0 && (threads == 256 || threads == 512), "bad fill args");
+    if (threads == 512)
+        hipLaunchKernelGGL(msat::fill_rows_kernel<512>, dim3(grid), dim3(512), 0, (hipStream_t)stream, (int4 *)dst, E,
+                           A, D16, amajor, value);
+    else
+        hipLaunchKernelGGL(msat::fill_rows_kernel<256>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (int4 *)dst, E,
+                           A, D16, amajor, value);
+    return msat::check_launch("fill_rows_kernel");
 }

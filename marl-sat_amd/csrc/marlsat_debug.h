@@ -16,6 +16,10 @@ int msat_debug_fill_chunked(void *dst, size_t bytes, int32_t value, int32_t nont
  * grid > 0: one lane per 16 B quad, grid-stride; grid < 0: -grid blocks, one wave per row. */
 int msat_debug_obs_expand(void *dst, int32_t E, int32_t A, int32_t D, const int32_t *inst, const uint32_t *vimg,
                           const uint32_t *mimg, int32_t grid, void *stream);
+/* One workgroup per env (grid-stride over E) writes its A rows of D16 x 16 B: env-major [E][A][D]
+ * (amajor = 0) or agent-major [A][E][D] (amajor = 1); threads 256 or 512. */
+int msat_debug_fill_rows(void *dst, int32_t E, int32_t A, int32_t D16, int32_t amajor, int32_t value, int32_t threads,
+                         int32_t grid, void *stream);
 #ifdef __cplusplus
 }
 #endif

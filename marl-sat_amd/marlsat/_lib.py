@@ -186,7 +186,9 @@ def debug_lib():
         P = c_void_p
         for name, args in (("msat_debug_fill", [P, c_size_t, c_int32, c_int32, c_int32, P]),
                            ("msat_debug_fill_chunked", [P, c_size_t, c_int32, c_int32, c_int32, P]),
-                           ("msat_debug_obs_expand", [P, c_int32, c_int32, c_int32, P, P, P, c_int32, P])):
+                           ("msat_debug_obs_expand", [P, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
+                           ("msat_debug_fill_rows", [P, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                                     P])):
             fn = getattr(d, name)
             fn.restype, fn.argtypes = c_int32, args
         _debug = d
