@@ -279,7 +279,13 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
     env = SATEnv(V, C, max_steps=512, vars_per_agent=vpa)
     pool = env.make_pool(generate_problem_pool(V, C, args.pool, size_id=size_id))
     net = GNNActorCritic(H, L, env.num_agents, env.max_vars_per_agent, 0, V, device=env.device, seed=0)
-    learner = MAPPOLearner(cfg, env, net, pool, dist=dist if world > 1 else None)
+    comm = dist if world > 1 else None
+    if comm is not None and os.environ.get("MARLSAT_COLLECTIVES") == "capi":
+        # the learner's all-reduces through the C-ABI communicator (msat_comm_init / msat_allreduce_sum)
+        from marlsat.learners.collectives import CapiComm
+
+        comm = CapiComm.from_dist(dist)
+    learner = MAPPOLearner(cfg, env, net, pool, dist=comm)
     rs = learner.init_runner_state(PRNGKey(77 + rank))
     gen = torch.Generator().manual_seed(99 + rank)
     learner.cfg["UPDATE_EPOCHS"] = 1  # warm-up cycle (every kernel and buffer shape), one epoch
@@ -332,7 +338,8 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
         "config": {"workload": workload, "num_vars": V, "num_clauses": C, "num_agents": env.num_agents,
                    "envs_per_gpu": B, "NUM_STEPS": T, "UPDATE_EPOCHS": E, "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"],
                    "GNN_HIDDEN_DIM": H, "GNN_NUM_MESSAGE_PASSING_STEPS": L, "micro_batch": learner.micro,
-                   "parallelism": f"dp{world} (env shards; RCCL gradient all-reduce per minibatch)"},
+                   "parallelism": f"dp{world} (env shards; RCCL gradient all-reduce per minibatch"
+                                  f"{', C-ABI communicator' if type(comm).__name__ == 'CapiComm' else ''})"},
         "roofline": mappo_roofline(dom),
         "kernels": kernels,
         "issued_gemm_tflops_over_cycle": gemm_tflops,

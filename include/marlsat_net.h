@@ -253,12 +253,20 @@ int msat_ppo_loss(const float *logits, int32_t S, int32_t A, int32_t M, int32_t 
                   float *dlogits, float *dvalue, float *row_terms, double *loss_sums, void *stream);
 int msat_adam(float *params, const float *grads, float *m, float *v, size_t n, float lr, float b1, float b2,
               float eps, int32_t count, float grad_scale, void *stream);
-/* Collectives: no msat_comm_init / msat_allreduce (SURVEY.md 8(b) sketched them).  The gradient is ONE
- * flat fp32 buffer (the grads of every parameter, 16-B aligned tensors), so the host all-reduces it with
- * RCCL in place (sum; marlsat/learners/collectives.py uses torch.distributed, whose "nccl" backend is
- * RCCL on ROCm) and passes grad_scale = 1 / world to msat_adam (learner:647-650).  A host binding in
- * another language calls ncclAllReduce on the same buffer and stream; nothing in this library keeps a
- * communicator. */
+/* ---- collectives (RCCL over xGMI, one communicator per process) ----
+ * The gradient is ONE flat fp32 buffer (the grads of every parameter, 16-B aligned tensors): before
+ * msat_adam(..., grad_scale = 1 / world) every rank SUM-all-reduces it in place (learner:647-650 is the
+ * single-device update this replaces).  The Python learner reaches RCCL either through torch.distributed
+ * (whose "nccl" backend is RCCL on ROCm; the default) or through these entry points
+ * (marlsat/learners/collectives.py CapiComm, MARLSAT_COLLECTIVES=capi); a cgo / JNI host uses these.
+ * Rank 0 draws the id, the host broadcasts its msat_comm_id_bytes() bytes, every rank calls
+ * msat_comm_init.  Errors: MSAT_EBADARG, MSAT_ECOMM (message from RCCL). */
+size_t msat_comm_id_bytes(void);
+int msat_comm_unique_id(uint8_t *id_out);
+int msat_comm_init(const uint8_t *id, int32_t rank, int32_t world, void **comm_out);
+/* in place: buf[0..count) = sum over ranks; dtype 0 = fp32, 1 = fp64; enqueued on `stream` */
+int msat_allreduce_sum(void *comm, void *buf, size_t count, int32_t dtype, void *stream);
+int msat_comm_destroy(void *comm);
 
 /* ---- learner glue (learner:562-592 minibatching, :661-719 metrics) ---- */
 /* out[0..N) = a keyed pseudo-random permutation of [0, N) (4-round Feistel + cycle walking), for the

@@ -166,6 +166,11 @@ def _load():
     sig["msat_adam"] = (I, [P, P, P, P, Z, F, F, F, F, I, F, P])
     sig["msat_moments"] = (I, [P, Z, P, P, P])
     sig["msat_standardize"] = (I, [P, Z, F, F, P])
+    sig["msat_comm_id_bytes"] = (Z, [])
+    sig["msat_comm_unique_id"] = (I, [P])
+    sig["msat_comm_init"] = (I, [P, I, I, P])
+    sig["msat_allreduce_sum"] = (I, [P, P, Z, I, P])
+    sig["msat_comm_destroy"] = (I, [P])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
@@ -196,6 +201,11 @@ def debug_lib():
 
 # Every symbol include/marlsat*.h declares (checked by tests/test_capi.py).
 EXPORTED = (
+    "msat_comm_id_bytes",
+    "msat_comm_unique_id",
+    "msat_comm_init",
+    "msat_allreduce_sum",
+    "msat_comm_destroy",
     "msat_moments",
     "msat_standardize",
     "msat_assemble_graph_batch",

@@ -16,6 +16,11 @@ replica of the parameters and Adam state.  The ranks meet only at:
 With ``dist is None`` or world 1 every function is the identity, so the
 single-GPU learner pays nothing.  The functions take torch tensors on any device:
 the CPU ``gloo`` tests (tests/test_dist_cpu.py) run exactly this code.
+
+``dist`` is torch.distributed (its "nccl" backend is RCCL on ROCm) or a ``CapiComm``: the same calls
+over the library's own RCCL communicator (``msat_comm_init`` / ``msat_allreduce_sum``,
+include/marlsat_net.h), the route a host without torch takes through the C-ABI
+(``MARLSAT_COLLECTIVES=capi`` in bench.py).
 """
 from __future__ import annotations
 
@@ -51,6 +56,68 @@ def global_moments(local_sums: torch.Tensor, n_local: int, dist) -> Tuple[float,
     s1, s2, cnt = mom.tolist()
     mean = s1 / cnt
     return mean, math.sqrt(max(s2 / cnt - mean * mean, 0.0)) + 1e-8
+
+
+class CapiComm:
+    """torch.distributed-shaped handle (``is_initialized``, ``get_world_size``, ``get_rank``,
+    ``all_reduce``: the calls this module makes) over one RCCL communicator of libmarlsat.so.  Tensors
+    must be contiguous fp32 / fp64 device tensors; the SUM runs in place on the current stream."""
+
+    def __init__(self, rank: int, world: int, uid: bytes):
+        import ctypes
+
+        from .. import _lib
+
+        self._lib, self.rank, self.world = _lib, int(rank), int(world)
+        n = int(_lib.lib.msat_comm_id_bytes())
+        if len(uid) != n:
+            raise ValueError(f"communicator id must be {n} bytes, got {len(uid)}")
+        buf = (ctypes.c_uint8 * n).from_buffer_copy(uid)
+        handle = ctypes.c_void_p()
+        _lib.check(_lib.lib.msat_comm_init(buf, self.rank, self.world, ctypes.byref(handle)), "msat_comm_init")
+        self._comm = handle
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+
+        from .. import _lib
+
+        n = int(_lib.lib.msat_comm_id_bytes())
+        buf = (ctypes.c_uint8 * n)()
+        _lib.check(_lib.lib.msat_comm_unique_id(buf), "msat_comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def from_dist(cls, dist) -> "CapiComm":
+        """Rank 0 draws the id and broadcasts it over an initialised torch.distributed group."""
+        rank, world = dist.get_rank(), dist.get_world_size()
+        box = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        return cls(rank, world, box[0])
+
+    def is_initialized(self) -> bool:
+        return self._comm is not None
+
+    def get_world_size(self) -> int:
+        return self.world
+
+    def get_rank(self) -> int:
+        return self.rank
+
+    def all_reduce(self, t: torch.Tensor, op=None) -> None:
+        if op is not None and "SUM" not in str(op).upper():
+            raise ValueError("CapiComm.all_reduce supports SUM only")
+        if not (t.is_cuda and t.is_contiguous() and t.dtype in (torch.float32, torch.float64)):
+            raise ValueError("CapiComm.all_reduce needs a contiguous fp32 / fp64 device tensor")
+        self._lib.check(self._lib.lib.msat_allreduce_sum(self._comm, t.data_ptr(), t.numel(),
+                                                         1 if t.dtype == torch.float64 else 0,
+                                                         self._lib.stream_ptr(t.device)), "msat_allreduce_sum")
+
+    def destroy(self) -> None:
+        if self._comm is not None:
+            self._lib.check(self._lib.lib.msat_comm_destroy(self._comm), "msat_comm_destroy")
+            self._comm = None
 
 
 def init_from_env(backend: Optional[str] = None):

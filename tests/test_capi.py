@@ -116,3 +116,19 @@ def test_ctypes_argtypes_match_header_prototypes():
         n = 0 if params in ("", "void") else params.count(",") + 1
         argtypes = getattr(_lib.lib, name).argtypes
         assert argtypes is not None and len(argtypes) == n, (name, n, argtypes)
+
+
+def test_collective_entry_points_reject_bad_arguments():
+    """msat_comm_init / msat_allreduce_sum argument checks run before any RCCL call."""
+    from marlsat import _lib
+
+    L = _lib.lib
+    assert L.msat_comm_id_bytes() == 128
+    h = ctypes.c_void_p()
+    uid = (ctypes.c_uint8 * 128)()
+    assert L.msat_comm_init(uid, 0, 0, ctypes.byref(h)) == -1
+    assert b"world" in L.msat_last_error()
+    assert L.msat_comm_init(uid, 2, 2, ctypes.byref(h)) == -1
+    assert L.msat_allreduce_sum(None, None, 4, 0, None) == -1
+    assert b"communicator" in L.msat_last_error()
+    assert L.msat_comm_destroy(None) == 0
