@@ -8,7 +8,10 @@ Measured (profiles/r02_ab_gather_xcd.log, 820 samples: 1.25M clause rows, 0.82M 
 384-394 / 496-501 / 548-569 us.  An XCD-contiguous row walk (XCD x = blockIdx % 8 walks the contiguous
 chunk x of the rows, so one graph's shared source rows stay in one L2) was built behind a switch and
 measured against the grid-stride walk, alternating: 1955 / 1946 us against 1954 / 1952 us for the four
-calls, i.e. neutral (the re-fetches across XCDs are served by the MALL), and removed."""
+calls, i.e. neutral (the re-fetches across XCDs are served by the MALL), and removed.  Loading the next
+row's slots while the current row's sources are in flight (one dependent round trip per row instead of
+two) made the clause gathers 1-4 % slower (r02_ab_gather_pf.log: 493-501 vs 480-487 us): 32 resident
+waves per CU already hide the chain."""
 import json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "marl-sat_amd")]
