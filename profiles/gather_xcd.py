@@ -11,7 +11,10 @@ measured against the grid-stride walk, alternating: 1955 / 1946 us against 1954 
 calls, i.e. neutral (the re-fetches across XCDs are served by the MALL), and removed.  Loading the next
 row's slots while the current row's sources are in flight (one dependent round trip per row instead of
 two) made the clause gathers 1-4 % slower (r02_ab_gather_pf.log: 493-501 vs 480-487 us): 32 resident
-waves per CU already hide the chain."""
+waves per CU already hide the chain.  PMC (profiles/ab_gather_walk.sh, r02_gather_walk/): with the XCD walk
+each gather's L2 fabric reads fall to its minimal bytes (clause fwd 1.67 -> 0.81 GB, var fwd 1.81 -> 0.75,
+clause bwd 2.31 -> 1.43, var bwd 2.74 -> 2.07) while the time stays within 1 % (grid cap 2048: -1 %,
+1024: +42 %), so the gathers are bound by per-row latency at full occupancy, not by bytes."""
 import json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "marl-sat_amd")]
