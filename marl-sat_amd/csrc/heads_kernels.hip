@@ -22,6 +22,11 @@ struct GraphRef {
 
 // ---------------------------------------------------------------- critic ----
 // pooled (S, 6H) = [mean_v(2H) | max_v(2H) | mean_c(H) | max_c(H)] over graph 0 of each sample.
+// The row loops of the pooling kernels are unrolled 8 deep so eight independent row loads fly per
+// round trip (a plain loop waited on each load: one HBM latency per row); the accumulation order is
+// unchanged, so the results are bit-identical.  Measured (uf100 x 4096 MAPPO leg, rocprof): critic
+// pool 282 -> 91 us, its backward 753 -> 435 us, actor pool 577 -> 517 us; the actor pool backward (a
+// read-modify-write stream over 8,200 blocks, already ~3.9 TB/s) ran 622 -> 700 us unrolled and is not.
 __global__ void __launch_bounds__(256)
 critic_pool_kernel(const float *__restrict__ Hp, const float *__restrict__ Hn, const float *__restrict__ Hc, int H,
                    GraphRef gr, float *__restrict__ pooled) {
@@ -44,6 +49,7 @@ critic_pool_kernel(const float *__restrict__ Hp, const float *__restrict__ Hn, c
             n = nc;
         }
         float sum = 0.f, mx = -INFINITY;
+        #pragma unroll 8
         for (int r = 0; r < n; ++r) {
             const float v = src[(size_t)(base + r) * ld + col];
             sum += v;
@@ -93,10 +99,13 @@ critic_pool_bwd_kernel(const float *__restrict__ Hp, const float *__restrict__ H
             dmax = dp[5 * H + col];
         }
         float mx = -INFINITY;
+        #pragma unroll 8
         for (int r = 0; r < n; ++r) mx = fmaxf(mx, src[(size_t)(base + r) * H + col]);
         int cnt = 0;
+        #pragma unroll 8
         for (int r = 0; r < n; ++r) cnt += src[(size_t)(base + r) * H + col] == mx;
         const float gm = dmean / (float)n, gx = dmax / (float)cnt;
+        #pragma unroll 8
         for (int r = 0; r < n; ++r) {
             const size_t i = (size_t)(base + r) * H + col;
             dst[i] += gm + (src[i] == mx ? gx : 0.f);
@@ -121,6 +130,7 @@ actor_pool_kernel(const float *__restrict__ Hp, const float *__restrict__ Hn, co
         const float *src = j < H ? Hp : Hn;
         const int col = j < H ? j : j - H;
         float so = 0.f, sn = 0.f;
+        #pragma unroll 8
         for (int r = 0; r < nv; ++r) {
             const float v = src[(size_t)(vb + r) * H + col];
             if (r < nown) {
@@ -130,12 +140,14 @@ actor_pool_kernel(const float *__restrict__ Hp, const float *__restrict__ Hn, co
                 sn += v;
             }
         }
+        #pragma unroll 8
         for (int r = nown; r < M; ++r) my_emb[((size_t)sa * M + r) * 2 * H + j] = 0.f;
         cx[j] = so / (float)max(nown, 1);
         cx[2 * H + j] = sn / (float)max(nv - nown, 1);
     }
     for (int j = threadIdx.x; j < H; j += blockDim.x) {
         float sc = 0.f;
+        #pragma unroll 8
         for (int r = 0; r < nc; ++r) sc += Hc[(size_t)(cb + r) * H + j];
         cx[4 * H + j] = sc / (float)max(nc, 1);
     }
