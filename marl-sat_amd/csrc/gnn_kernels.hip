@@ -184,7 +184,138 @@ gru_ln_fwd_kernel(const float *__restrict__ Gi, int ldi, const float *__restrict
 #ifndef MSAT_BWD_OCC6
 #define MSAT_BWD_OCC6 1  // workgroups per CU the NF = 6 (var cell) form is compiled for (1: no bound)
 #endif
-template <int PER, bool G4, int NQ = 2, int NF = 0>
+// MSAT_BWD_VEC: for PER >= 2 a lane owns PER adjacent columns (PER * lane + u), loaded and stored as one
+// PER-wide vector access, instead of columns lane + 64 u (one dword access each).  The per-column
+// partials keep their row order; only the row sums behind the LayerNorm statistics change order.
+#ifndef MSAT_BWD_VEC
+#define MSAT_BWD_VEC 1
+#endif
+template <int N>
+__device__ __forceinline__ void ldv(const float *__restrict__ p, float *o) {
+    if constexpr (N == 1) {
+        o[0] = *p;
+    } else {
+        typedef float v __attribute__((ext_vector_type(N)));
+        const v t = *reinterpret_cast<const v *>(p);
+#pragma unroll
+        for (int u = 0; u < N; ++u) o[u] = t[u];
+    }
+}
+template <int N>
+__device__ __forceinline__ void stv(float *__restrict__ p, const float *o) {
+    if constexpr (N == 1) {
+        *p = o[0];
+    } else {
+        typedef float v __attribute__((ext_vector_type(N)));
+        v t;
+#pragma unroll
+        for (int u = 0; u < N; ++u) t[u] = o[u];
+        *reinterpret_cast<v *>(p) = t;
+    }
+}
+
+// One row of the backward in the vector column layout (columns PER * lane + u); same arithmetic per
+// element as the scalar body of gru_ln_bwd_kernel below.
+template <int PER, int NQ, int NF, int NQT>
+__device__ __forceinline__ void bwd_row_vec(const float *__restrict__ gi, const float *__restrict__ h,
+                                            const float *__restrict__ g, const float *__restrict__ scale,
+                                            float *__restrict__ di, float *__restrict__ dhh, float *__restrict__ dhp,
+                                            int H, int dh_assign, int packed, const float *__restrict__ feat,
+                                            int *__restrict__ rexp_r, int lane, float (&pq)[NQT][PER]) {
+    const int j0 = PER * lane;
+    float fw[NF > 0 ? NF : 1];
+#pragma unroll
+    for (int k = 0; k < NF; ++k) fw[k] = feat[k];
+    float rp[PER], zp[PER], np_[PER], ghn[PER], hv[PER], dyv[PER], sc[PER];
+    ldv<PER>(gi + j0, rp);
+    ldv<PER>(gi + H + j0, zp);
+    ldv<PER>(gi + 2 * H + j0, np_);
+    ldv<PER>(gi + 3 * H + j0, ghn);
+    ldv<PER>(h + j0, hv);
+    ldv<PER>(g + j0, dyv);
+    ldv<PER>(scale + j0, sc);
+    float old_dh[PER];
+    if (!dh_assign) ldv<PER>(dhp + j0, old_dh);
+    float rg[PER], zg[PER], ng[PER], hn[PER];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        rg[u] = sigmoidf_(rp[u]);
+        zg[u] = sigmoidf_(zp[u]);
+        ng[u] = tanhf(np_[u] + rg[u] * ghn[u]);
+        hn[u] = (1.0f - zg[u]) * ng[u] + zg[u] * hv[u];
+        s1 += hn[u];
+        s2 += hn[u] * hn[u];
+    }
+    s1 = wave_sum_f32(s1);
+    s2 = wave_sum_f32(s2);
+    const float mean = s1 / (float)H;
+    const float var = fmaxf(s2 / (float)H - mean * mean, 0.0f);
+    const float rs = rsqrtf(var + 1e-6f);
+    float xh[PER], dxh[PER];
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        xh[u] = (hn[u] - mean) * rs;
+        dxh[u] = dyv[u] * sc[u];
+        a1 += dxh[u];
+        a2 += dxh[u] * xh[u];
+        pq[0][u] += dyv[u] * xh[u];
+        pq[1][u] += dyv[u];
+    }
+    a1 = wave_sum_f32(a1) / (float)H;
+    a2 = wave_sum_f32(a2) / (float)H;
+    float rmax = 0.f;
+    float o_an[PER], o_ar[PER], o_az[PER], o_anr[PER], o_dh[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const float dhn = rs * (dxh[u] - a1 - xh[u] * a2);
+        const float dn = dhn * (1.0f - zg[u]);
+        const float dz = dhn * (hv[u] - ng[u]);
+        const float dan = dn * (1.0f - ng[u] * ng[u]);
+        const float dr = dan * ghn[u];
+        const float dar = dr * rg[u] * (1.0f - rg[u]);
+        const float daz = dz * zg[u] * (1.0f - zg[u]);
+        o_an[u] = dan;
+        o_ar[u] = dar;
+        o_az[u] = daz;
+        o_anr[u] = dan * rg[u];
+        o_dh[u] = dh_assign ? dhn * zg[u] : old_dh[u] + dhn * zg[u];
+        if (rexp_r) rmax = fmaxf(rmax, fmaxf(fmaxf(fabsf(dan), fabsf(dar)), fmaxf(fabsf(daz), fabsf(o_anr[u]))));
+        if constexpr (NQ == 6) {
+            pq[2][u] += dar;
+            pq[3][u] += daz;
+            pq[4][u] += dan;
+            pq[5][u] += o_anr[u];
+        }
+#pragma unroll
+        for (int k = 0; k < NF; ++k) {
+            pq[NQ + 3 * k][u] += fw[k] * dar;
+            pq[NQ + 3 * k + 1][u] += fw[k] * daz;
+            pq[NQ + 3 * k + 2][u] += fw[k] * dan;
+        }
+    }
+    if (packed) {  // [dan | dar | daz | dan r]
+        stv<PER>(di + j0, o_an);
+        stv<PER>(di + H + j0, o_ar);
+        stv<PER>(di + 2 * H + j0, o_az);
+        stv<PER>(di + 3 * H + j0, o_anr);
+    } else {
+        stv<PER>(di + j0, o_ar);
+        stv<PER>(di + H + j0, o_az);
+        stv<PER>(di + 2 * H + j0, o_an);
+        stv<PER>(dhh + j0, o_ar);
+        stv<PER>(dhh + H + j0, o_az);
+        stv<PER>(dhh + 2 * H + j0, o_anr);
+    }
+    stv<PER>(dhp + j0, o_dh);
+    if (rexp_r) {
+        rmax = wave_max_f32(rmax);
+        if (lane == 0) *rexp_r = f16x2_row_exp(rmax);
+    }
+}
+
+template <int PER, bool G4, int NQ = 2, int NF = 0, bool VEC = false>
 __global__ void __launch_bounds__(kRowThreads, NF == 6 ? MSAT_BWD_OCC6 : 1)
 gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
@@ -202,6 +333,13 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
     for (int r = blockIdx.x * 4 + w; r < R; r += gridDim.x * 4) {
         const float *gi = Gi + (size_t)r * ldi, *gh = G4 ? gi : Gh + (size_t)r * ldh, *h = hp + (size_t)r * ldp;
         const float *g = dy + (size_t)r * ldy;
+        if constexpr (VEC) {
+            static_assert(G4, "vector form reads the packed tape");
+            bwd_row_vec<PER, NQ, NF, NQT>(gi, h, g, scale, dGi + (size_t)r * lddi, dGh + (size_t)r * lddh,
+                                          dh + (size_t)r * lddh_prev, H, dh_assign, packed, feat + (size_t)r * ldf,
+                                          rexp ? rexp + r : nullptr, lane, pq);
+            continue;
+        }
         float fw[NF > 0 ? NF : 1];
 #pragma unroll
         for (int k = 0; k < NF; ++k) fw[k] = feat[(size_t)r * ldf + k];
@@ -297,7 +435,7 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
 #pragma unroll
         for (int q = 0; q < QC; ++q)
 #pragma unroll
-            for (int u = 0; u < PER; ++u) s_part[w][q * 64 * PER + lane + 64 * u] = pq[q0 + q][u];
+            for (int u = 0; u < PER; ++u) s_part[w][q * 64 * PER + (VEC ? PER * lane + u : lane + 64 * u)] = pq[q0 + q][u];
         __syncthreads();
         for (int j = threadIdx.x; j < QC * 64 * PER; j += kRowThreads) {
             const float v = (s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]);
@@ -652,14 +790,26 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
     MSAT_REQUIRE(!packed || (dGh == dGi + H && lddi == lddh && lddi >= 4 * H),
                  "gru_ln_bwd_g4: packed rows need dGh = dGi + H and a shared ld >= 4H");
     const int NQ = (bias ? 6 : 2) + 3 * nfeat;
+    // vector column layout when every row start is PER-float aligned (H = 64 has PER = 1: same layout)
+    const int vper = H / 64, va = 4 * vper;
+    const bool vec = MSAT_BWD_VEC && vper >= 2 && ((uintptr_t)dy | (uintptr_t)g4 | (uintptr_t)hprev |
+                                                   (uintptr_t)ln_scale | (uintptr_t)dGi | (uintptr_t)dGh |
+                                                   (uintptr_t)dhprev) % va == 0 &&
+                     (ldy | ldg | ldp | lddi | lddh | lddp) % vper == 0;
 #define MSAT_BWD1(PER, Q, F)                                                                                      \
-    hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev, ldp,   \
-                       ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed, feat, ldf, rexp)
+    if (vec)                                                                                                      \
+        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, \
+                           hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign,    \
+                           packed, feat, ldf, rexp);                                                              \
+    else                                                                                                          \
+        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev,   \
+                           ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed,   \
+                           feat, ldf, rexp)
 #define MSAT_BWD(PER)                                                                                             \
-    if (!bias) MSAT_BWD1(PER, 2, 0);                                                                               \
-    else if (nfeat == 0) MSAT_BWD1(PER, 6, 0);                                                                     \
-    else if (nfeat == 2) MSAT_BWD1(PER, 6, 2);                                                                     \
-    else MSAT_BWD1(PER, 6, 6);
+    if (!bias) { MSAT_BWD1(PER, 2, 0); }                                                                           \
+    else if (nfeat == 0) { MSAT_BWD1(PER, 6, 0); }                                                                 \
+    else if (nfeat == 2) { MSAT_BWD1(PER, 6, 2); }                                                                 \
+    else { MSAT_BWD1(PER, 6, 6); }
     if (H == 64) { MSAT_BWD(1) }
     else if (H == 128) { MSAT_BWD(2) }
     else { MSAT_BWD(4) }

@@ -14,5 +14,5 @@ for o in $R/marl-sat_amd/build/*.o; do
   [ "$b" = debug.o ] && continue
   if [ "$b" = "${SRC%.hip}.o" ]; then OBJS="$OBJS /tmp/abobj_$TAG/$b"; else OBJS="$OBJS $o"; fi
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/ab/$TAG.so $OBJS
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/ab/$TAG.so $OBJS -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built $R/ab/$TAG.so
