@@ -790,15 +790,18 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
     MSAT_REQUIRE(!packed || (dGh == dGi + H && lddi == lddh && lddi >= 4 * H),
                  "gru_ln_bwd_g4: packed rows need dGh = dGi + H and a shared ld >= 4H");
     const int NQ = (bias ? 6 : 2) + 3 * nfeat;
-    // vector column layout when every row start is PER-float aligned (H = 64 has PER = 1: same layout)
+    // vector column layout for the var cell (nfeat = 6) when every row start is PER-float aligned (H = 64
+    // has PER = 1: same layout).  Measured on the uf50 training shapes (profiles/r02y_ab_bwd_vec.log):
+    // var cell 503-506 vs 510-517 us; the clause cell (nfeat = 2) ran 1310-1341 vs 1132-1135 us in this
+    // layout, so it and the bias-less / feature-less forms keep the scalar layout.
     const int vper = H / 64, va = 4 * vper;
-    const bool vec = MSAT_BWD_VEC && vper >= 2 && ((uintptr_t)dy | (uintptr_t)g4 | (uintptr_t)hprev |
+    const bool vec = MSAT_BWD_VEC && nfeat == 6 && vper >= 2 && ((uintptr_t)dy | (uintptr_t)g4 | (uintptr_t)hprev |
                                                    (uintptr_t)ln_scale | (uintptr_t)dGi | (uintptr_t)dGh |
                                                    (uintptr_t)dhprev) % va == 0 &&
                      (ldy | ldg | ldp | lddi | lddh | lddp) % vper == 0;
 #define MSAT_BWD1(PER, Q, F)                                                                                      \
     if (vec)                                                                                                      \
-        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, \
+        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2 && F == 6>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, \
                            hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign,    \
                            packed, feat, ldf, rexp);                                                              \
     else                                                                                                          \
