@@ -254,7 +254,7 @@ def mappo_roofline(dom: dict) -> dict:
          "note": "dominant matrix kernel of the timed cycle; algorithmic fp32 FLOPs (2*R*3H*(H+Kx) per GRU call, "
                  "2*M*N*K per GEMM) and algorithmic HBM bytes (operands once + results, GRU: x, h in, h' and the "
                  "4H tape out) over its launches' summed duration (HIP events on the launch stream); rocprofv3 "
-                 "trace of the same leg, timed-cycle slice: profiles/r02f_mappo_uf100-430_slice.json"}
+                 "trace of the same leg, timed-cycle slice: profiles/r02y_mappo_uf100-430_slice.json"}
     return r
 
 
