@@ -190,6 +190,9 @@ gru_ln_fwd_kernel(const float *__restrict__ Gi, int ldi, const float *__restrict
 #ifndef MSAT_BWD_VEC
 #define MSAT_BWD_VEC 1
 #endif
+#ifndef MSAT_BWD_VEC_ALL
+#define MSAT_BWD_VEC_ALL 0  // A/B only: the vector layout for every cell form, not just the var cell
+#endif
 template <int N>
 __device__ __forceinline__ void ldv(const float *__restrict__ p, float *o) {
     if constexpr (N == 1) {
@@ -795,13 +798,13 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
     // var cell 503-506 vs 510-517 us; the clause cell (nfeat = 2) ran 1310-1341 vs 1132-1135 us in this
     // layout, so it and the bias-less / feature-less forms keep the scalar layout.
     const int vper = H / 64, va = 4 * vper;
-    const bool vec = MSAT_BWD_VEC && nfeat == 6 && vper >= 2 && ((uintptr_t)dy | (uintptr_t)g4 | (uintptr_t)hprev |
+    const bool vec = MSAT_BWD_VEC && (MSAT_BWD_VEC_ALL || nfeat == 6) && vper >= 2 && ((uintptr_t)dy | (uintptr_t)g4 | (uintptr_t)hprev |
                                                    (uintptr_t)ln_scale | (uintptr_t)dGi | (uintptr_t)dGh |
                                                    (uintptr_t)dhprev) % va == 0 &&
                      (ldy | ldg | ldp | lddi | lddh | lddp) % vper == 0;
 #define MSAT_BWD1(PER, Q, F)                                                                                      \
     if (vec)                                                                                                      \
-        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2 && F == 6>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, \
+        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2 && (MSAT_BWD_VEC_ALL || F == 6)>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, \
                            hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign,    \
                            packed, feat, ldf, rexp);                                                              \
     else                                                                                                          \
