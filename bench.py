@@ -10,20 +10,24 @@ timed region), obs int32 (the reference dtype).  One "step" = one fused
 Multi-GPU (torchrun, one process per GPU): independent env shards, no
 collective on the data path; barrier + synchronize around the timed region,
 max elapsed over ranks; value = all ranks' env-steps / that time (weak scaling).
+``python bench.py --gpus N`` without torchrun's env times the CPU baselines and
+then starts ``python -m torch.distributed.run --nproc-per-node N bench.py ...``
+as a child process; a world size that disagrees with ``--gpus`` fails.
 
 MAPPO legs (the metric's "MAPPO updates/sec"): one full train cycle of the device
 learner -- rollout of T steps (actor + critic forward, sampling, fused env step with
 auto-reset), GAE + global advantage normalisation, UPDATE_EPOCHS x T*B/MINIBATCH_SIZE
 PPO minibatches (forward, loss, backward, gradient all-reduce over RCCL when N>1,
 Adam) and the cycle metrics -- timed after one warm-up cycle.  The headline leg is
-uf100-430 x 4096 envs (BASELINE config 3, the metric's 4096 envs), T = 8; uf50-218 x
-1024 envs, T = 32 (config 2) is reported beside it.  Each leg carries per-phase times
-and a per-kernel table of the matrix kernels (HIP events around each launch, algorithmic
-FLOPs and HBM bytes per launch), and its roofline is the dominant kernel's against the lower
-of its two roofs: the ceiling of the matrix instruction it issues (fp16 dense / 3 for the
-fp16x2 kernels, bf16 dense / 6 for bf16x3) and its intensity x the 8 TB/s HBM peak.
+uf100-430 x 4096 envs (BASELINE config 3, the metric's 4096 envs), T = 8; uf200-860 x
+4096 envs per GPU, 25 agents, T = 2 (config 4) is reported beside it.  Each leg carries
+per-phase times and its roofline: the dominant matrix kernel (HIP events around each launch,
+algorithmic FLOPs and HBM bytes per launch) against the lower of its two roofs, the ceiling of
+the matrix instruction it issues (fp16 dense / 3 for the fp16x2 kernels, bf16 dense / 6 for
+bf16x3) and its intensity x the 8 TB/s HBM peak.  The full per-kernel tables go to a side
+file under gpurun_out/.
 
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0; the MAPPO legs close it.
 """
 from __future__ import annotations
 
@@ -31,8 +35,11 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
+from typing import Optional
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, "marl-sat_amd")):
@@ -92,15 +99,37 @@ def _cpu_worker(args):
         return steps * nenv, time.perf_counter() - t0
 
 
+def host_cpu() -> dict:
+    """The host the CPU baselines run on: model name (/proc/cpuinfo, as lscpu prints it), the cores
+    this process may run on (sched_getaffinity) and the cores used.  The default cap is the box's CPU
+    share: OMP_NUM_THREADS (16 per GPU on the GPU pool, where the affinity mask shows the whole
+    machine); MARLSAT_CPU_BASELINE_CORES overrides it."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    cap_src = "MARLSAT_CPU_BASELINE_CORES" if os.environ.get("MARLSAT_CPU_BASELINE_CORES") else (
+        "OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS") else "affinity")
+    cap = int(os.environ.get("MARLSAT_CPU_BASELINE_CORES") or os.environ.get("OMP_NUM_THREADS") or affinity)
+    return {"cpu_model": model, "affinity_cores": affinity, "cores": max(1, min(affinity, cap)),
+            "cap_source": cap_src}
+
+
 def cpu_baseline(V, C, vpa, pool, budget_s=12.0, nenv=16):
-    """Reference algorithm restated in NumPy (oracle), one process per host core (<=16)."""
+    """Reference algorithm restated in NumPy (oracle), one single-thread process per host core."""
     import multiprocessing as mp
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, int(os.environ.get("MARLSAT_CPU_BASELINE_CORES", 16))))
+    host = host_cpu()
+    cores = host["cores"]
     ctx = mp.get_context("fork")  # forked before any GPU initialisation
     with ctx.Pool(cores) as p:
         res = p.map(_cpu_worker, [(V, C, vpa, nenv, budget_s, w, pool) for w in range(cores)])
@@ -111,9 +140,11 @@ def cpu_baseline(V, C, vpa, pool, budget_s=12.0, nenv=16):
         "unit": "env-steps/s",
         "cores": cores,
         "kind": "port",
+        "host": host,
         "sample": f"oracle/sat_env.py step_autoreset (reference algorithm: full rescan, dense int32 obs, "
                   f"reset-all-then-select) on {cores} processes x {nenv} envs of the same workload, "
-                  f"{budget_s:.0f} s each ({total} env-steps)",
+                  f"{budget_s:.0f} s each ({total} env-steps); host {host['cpu_model']}, "
+                  f"{host['affinity_cores']} cores in the affinity mask, {cores} used ({host['cap_source']})",
     }
 
 
@@ -155,11 +186,8 @@ def mappo_cpu_baseline(workload: str, budget_s: float = 10.0, batch: int = 8):
     from oracle import net as onet
     from oracle.sat_env import OracleSATEnv
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, int(os.environ.get("MARLSAT_CPU_BASELINE_CORES", 16))))
+    host = host_cpu()
+    cores = host["cores"]
     prev = torch.get_num_threads()
     torch.set_num_threads(cores)
     try:
@@ -189,9 +217,10 @@ def mappo_cpu_baseline(workload: str, budget_s: float = 10.0, batch: int = 8):
     finally:
         torch.set_num_threads(prev)
     return {"value": n / wall, "unit": "PPO samples/s (minibatch forward + backward)", "cores": cores,
-            "kind": "port",
+            "kind": "port", "host": host,
             "sample": f"oracle/net.py ppo_loss + autograd (reference GNN_ActorCritic restated: dense masked per-agent "
-                      f"encoders), float32, {workload}, H=128, L=16, minibatches of {batch}, {n} samples in {wall:.1f} s"}
+                      f"encoders), float32, {workload}, H=128, L=16, minibatches of {batch}, {n} samples in {wall:.1f} s; "
+                      f"host {host['cpu_model']}, {cores} torch threads of {host['affinity_cores']} affinity cores"}
 
 
 def kernel_table(ktimer: dict) -> list:
@@ -229,7 +258,7 @@ def kernel_table(ktimer: dict) -> list:
     return rows
 
 
-def mappo_roofline(dom: dict) -> dict:
+def mappo_roofline(dom: dict, workload: str) -> dict:
     """The MAPPO leg's roofline object for its dominant matrix kernel: against the lower of its two roofs
     (the matrix ceiling of the instruction it issues, and its algorithmic intensity x the HBM peak).
     HBM-bound: achieved = algorithmic GB/s vs 8 TB/s; MFMA-bound: fp32-equivalent TF/s vs the ceiling.
@@ -246,15 +275,12 @@ def mappo_roofline(dom: dict) -> dict:
                             if ratio else None),
          "kernel_ms": dom["ms_avg"], "launches": dom["launches"],
          "algorithmic_bytes_per_launch": dom.get("algorithmic_bytes_avg"),
-         "mfma": {"achieved_tflops_fp32_equiv": dom["tflops_fp32_equiv"], "peak": dom["peak"], "frac": dom["frac"],
-                  "peak_basis": dom["peak_basis"]},
+         "mfma": {"achieved_tflops_fp32_equiv": dom["tflops_fp32_equiv"], "peak": dom["peak"], "frac": dom["frac"]},
          "hbm": {"achieved_GBps": dom["hbm_GBps"], "peak": HBM_PEAK_GBS, "frac": dom["hbm_frac"]},
          "intensity_flop_per_byte": dom.get("intensity_flop_per_byte"),
          "frac_of_attainable": dom.get("roofline_frac"),
-         "note": "dominant matrix kernel of the timed cycle; algorithmic fp32 FLOPs (2*R*3H*(H+Kx) per GRU call, "
-                 "2*M*N*K per GEMM) and algorithmic HBM bytes (operands once + results, GRU: x, h in, h' and the "
-                 "4H tape out) over its launches' summed duration (HIP events on the launch stream); rocprofv3 "
-                 "trace of the same leg, timed-cycle slice: profiles/r02y_mappo_uf100-430_slice.json"}
+         "note": f"dominant matrix kernel of the timed cycle, algorithmic FLOPs / bytes over its HIP-event time "
+                 f"(DESIGN.md §7); rocprof slice: profiles/*_mappo_{workload}_slice.json"}
     return r
 
 
@@ -317,15 +343,27 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
     kernels = kernel_table(GNNActorCritic.ktimer)
     GNNActorCritic.ktimer = None
     cycle_ms = sum(phases)
+    dom = next(k for k in kernels if k["peak"])  # the matrix kernel with the most time in the cycle
+    rank_ms = [0.0] * world  # each rank's dominant-kernel average launch time
+    rank_ms[rank] = dom["ms_avg"]
     if dist is not None:
         t = torch.tensor([elapsed] + phases, dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, phases = float(t[0]), [float(v) for v in t[1:]]
+        rk = torch.tensor(rank_ms, dtype=torch.float64, device="cuda")
+        dist.all_reduce(rk)  # every rank fills its own slot: SUM = gather
+        rank_ms = [float(v) for v in rk]
+    if type(comm).__name__ == "CapiComm":
+        comm.destroy()
     n_mb = B * T // cfg["MINIBATCH_SIZE"]
     gemm_tflops = flops / (elapsed * 1e12)
-    dom = next(k for k in kernels if k["peak"])  # the matrix kernel with the most time in the cycle
     for k in kernels:
         k["share_of_cycle"] = k["ms_total"] / cycle_ms
+    side = write_side_file(f"mappo_{workload}_n{world}_rank{rank}", {"workload": workload, "kernels": kernels})
+    roof = mappo_roofline(dom, workload)
+    roof["per_rank_kernel_ms"] = rank_ms
+    top = [{"kernel": k["kernel"], "share": round(k["share_of_cycle"], 4), "ms_avg": round(k["ms_avg"], 4)}
+           for k in kernels[:4]]
     return {
         "metric": "MAPPO updates/sec",
         "value": 1.0 / elapsed,
@@ -334,20 +372,34 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
         "adam_steps_per_s": E * n_mb / elapsed,
         "samples_per_s": world * B * T / elapsed,
         "ppo_samples_per_s": world * E * B * T / (phases[2] * 1e-3),
-        "phase_ms": dict(zip(("rollout", "gae", "ppo_update", "metrics"), phases)),
-        "config": {"workload": workload, "num_vars": V, "num_clauses": C, "num_agents": env.num_agents,
-                   "envs_per_gpu": B, "NUM_STEPS": T, "UPDATE_EPOCHS": E, "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"],
-                   "GNN_HIDDEN_DIM": H, "GNN_NUM_MESSAGE_PASSING_STEPS": L, "micro_batch": learner.micro,
+        "phase_ms": {k: round(v, 2) for k, v in zip(("rollout", "gae", "ppo_update", "metrics"), phases)},
+        "config": {"workload": workload, "num_agents": env.num_agents, "max_vars_per_agent": env.max_vars_per_agent,
+                   "envs_per_gpu": B, "global_envs": B * world, "NUM_STEPS": T, "UPDATE_EPOCHS": E,
+                   "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"], "H": H, "L": L, "micro_batch": learner.micro,
                    "parallelism": f"dp{world} (env shards; RCCL gradient all-reduce per minibatch"
                                   f"{', C-ABI communicator' if type(comm).__name__ == 'CapiComm' else ''})"},
-        "roofline": mappo_roofline(dom),
-        "kernels": kernels,
+        "top_kernels": top,
+        "kernels_file": side,
         "issued_gemm_tflops_over_cycle": gemm_tflops,
-        "dtype": "f32 (fp32 accumulate; fp16x2 split MFMAs for the dominant products, bf16x3 where fp16's range "
-                 "does not hold)",
+        "dtype": "f32 (fp32 accumulate; fp16x2 split MFMAs, bf16x3 where fp16's range does not hold)",
         "solve_rate": met["solve_rate"],
         "peak_hbm_gb": torch.cuda.max_memory_allocated() / 1e9,
+        "roofline": roof,
     }
+
+
+def write_side_file(name: str, obj) -> Optional[str]:
+    """Per-kernel tables go to a side file (MARLSAT_BENCH_SIDE_DIR, default gpurun_out/) so the one JSON
+    line stays short enough for the driver's tail to hold its MAPPO legs."""
+    d = os.environ.get("MARLSAT_BENCH_SIDE_DIR", os.path.join(ROOT, "gpurun_out"))
+    try:
+        os.makedirs(d, exist_ok=True)
+        p = os.path.join(d, f"bench_{name}.json")
+        with open(p, "w") as f:
+            json.dump(obj, f, indent=1)
+        return os.path.relpath(p, ROOT)
+    except OSError:
+        return None
 
 
 MIXED = ("uf50-218", "uf100-430", "uf200-860")  # BASELINE config 5 size classes (1024 envs per GPU of 8192)
@@ -437,10 +489,15 @@ def env_leg(args, rank, world, dist):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K  # mean launch duration on the kernel's stream
+    rank_ms = [0.0] * world
+    rank_ms[rank] = kern_ms
     if dist is not None:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+        rk = torch.tensor(rank_ms, dtype=torch.float64, device="cuda")
+        dist.all_reduce(rk)  # every rank fills its own slot: SUM = gather
+        rank_ms = [float(v) for v in rk]
     # sanity: the state stays consistent (cheap device checks, after timing)
     for e, st in zip(classes, states):
         assert torch.equal(e.num_clauses - st.clauses_satisfied_status.int().sum(1), st.num_unsatisfied)
@@ -459,13 +516,67 @@ def env_leg(args, rank, world, dist):
         per_class.append({"workload": name, "num_vars": e.num_vars, "num_clauses": e.num_clauses,
                           "num_agents": e.num_agents, "vars_per_agent": WORKLOADS[name][2], "envs_per_gpu": b,
                           "algorithmic_bytes_per_env_step": pe})
-    return {"names": names, "sizes": sizes, "elapsed": elapsed, "kern_ms": kern_ms, "K": K, "kernel": kernel,
+    return {"names": names, "sizes": sizes, "elapsed": elapsed, "kern_ms": kern_ms, "rank_ms": rank_ms, "K": K,
+            "kernel": kernel,
             "launch_bytes": launch_bytes, "per_class": per_class, "done_frac": done_frac, "resets": resets}
+
+
+def run_cpu_baselines(args) -> dict:
+    """The CPU legs, timed before anything touches the GPU (forked workers, torch CPU threads): the env
+    step restated (``cpu_baseline``) and the PPO minibatch forward + backward restated on the first MAPPO
+    leg's size (``mappo_cpu_baseline``)."""
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+
+    names = MIXED if args.workload == "mixed" else (args.workload,)
+    rates = []
+    for name in names:
+        V, C, vpa, _, size_id = WORKLOADS[name]
+        pnp = generate_problem_pool(V, C, min(256, args.pool), size_id=size_id)
+        rates.append(cpu_baseline(V, C, vpa, pnp, budget_s=args.cpu_budget / len(names)))
+    cpu = rates[0]
+    if len(rates) > 1:  # time to step one env of each class in the workload's proportions
+        tot = args.envs or 1024
+        sz = [tot // 3 + (1 if i < tot % 3 else 0) for i in range(3)]
+        cpu = dict(rates[0], value=sum(sz) / sum(b / r["value"] for b, r in zip(sz, rates)),
+                   sample=" | ".join(r["sample"] for r in rates))
+    out = {"env": cpu, "mappo": None}
+    legs = [s for s in args.mappo.split(",") if s]
+    if legs:
+        out["mappo"] = mappo_cpu_baseline(legs[0].split(":")[0], budget_s=min(10.0, args.cpu_budget))
+    return out
+
+
+def launch_ranks(args) -> int:
+    """``bench.py --gpus N`` (N > 1) started without torchrun: time the CPU baselines here, then run N
+    ranks as a fresh child ``python -m torch.distributed.run`` (one process per GPU, RCCL) and return its
+    exit code.  This process never initialises the GPU (no exec from a GPU process; the child is a new
+    process tree)."""
+    import tempfile
+
+    env = dict(os.environ)
+    if args.cpu_budget > 0:
+        base = run_cpu_baselines(args)
+        fd, path = tempfile.mkstemp(prefix="marlsat_cpu_", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            json.dump(base, f)
+        env["MARLSAT_BENCH_CPU_JSON"] = path
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    try:
+        return subprocess.call(cmd, env=env)
+    finally:
+        if "MARLSAT_BENCH_CPU_JSON" in env:
+            os.unlink(env["MARLSAT_BENCH_CPU_JSON"])
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU; N > 1 without torchrun's env starts an N-rank torchrun child")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="uf200-860", choices=sorted(WORKLOADS) + ["mixed"],
@@ -474,32 +585,30 @@ def main():
     ap.add_argument("--pool", type=int, default=1024, help="problem instances in the pool")
     ap.add_argument("--obs-dtype", default="int32", choices=["int32", "int8"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline per core (0: skip)")
-    ap.add_argument("--mappo", default="uf100-430:4096:8,uf50-218:1024:32",
+    ap.add_argument("--mappo", default="uf100-430:4096:8,uf200-860:4096:2",
                     help="MAPPO legs 'workload:envs_per_gpu:NUM_STEPS,...' ('' skips); the first is the headline "
-                         "(the metric's 4096 envs, BASELINE config 3), the others are reported beside it")
+                         "'mappo' (BASELINE config 3, the metric's 4096 envs), the others are 'mappo_other_legs' "
+                         "(config 4: uf200-860, 25 agents, 4096 envs per GPU)")
     ap.add_argument("--mappo-micro-gb", type=float, default=240.0, help="activation budget per PPO micro-batch")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
 
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
-        from marlsat.utils.generate_cnf_dataset import generate_problem_pool
-
-        names = MIXED if args.workload == "mixed" else (args.workload,)
-        rates = []
-        for name in names:  # forked before any GPU initialisation
-            V, C, vpa, _, size_id = WORKLOADS[name]
-            pnp = generate_problem_pool(V, C, min(256, args.pool), size_id=size_id)
-            rates.append(cpu_baseline(V, C, vpa, pnp, budget_s=args.cpu_budget / len(names)))
-        cpu = rates[0]
-        if len(rates) > 1:  # time to step one env of each class in the workload's proportions
-            tot = args.envs or 1024
-            sz = [tot // 3 + (1 if i < tot % 3 else 0) for i in range(3)]
-            cpu = dict(rates[0], value=sum(sz) / sum(b / r["value"] for b, r in zip(sz, rates)),
-                       sample=" | ".join(r["sample"] for r in rates))
+    base = None
+    if rank == 0 and args.cpu_budget > 0:
+        path = os.environ.get("MARLSAT_BENCH_CPU_JSON")
+        if path:  # timed by the launching parent (launch_ranks) before the ranks started
+            with open(path) as f:
+                base = json.load(f)
+        else:  # forked before any GPU initialisation
+            base = run_cpu_baselines(args)
 
     import torch
 
@@ -509,6 +618,7 @@ def main():
     dev_idx = local_rank % torch.cuda.device_count() if share else local_rank
     torch.cuda.set_device(dev_idx)
     dist = None
+    backend = None
     if world > 1:
         import torch.distributed as dist
 
@@ -517,6 +627,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {dist.get_world_size()} ranks")
 
     r = env_leg(args, rank, world, dist)
     legs = []
@@ -524,9 +636,6 @@ def main():
         wl, envs, T = spec.split(":")
         legs.append(mappo_bench(args, rank, world, dist, wl, int(envs), int(T)))
     mappo = legs[0] if legs else None
-    if mappo is not None and rank == 0 and world == 1 and args.cpu_budget > 0:
-        wl0 = mappo["config"]["workload"]
-        mappo["cpu_baseline"] = mappo_cpu_baseline(wl0, budget_s=min(10.0, args.cpu_budget))
 
     if rank == 0:
         B, K, elapsed, kern_ms = sum(r["sizes"]), r["K"], r["elapsed"], r["kern_ms"]
@@ -552,6 +661,8 @@ def main():
             "value": B * K * world / elapsed,
             "unit": "env-steps/s",
             "n_gpus": world,
+            "rccl_ranks": dist.get_world_size() if dist is not None else 1,
+            "dist_backend": backend,
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": elapsed / K * 1e3,
@@ -562,6 +673,11 @@ def main():
             "data": "synthetic (planted-solution random 3-SAT from the reference generator algorithm, "
                     f"seed=1000*size_id+i (size_id {sids}), pool {args.pool}; random valid mode-0 actions)",
             "config": cfg,
+            "cpu_baseline": base["env"] if base else None,
+            "mappo_cpu_baseline": base["mappo"] if base else None,
+            "done_fraction_last_step": r["done_frac"],
+            "auto_resets_in_timed_region": r["resets"],
+            "steady_state": "episode-step counters staggered uniformly over [0, 512) before warm-up",
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -571,16 +687,14 @@ def main():
                 "traffic": traffic,
                 "kernel": r["kernel"],
                 "kernel_ms": kern_ms,
+                "per_rank_kernel_ms": r["rank_ms"],
                 "algorithmic_bytes_per_env_step": per_env,
                 "algorithmic_bytes_per_launch": r["launch_bytes"],
                 "traffic_source": traffic_src,
             },
-            "cpu_baseline": cpu,
-            "mappo": mappo,
+            # the MAPPO legs close the line, so the driver's tail of stdout holds them
             "mappo_other_legs": legs[1:],
-            "done_fraction_last_step": r["done_frac"],
-            "auto_resets_in_timed_region": r["resets"],
-            "steady_state": "episode-step counters staggered uniformly over [0, 512) before warm-up",
+            "mappo": mappo,
         }
         print(json.dumps(rec), flush=True)
     if dist is not None:

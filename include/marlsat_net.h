@@ -279,7 +279,8 @@ int msat_gather_rows(const int32_t *idx, int32_t S, int32_t nfields, const void 
                      const int32_t *row_bytes, void *stream);
 /* Row bases of a graph batch (learner:148-195 batch assembly): per sample s of instance inst[s],
  * bases[s] = exclusive prefix sums of the instances' (var rows, clause rows, incidences) counts
- * nv / nc / ne, totals[3] = their sums (the batch's Nv, Nc, nnz). */
+ * nv / nc / ne, totals[3] = their sums (the batch's Nv, Nc, nnz), or -1 for a sum above INT32_MAX
+ * (the batch cannot be indexed in int32; the caller must split it). */
 int msat_graph_bases(int32_t S, const int32_t *inst, const int32_t *nv, const int32_t *nc, const int32_t *ne,
                      int32_t *bases, int32_t *totals, void *stream);
 /* fp64 cycle sums over N transitions (learner:661-719): out[9] = sum reward, sum done, sum solved&done,

@@ -461,7 +461,11 @@ constexpr size_t kWgradFlagBytes = 1024 * sizeof(int);  // >= 256 workgroups' fl
 extern "C" size_t msat_gemm_wgrad_workspace_bytes(int32_t M, int32_t K, int32_t N) {
     const size_t sp = std::max({wgrad_splits(M, K, N), K <= kSkinnyK ? skinny_splits(M, N) : 0,
                                 msat_wgrad_x3w_splits(M, K)});
-    return sp * K * N * sizeof(float) + kWgradFlagBytes;  // + the fp16x2 kernel's workgroup flags
+    size_t floats = sp * K * N;
+    // msat_gemm_wgrad_rot's tiled fallback runs two narrower products (N - rot and rot columns) in the
+    // same workspace, and narrower products take more splits: size for the widest need of any width
+    for (int n = 1; n < N; ++n) floats = std::max(floats, (size_t)wgrad_splits(M, K, n) * K * n);
+    return floats * sizeof(float) + kWgradFlagBytes;  // + the fp16x2 kernel's workgroup flags
 }
 
 static int wgrad_reduce(const float *part, int splits, int K, int N, float *W, int ldw, int accumulate, hipStream_t s) {

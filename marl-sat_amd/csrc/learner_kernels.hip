@@ -121,7 +121,8 @@ __global__ void __launch_bounds__(kMetT) cycle_metrics_kernel(int N, const float
 // ---------------------------------------------------------------------------------------------
 // Row bases of a graph batch: for samples s < S of instances inst[s], with per-instance row counts
 // (var rows, clause rows, incidences) nv[i], nc[i], ne[i], bases[s] = exclusive prefix sums (S, 3) and
-// totals[3] = the sums.  One workgroup (the batch is at most a few ten thousand samples): each thread
+// totals[3] = the sums, or -1 for a sum above INT32_MAX (the batch's int32 row indices would wrap;
+// the caller refuses the batch).  One workgroup (the batch is at most a few ten thousand samples): each thread
 // sums a contiguous chunk, the chunk sums are scanned in LDS, then every chunk is re-walked.
 constexpr int kScanT = 1024;
 
@@ -166,7 +167,7 @@ __global__ void __launch_bounds__(kScanT) graph_bases_kernel(int S, const int32_
     }
     if (t == kScanT - 1) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) totals[q] = (int32_t)min(sc[q][t], (long long)INT32_MAX);
+        for (int q = 0; q < 3; ++q) totals[q] = sc[q][t] > (long long)INT32_MAX ? -1 : (int32_t)sc[q][t];
     }
 }
 

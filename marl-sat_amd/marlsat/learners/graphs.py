@@ -186,6 +186,9 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
     _lib.check(_lib.lib.msat_graph_bases(S, inst.data_ptr(), tv.data_ptr(), tc.data_ptr(), te.data_ptr(), sb.data_ptr(),
                                          tot.data_ptr(), _lib.stream_ptr(dev)), "msat_graph_bases")
     Nv, Nc, nnz = tot.tolist()  # sizes the outputs (one small device -> host read)
+    if min(Nv, Nc, nnz) < 0:  # msat_graph_bases flags a total above INT32_MAX with -1
+        raise ValueError(f"graph batch of {S} samples exceeds int32 row indices (var rows, clause rows, incidences "
+                         f"= {Nv}, {Nc}, {nnz}; -1 = overflow): use smaller micro-batches")
     out = GraphBatch(S, G, Nv, Nc, nnz,
                      torch.empty((Nv, 8), dtype=torch.float32, device=dev),
                      torch.empty((Nc, 3), dtype=torch.float32, device=dev),

@@ -325,10 +325,14 @@ class MAPPOLearner:
                     self.trace.append({"idx": idx.cpu(), "params": net.params.clone(),
                                        "grads": net.grads.clone() * scale, "lr": lr})
                 net.adam_step(lr, grad_scale=scale)
-        # per-minibatch means: (value_loss, loss_actor, entropy)
-        losses[..., 0] /= MB
-        losses[..., 1] /= MB * A
-        losses[..., 2] /= n_ent
+        # per-minibatch means over the UNION minibatch (learner:708-719 reports each minibatch's loss
+        # triple over the whole minibatch): the row sums of every rank are added once per cycle, then
+        # divided by the union's row counts (every rank's slice has MB rows)
+        allreduce_sums(losses, self.dist)
+        w = self.world
+        losses[..., 0] /= MB * w
+        losses[..., 1] /= MB * A * w
+        losses[..., 2] /= n_ent * w
         return losses, ent
 
     # ------------------------------------------------------------ metrics ----

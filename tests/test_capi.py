@@ -132,3 +132,17 @@ def test_collective_entry_points_reject_bad_arguments():
     assert L.msat_allreduce_sum(None, None, 4, 0, None) == -1
     assert b"communicator" in L.msat_last_error()
     assert L.msat_comm_destroy(None) == 0
+
+
+def test_library_does_not_link_rccl():
+    """RCCL is opened lazily by msat_comm_* (comm.hip): a host that only steps environments loads
+    libmarlsat.so without librccl installed."""
+    import shutil
+    import subprocess
+
+    if shutil.which("readelf") is None:
+        pytest.skip("readelf not available")
+    lib = os.path.join(ROOT, "marl-sat_amd", "marlsat", "lib", "libmarlsat.so")
+    out = subprocess.run(["readelf", "-d", lib], capture_output=True, text=True, check=True).stdout
+    needed = [l for l in out.splitlines() if "(NEEDED)" in l]
+    assert needed and not any("rccl" in l for l in needed), needed

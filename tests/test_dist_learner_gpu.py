@@ -14,8 +14,8 @@ of the two ranks' minibatch rows from the sharded run's own parameters.  Checks:
     elementwise 1e-5 relative + 4x the tensor's fp32 reduction-order noise (the union gradient
     summed in one vs two micro-batches; the forward of a sample is row-local, so summation
     order is the only difference);
-  * the sharded loss triple of every minibatch equals the union minibatch's (rank mean of
-    equal-size means), 1e-5 relative.
+  * the loss triple every rank REPORTS for each minibatch (MAPPOLearner.metrics' arrays) is the
+    union minibatch's, identical on both ranks, 1e-5 relative to the union run.
 """
 import os
 import socket
@@ -65,7 +65,10 @@ def test_two_rank_learner_equals_union(tmp_path):
     # the other branch of min(r A, clip(r) A) and move a whole sample's actor gradient
     learner.adv.copy_(cat("adv").to(learner.adv.device))
     learner.targets.copy_(cat("targets").to(learner.targets.device))
-    losses_sharded = 0.5 * (ranks[0]["losses"] + ranks[1]["losses"])  # each (E, n_mb, 3) of equal-size means
+    # the learner reports rank-global losses (learner:708-719): every rank holds the union minibatch's
+    # triple itself, identical on both ranks (one all-reduce of the row sums per cycle)
+    assert torch.equal(ranks[0]["losses"], ranks[1]["losses"])
+    losses_sharded = ranks[0]["losses"]
     for s, rec in enumerate(ranks[0]["trace"]):
         rows = []
         for k in range(2):

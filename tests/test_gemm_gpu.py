@@ -122,21 +122,28 @@ def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
         _ref_close(W, ref, absprod)
 
 
-@pytest.mark.parametrize("path", ["x3w", "x3"])
+@pytest.mark.parametrize("path", ["x3w", "x3", "fp32"])
 @pytest.mark.parametrize("M,K,N,rot,ldg", [(5000, 128, 384, 256, 512), (70001, 256, 384, 256, 512), (999, 128, 128, 32, 128),
-                                           (300, 256, 384, 128, 384)])
+                                           (300, 256, 384, 128, 384), (700001, 64, 192, 128, 192)])
 def test_wgrad_rot(M, K, N, rot, ldg, path, monkeypatch):
     """msat_gemm_wgrad_rot: W[:, (n + rot) % N] (+)= (A^T G)[:, n] (the packed GRU backward rows), on the
-    whole-row kernel's rotated store and on the two-range fallback; G read from a wider row (ld > N)."""
+    whole-row kernel's rotated store and on the two-range fallback (bf16x3 tiles, or fp32 MFMA tiles with
+    MARLSAT_WGRAD_X3=0); G read from a wider row (ld > N).  The H = 64, 700 K-row case: the fallback's
+    128-column sub-product takes more row splits than the full width, and the workspace
+    (msat_gemm_wgrad_workspace_bytes) must hold them."""
     from marlsat import _lib
 
+    if path == "fp32" and M < 700001:
+        pytest.skip("the fp32 fallback is covered by the large-M case")
     monkeypatch.setenv("MARLSAT_WGRAD_W", "1" if path == "x3w" else "0")
+    monkeypatch.setenv("MARLSAT_WGRAD_X3", "0" if path == "fp32" else "1")
     g = torch.Generator(device="cuda").manual_seed(M + K + N + rot)
     A = torch.randn(M, K, device="cuda", generator=g)
     Gw = torch.randn(M, ldg, device="cuda", generator=g)
     G = Gw[:, :N]
     W0 = torch.randn(K, N, device="cuda", generator=g)
-    ws = torch.empty(int(_lib.lib.msat_gemm_wgrad_workspace_bytes(M, K, N)) // 4 + 1, device="cuda")
+    nws = int(_lib.lib.msat_gemm_wgrad_workspace_bytes(M, K, N)) // 4 + 1
+    ws = torch.full((nws + (1 << 20),), 7.0, device="cuda")  # + a canary tail that must stay untouched
     for acc in (0, 1):
         W = W0.clone()
         _lib.check(_lib.lib.msat_gemm_wgrad_rot(A.data_ptr(), K, Gw.data_ptr(), ldg, W.data_ptr(), N, M, K, N, rot, acc,
@@ -144,6 +151,7 @@ def test_wgrad_rot(M, K, N, rot, ldg, path, monkeypatch):
         ref = torch.roll(A.double().t() @ G.double(), rot, dims=1) + (W0.double() if acc else 0)
         absprod = torch.roll(A.double().abs().t() @ G.double().abs(), rot, dims=1) + (W0.double().abs() if acc else 0)
         _ref_close(W, ref, absprod)
+        assert bool((ws[nws:] == 7.0).all()), "wgrad_rot wrote past its workspace"
 
 
 def row_exp(G: torch.Tensor) -> torch.Tensor:

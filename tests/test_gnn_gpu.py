@@ -142,12 +142,30 @@ def _close_yard(dev, ref, yard, factor, what, report, kink=None):
     assert (err <= bound).all(), f"{what}: max err {err.max():.3g}, worst ratio {(err / bound).max():.3g}"
 
 
-@pytest.mark.parametrize("path", ["default", "fp32"])
+def _set_path(monkeypatch, path):
+    """'default': the bench's kernels (phi folded, fp16x2 GRU forward / data / weight gradients with
+    dual launches); 'bf16x3': phi folded, the four fp16x2 switches off (the bf16x3 register-A GRU
+    forward, bf16x3 data and weight gradients: the fallback wherever fp16's range fails); 'fp32': the
+    reference operation order on fp32 MFMA kernels."""
+    from marlsat.learners.gnn import GNNActorCritic
+
+    fast = path != "fp32"
+    monkeypatch.setattr(GNNActorCritic, "fuse_phi", fast)
+    monkeypatch.setattr(GNNActorCritic, "use_x3", fast)
+    monkeypatch.setattr(GNNActorCritic, "use_gru_x3", fast)
+    monkeypatch.setattr(GNNActorCritic, "use_gru_x3r", fast)
+    h2 = path == "default"
+    for sw in ("use_gru_h2", "use_dgrad_h2", "use_wgrad_h2", "use_dual"):
+        monkeypatch.setattr(GNNActorCritic, sw, h2)
+
+
+@pytest.mark.parametrize("path", ["default", "bf16x3", "fp32"])
 @pytest.mark.parametrize("V,C,vpa,H,L,S,mode", DEPTH_CASES)
 def test_depth16_matches_oracle(V, C, vpa, H, L, S, mode, path, monkeypatch):
     """The reference's depth L = 16 at H = 128 on uf50 / uf100 / mode 1, on the kernels the bench
-    runs ("default": phi folded, register-A bf16x3 GRU forward, bf16x3 data gradients) and on the
-    reference-order fp32 path, against the float64 oracle.
+    runs ("default": phi folded, fp16x2 GRU forward and data / weight gradients, dual launches), on
+    the bf16x3 path those kernels fall back to, and on the reference-order fp32 path, against the
+    float64 oracle.
 
     Bar: normwise 1e-5 (max |err| <= 1e-5 max |ref| per tensor) AND elementwise
     |err| <= 1e-5 |ref| + atol, atol = 4x (forward) / 8x (gradients) the largest error of the same
@@ -158,13 +176,24 @@ def test_depth16_matches_oracle(V, C, vpa, H, L, S, mode, path, monkeypatch):
     within 3e-5 (relative) of 0 may land on either side in fp32, and the two sides' gradients
     differ by a whole term (tests/probe_head_bisect.py: one flipped flip-head unit moved its bias
     gradient by 5e-3)."""
-    from marlsat.learners.gnn import GNNActorCritic
+    _set_path(monkeypatch, path)
+    _depth_check(V, C, vpa, H, L, S, mode, path)
 
-    fuse, x3 = (True, True) if path == "default" else (False, False)
-    monkeypatch.setattr(GNNActorCritic, "fuse_phi", fuse)
-    monkeypatch.setattr(GNNActorCritic, "use_x3", x3)
-    monkeypatch.setattr(GNNActorCritic, "use_gru_x3", x3)
-    monkeypatch.setattr(GNNActorCritic, "use_gru_x3r", x3)
+
+# BASELINE config 4's network: uf200-860, VARS_PER_AGENT 8 -> 25 agents of m = 8, one sample (the
+# float64 oracle runs 25 dense masked per-agent encoders of 200 x 860 at the reference depth)
+UF200_CASE = (200, 860, 8, 128, 16, 1, 0)
+
+
+@pytest.mark.parametrize("path", ["default", "fp32"])
+def test_uf200_network_matches_oracle(path, monkeypatch):
+    """Config 4 (uf200, A = 25, m = 8) at H = 128, L = 16 against the float64 oracle, same bar as
+    test_depth16_matches_oracle."""
+    _set_path(monkeypatch, path)
+    _depth_check(*UF200_CASE, path)
+
+
+def _depth_check(V, C, vpa, H, L, S, mode, path):
     net, b, P, batch, av, am, A, M = _setup(V, C, vpa, H, L, S, mode, seed=11)
     args = (batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"])
     onet.RELU_LOG = log = []

@@ -105,3 +105,19 @@ def test_graph_bases_match_cumsum(S):
     ref = np.cumsum(per, 0) - per
     assert np.array_equal(bases.cpu().numpy()[:S], ref)
     assert np.array_equal(tot.cpu().numpy(), per.sum(0))
+
+
+def test_graph_bases_flag_int32_overflow():
+    """A batch whose var-row total passes INT32_MAX gets the total -1 (not a clamped or wrapped
+    count), and assemble-side callers refuse it."""
+    from marlsat import _lib
+
+    S = 3000
+    counts = [np.full(2, 1_000_000, np.int32), np.full(2, 5, np.int32), np.full(2, 7, np.int32)]
+    dc = [torch.from_numpy(c).cuda() for c in counts]
+    di = torch.zeros(S, dtype=torch.int32, device="cuda")
+    bases = torch.empty((S, 3), dtype=torch.int32, device="cuda")
+    tot = torch.empty(3, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.msat_graph_bases(S, di.data_ptr(), *[c.data_ptr() for c in dc], bases.data_ptr(),
+                                         tot.data_ptr(), _lib.stream_ptr()), "graph_bases")
+    assert tot.cpu().tolist() == [-1, 5 * S, 7 * S]
