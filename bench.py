@@ -359,12 +359,9 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
     gemm_tflops = flops / (elapsed * 1e12)
     for k in kernels:
         k["share_of_cycle"] = k["ms_total"] / cycle_ms
-    side = write_side_file(f"mappo_{workload}_n{world}_rank{rank}", {"workload": workload, "kernels": kernels})
     roof = mappo_roofline(dom, workload)
     roof["per_rank_kernel_ms"] = rank_ms
-    top = [{"kernel": k["kernel"], "share": round(k["share_of_cycle"], 4), "ms_avg": round(k["ms_avg"], 4)}
-           for k in kernels[:4]]
-    return {
+    full = {
         "metric": "MAPPO updates/sec",
         "value": 1.0 / elapsed,
         "unit": "updates/s",
@@ -372,19 +369,48 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
         "adam_steps_per_s": E * n_mb / elapsed,
         "samples_per_s": world * B * T / elapsed,
         "ppo_samples_per_s": world * E * B * T / (phases[2] * 1e-3),
-        "phase_ms": {k: round(v, 2) for k, v in zip(("rollout", "gae", "ppo_update", "metrics"), phases)},
+        "phase_ms": dict(zip(("rollout", "gae", "ppo_update", "metrics"), phases)),
         "config": {"workload": workload, "num_agents": env.num_agents, "max_vars_per_agent": env.max_vars_per_agent,
                    "envs_per_gpu": B, "global_envs": B * world, "NUM_STEPS": T, "UPDATE_EPOCHS": E,
-                   "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"], "H": H, "L": L, "micro_batch": learner.micro,
+                   "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"], "GNN_HIDDEN_DIM": H, "GNN_NUM_MESSAGE_PASSING_STEPS": L,
+                   "micro_batch": learner.micro,
                    "parallelism": f"dp{world} (env shards; RCCL gradient all-reduce per minibatch"
                                   f"{', C-ABI communicator' if type(comm).__name__ == 'CapiComm' else ''})"},
-        "top_kernels": top,
-        "kernels_file": side,
+        "roofline": roof,
+        "kernels": kernels,
         "issued_gemm_tflops_over_cycle": gemm_tflops,
         "dtype": "f32 (fp32 accumulate; fp16x2 split MFMAs, bf16x3 where fp16's range does not hold)",
         "solve_rate": met["solve_rate"],
         "peak_hbm_gb": torch.cuda.max_memory_allocated() / 1e9,
-        "roofline": roof,
+    }
+    side = write_side_file(f"mappo_{workload}_n{world}_rank{rank}", full)
+    return compact_leg(full, side)
+
+
+def _sig(x, n=4):
+    return float(f"{x:.{n}g}") if isinstance(x, float) else x
+
+
+def compact_leg(full: dict, side: Optional[str]) -> dict:
+    """The MAPPO leg as it goes into the JSON line: ~0.8 KB, so both legs fit the driver's 2,000-character
+    tail of stdout.  The full record (per-kernel table, both roofline views) is in the side file."""
+    c, r = full["config"], full["roofline"]
+    return {
+        "metric": full["metric"], "value": _sig(full["value"]), "unit": full["unit"],
+        "s_per_update": _sig(full["s_per_update"]), "samples_per_s": _sig(full["samples_per_s"]),
+        "adam_steps_per_s": _sig(full["adam_steps_per_s"]),
+        "phase_ms": {k: round(v, 1) for k, v in full["phase_ms"].items()},
+        "config": {"workload": c["workload"], "agents": c["num_agents"], "m": c["max_vars_per_agent"],
+                   "envs_per_gpu": c["envs_per_gpu"], "T": c["NUM_STEPS"], "epochs": c["UPDATE_EPOCHS"],
+                   "minibatch": c["MINIBATCH_SIZE"], "H": c["GNN_HIDDEN_DIM"], "L": c["GNN_NUM_MESSAGE_PASSING_STEPS"],
+                   "parallelism": c["parallelism"].split(" ")[0]},
+        "roofline": {"bound": r["bound"], "achieved": _sig(r["achieved"]), "peak": r["peak"],
+                     "unit": r["unit"].split(" ")[0], "frac": _sig(r["frac"], 3),
+                     "traffic": _sig(r["traffic"]) if r["traffic"] else None,
+                     "kernel": r["kernel"].split(" ")[0], "kernel_ms": _sig(r["kernel_ms"]),
+                     "mfma_frac": _sig(r["mfma"]["frac"], 3),
+                     "per_rank_kernel_ms": [_sig(v) for v in r["per_rank_kernel_ms"]]},
+        "detail": side,
     }
 
 

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <stdlib.h>
 
+#include <cstring>
+
 #include "common.h"
 
 namespace msat {
@@ -353,19 +355,13 @@ static int skinny_splits(int M, int N) {
 }
 
 static bool skinny_ok(const float *G, int ldg, const float *W, int ldw, int K, int N) {
-    const char *e = getenv("MARLSAT_WGRAD_SKINNY");  // 0: MFMA tiles for every K (A/B measurements)
-    if (e && e[0] == '0') return false;
     return K <= kSkinnyK && N % 4 == 0 && ldg % 4 == 0 && ldw % 4 == 0 &&
            (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0;
 }
 
-// at most 768 workgroups (3 per CU: the x3 weight gradient's occupancy), >= ~1024 rows per split;
-// MARLSAT_WGRAD_WG overrides the workgroup budget (A/B measurements)
+// at most 768 workgroups (3 per CU: the x3 weight gradient's occupancy), >= ~1024 rows per split
 static int wgrad_splits(int M, int K, int N) {
-    static const int budget = [] {
-        const char *e = getenv("MARLSAT_WGRAD_WG");
-        return e ? std::max(1, atoi(e)) : 768;
-    }();
+    constexpr int budget = 768;
     const int tiles = ((K + kTM - 1) / kTM) * ((N + kTN - 1) / kTN);
     return std::max(1, std::min(budget / std::max(tiles, 1), (M + 1023) / 1024));
 }
@@ -374,7 +370,7 @@ static int wgrad_splits(int M, int K, int N) {
 
 using namespace msat;
 
-// LDS-DMA fast path (gemm2.hip); MARLSAT_GEMM=1 forces the register-staged kernels (A/B tests).
+// LDS-DMA fast path (gemm2.hip); the register-staged kernels here take the shapes it cannot.
 bool msat_gemm2_ok(const float *A, int lda, const float *B, int ldb, int transB, int N, int K);
 int msat_gemm2_launch(const float *A, int lda, const float *B, int ldb, int transB, float *C, int ldc,
                       const float *bias, int M, int N, int K, int accumulate, hipStream_t s);
@@ -393,18 +389,14 @@ int msat_wgrad_h2w_launch(const float *A, int lda, const float *G, int ldg, cons
 int msat_wgrad_x3_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
                          int rows_per_split, hipStream_t s);
 
-// MARLSAT_WGRAD_X3=0 keeps the fp32-MFMA weight gradient (A/B measurements)
+// MARLSAT_PRECISION=fp32 (the accuracy reference path, README) keeps the weight gradients on fp32
+// MFMA; otherwise they run on the fp32-accurate bf16x3 split.  Read per call.
 static bool wgrad_x3() {
-    const char *e = getenv("MARLSAT_WGRAD_X3");
-    return !(e && e[0] == '0');
+    const char *e = getenv("MARLSAT_PRECISION");
+    return !(e && std::strcmp(e, "fp32") == 0);
 }
 int msat_wgrad2_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
                        int rows_per_split, hipStream_t s);
-
-static bool legacy_gemm() {
-    const char *e = getenv("MARLSAT_GEMM");
-    return e && e[0] == '1';
-}
 
 // Small fp32 products accumulated in fp64 and rounded once (gnn.py phi folding: F = W Wi and its
 // unfolding dW = dF Wi^T, dWi = W^T dF).  F multiplies every row of every message step, so a
@@ -445,11 +437,8 @@ extern "C" int msat_gemm(const float *A, int32_t lda, const float *B, int32_t ld
     MSAT_REQUIRE(M >= 0 && N >= 1 && K >= 0, "bad dims M=%d N=%d K=%d", M, N, K);
     MSAT_REQUIRE(lda >= K && ldc >= N && ldb >= (transB ? K : N), "leading dims too small");
     if (M == 0) return MSAT_OK;
-    if (!legacy_gemm() && msat_gemm2_ok(A, lda, B, ldb, transB, N, K)) {
-        const char *e = getenv("MARLSAT_GEMM");
-        const int acc = (e && e[0] == '2') ? 2 : accumulate;  // 2: store-less diagnostic
-        return msat_gemm2_launch(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, acc, (hipStream_t)stream);
-    }
+    if (msat_gemm2_ok(A, lda, B, ldb, transB, N, K))
+        return msat_gemm2_launch(A, lda, B, ldb, transB, C, ldc, bias, M, N, K, accumulate, (hipStream_t)stream);
     dim3 grid((M + kTM - 1) / kTM, (N + kTN - 1) / kTN);
     hipLaunchKernelGGL(gemm_kernel, grid, dim3(kGT), 0, (hipStream_t)stream, A, lda, B, ldb, transB, C, ldc, bias, M,
                        N, K, accumulate);
@@ -486,13 +475,13 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
     MSAT_REQUIRE(A && G && W && workspace, "NULL operand");
     MSAT_REQUIRE(M >= 0 && K >= 1 && N >= 1 && lda >= K && ldg >= N && ldw >= N, "bad dims");
     hipStream_t s = (hipStream_t)stream;
-    if (!legacy_gemm() && wgrad_x3() && K > kSkinnyK && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
+    if (wgrad_x3() && K > kSkinnyK && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
         const int splits = msat_wgrad_x3w_splits(M, K);
         const int rc = msat_wgrad_x3w_launch(A, lda, G, ldg, (float *)workspace, M, K, N, 0, splits, s);
         if (rc) return rc;
         return wgrad_reduce((const float *)workspace, splits, K, N, W, ldw, accumulate, s);
     }
-    if (!legacy_gemm() && skinny_ok(G, ldg, W, ldw, K, N) && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0) {
+    if (skinny_ok(G, ldg, W, ldw, K, N) && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0) {
         const int sp = skinny_splits(M, N), rows_per = (M + sp - 1) / sp, N4 = N / 4;
         float4 *ws4 = reinterpret_cast<float4 *>(workspace);
         const bool av = lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
@@ -511,10 +500,10 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
     const int splits = wgrad_splits(M, K, N);
     const int rows = (M + splits - 1) / splits;
     int rc;
-    if (!legacy_gemm() && wgrad_x3() && msat_wgrad_x3_ok(A, lda, G, ldg, K, N)) {
+    if (wgrad_x3() && msat_wgrad_x3_ok(A, lda, G, ldg, K, N)) {
         const int rows16 = ((rows + 15) / 16) * 16;
         rc = msat_wgrad_x3_launch(A, lda, G, ldg, (float *)workspace, M, K, N, splits, rows16, s);
-    } else if (!legacy_gemm() && msat_wgrad2_ok(A, lda, G, ldg, K, N)) {
+    } else if (msat_wgrad2_ok(A, lda, G, ldg, K, N)) {
         const int rows32 = ((rows + 31) / 32) * 32;
         rc = msat_wgrad2_launch(A, lda, G, ldg, (float *)workspace, M, K, N, splits, rows32, s);
     } else {
@@ -539,7 +528,7 @@ extern "C" int msat_gemm_wgrad_rot(const float *A, int32_t lda, const float *G, 
     MSAT_REQUIRE(A && G && W && workspace, "NULL operand");
     MSAT_REQUIRE(M >= 0 && K >= 1 && N >= 1 && lda >= K && ldg >= N && ldw >= N, "bad dims");
     hipStream_t s = (hipStream_t)stream;
-    if (!legacy_gemm() && wgrad_x3() && K > kSkinnyK && rot % 4 == 0 && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
+    if (wgrad_x3() && K > kSkinnyK && rot % 4 == 0 && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
         const int splits = msat_wgrad_x3w_splits(M, K);
         const int rc = msat_wgrad_x3w_launch(A, lda, G, ldg, (float *)workspace, M, K, N, rot, splits, s);
         if (rc) return rc;

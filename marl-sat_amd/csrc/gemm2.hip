@@ -206,10 +206,6 @@ gemm2_kernel(const float *__restrict__ A, int lda, const float *__restrict__ B, 
                 v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
                 if (row < M && col < N) {
                     float4 *c = reinterpret_cast<float4 *>(C + (size_t)row * ldc + col);
-                    if (accumulate == 2) {  // diagnostic (MARLSAT_GEMM=2): no store unless NaN
-                        if (v.x != v.x) *c = v;
-                        continue;
-                    }
                     if (accumulate) {
                         const float4 o = *c;
                         v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
@@ -309,17 +305,8 @@ static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 using namespace msat;
 
 // Fast-path predicates and launches (called from gemm.hip's C-ABI entry points).
-// MARLSAT_GEMM_D selects the slab depth (16 or 32; default 16: 32 KiB LDS, 3 workgroups per CU).
-static int slab_depth() {
-    const char *e = getenv("MARLSAT_GEMM_D");
-    return (e && atoi(e) == 32) ? 32 : 16;
-}
-
-// MARLSAT_GEMM_STAGES selects the GEMM pipeline depth (2: double buffer; 3: two slabs in flight).
-static int gemm_stages() {
-    const char *e = getenv("MARLSAT_GEMM_STAGES");
-    return (e && atoi(e) == 3) ? 3 : 2;
-}
+// Slab depth 16 (32 KiB LDS, 3 workgroups per CU) and a double buffer: depth 32 and a third stage
+// measured equal or slower in round 1.
 
 bool msat_gemm2_ok(const float *A, int lda, const float *B, int ldb, int transB, int N, int K) {
     if (K % 32 || K == 0 || lda % 4 || ldb % 4 || !al16(A) || !al16(B)) return false;
@@ -333,19 +320,12 @@ int msat_gemm2_launch(const float *A, int lda, const float *B, int ldb, int tran
     const dim3 grid(ntm * ntn), blk(kG2T);
     // float4 epilogue when whole 16-byte column chunks are addressable (else the scalar epilogue)
     const int vec = (N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!bias || al16(bias))) ? 1 : 0;
-#define MSAT_G2(D, T) hipLaunchKernelGGL((gemm2_kernel<D, T>), grid, blk, 0, s, A, lda, B, ldb, C, ldc, bias, M, N, K, \
-                                         accumulate, ntn, vec)
-#define MSAT_G3(T) hipLaunchKernelGGL((gemm2_kernel<16, T, 3>), grid, blk, 0, s, A, lda, B, ldb, C, ldc, bias, M, N, \
-                                      K, accumulate, ntn, vec)
-    if (gemm_stages() == 3 && slab_depth() == 16) {
-        if (transB) MSAT_G3(true); else MSAT_G3(false);
-    } else if (slab_depth() == 16) {
-        if (transB) MSAT_G2(16, true); else MSAT_G2(16, false);
-    } else {
-        if (transB) MSAT_G2(32, true); else MSAT_G2(32, false);
-    }
-#undef MSAT_G2
-#undef MSAT_G3
+    if (transB)
+        hipLaunchKernelGGL((gemm2_kernel<16, true>), grid, blk, 0, s, A, lda, B, ldb, C, ldc, bias, M, N, K, accumulate,
+                           ntn, vec);
+    else
+        hipLaunchKernelGGL((gemm2_kernel<16, false>), grid, blk, 0, s, A, lda, B, ldb, C, ldc, bias, M, N, K,
+                           accumulate, ntn, vec);
     return check_launch("gemm2_kernel");
 }
 
@@ -357,11 +337,7 @@ int msat_wgrad2_launch(const float *A, int lda, const float *G, int ldg, float *
                        int rows_per_split, hipStream_t s) {
     const int ntk = (K + kG2M - 1) / kG2M, ntn = (N + kG2M - 1) / kG2M;
     const int tiles = ntk * ntn;
-    if (slab_depth() == 16)
-        hipLaunchKernelGGL((wgrad2_kernel<16>), dim3(tiles * splits), dim3(kG2T), 0, s, A, lda, G, ldg, part, M, K, N,
-                           rows_per_split, ntn, tiles);
-    else
-        hipLaunchKernelGGL((wgrad2_kernel<32>), dim3(tiles * splits), dim3(kG2T), 0, s, A, lda, G, ldg, part, M, K, N,
-                           rows_per_split, ntn, tiles);
+    hipLaunchKernelGGL((wgrad2_kernel<16>), dim3(tiles * splits), dim3(kG2T), 0, s, A, lda, G, ldg, part, M, K, N,
+                       rows_per_split, ntn, tiles);
     return check_launch("wgrad2_kernel");
 }

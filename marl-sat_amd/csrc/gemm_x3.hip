@@ -27,13 +27,6 @@ namespace msat {
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// diagnostic ablations of gemm_x3_kernel (timing only, wrong results; never set in the product
-// build): bit 0 no weight DMA after slab 0, 1 no activation loads after the prologue, 2 no split
-// store after the prologue, 3 no MFMAs
-#ifndef MSAT_GEMM_ABL
-#define MSAT_GEMM_ABL 0
-#endif
-
 constexpr int kX3T = 256;
 constexpr int kX3M = 128;  // tile rows / cols
 constexpr int kX3D = 16;   // slab depth (one bf16 MFMA k step)
@@ -64,9 +57,9 @@ __global__ void split_bf16x3_kernel(const float *__restrict__ W, int rows, int c
 }
 
 // C[M,N] (+)= A[M,K] @ W^T + bias, W planes [3][N][K] bf16.  K % 16 == 0, lda % 4 == 0, A 16-B aligned.
-// TI = 32-row MFMA tiles per wave: the workgroup tile is (64 TI) x 128 (2 x 2 waves).  TI = 4 reads
-// each weight fragment once for four row tiles (0.375 LDS fragment reads per MFMA instead of 0.5)
-// at two workgroups per CU instead of three.
+// The LDS-staged form, for K % 32 != 0 (the register-A kernel below takes K % 32 == 0).
+// TI = 32-row MFMA tiles per wave: the workgroup tile is (64 TI) x 128 (2 x 2 waves); launched with
+// TI = 2 (TI = 4, 256-row tiles, measured 8 % slower on the 407 K-row shape in round 1).
 template <int TI>
 __global__ void __launch_bounds__(kX3T, TI == 2 ? 3 : 2)
 gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ Wp, float *__restrict__ C, int ldc,
@@ -156,11 +149,11 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
     auto iter = [&](int s, float4 (&Rn)[SR][2], float4 (&Rf)[SR][2]) {
         const int buf = s & 1;
         const bool more = s + 1 < ns;
-        if (!(MSAT_GEMM_ABL & 1) && more) issueW(s + 1, buf ^ 1);
-        if (!(MSAT_GEMM_ABL & 2) && s >= 1 && s + 2 < ns) loadA(s + 2, Rf);  // s = 0: A(2) was issued in the prologue
-        if (!(MSAT_GEMM_ABL & 8)) slab(buf);
+        if (more) issueW(s + 1, buf ^ 1);
+        if (s >= 1 && s + 2 < ns) loadA(s + 2, Rf);  // s = 0: A(2) was issued in the prologue
+        slab(buf);
         __builtin_amdgcn_sched_barrier(0);
-        if (!(MSAT_GEMM_ABL & 4) && more) storeA(Rn, buf ^ 1);
+        if (more) storeA(Rn, buf ^ 1);
         // W(s+1) and A(s+1) landed; A(s+2) (issued after W(s+1) for s >= 1) may fly.  At s = 0,
         // A(2) precedes W(1) in issue order, so the wait drains everything.
         if (s >= 1 && s + 2 < ns) wait_vmcnt<NL>();
@@ -215,181 +208,6 @@ gemm_x3_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ 
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) {
                 const int row = m0 + wr + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-                if (row >= M) continue;
-                float *c = C + (size_t)row * ldc + col;
-                const float v = acc[i][j][reg] + bv;
-                *c = accumulate ? *c + v : v;
-            }
-        }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Register-A form of the same product (K % 32 == 0).  Each wave owns 32 TI rows x all 128 columns
-// of the workgroup tile, so no other wave needs its activation rows: they go global -> registers
-// -> split -> MFMA operands and never touch LDS.  For the 32x32x16 MFMA lane (r, h) holds
-// A[r][8h + j] of a 16-deep step, i.e. 32 contiguous bytes per lane: two float4 loads per row
-// tile and step, straight from the row.  Only the weight planes, shared by the four waves, are
-// staged: 32-deep double slabs by LDS-DMA into [plane][128 rows][4 chunks of 8 k] images (64-B
-// rows, chunk XOR (row >> 2) & 3: conflict-free ds_read_b128 fragments), one barrier per 32 k.
-// The MFMA sequence per (row tile, column tile, k step) is the register-staged kernel's, so the
-// results are bitwise those of gemm_x3_kernel.
-template <int TI, int PF>
-__global__ void __launch_bounds__(kX3T, TI == 1 && PF == 1 ? 3 : 2)
-gemm_x3r_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict__ Wp, float *__restrict__ C, int ldc,
-                const float *__restrict__ bias, int M, int N, int K, int accumulate, int ntn, int vec_out) {
-    constexpr int MT = 128 * TI;       // tile rows (4 waves x 32 TI)
-    constexpr int WPL = kX3M * 4;      // uint4 per weight plane image: 128 rows x 4 chunks = 8 KiB
-    __shared__ uint4 lds_w[2][3][WPL];  // 48 KiB
-    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
-    const int m0 = (id / ntn) * MT, n0 = (id % ntn) * kX3M;
-    const int t = threadIdx.x, w = t >> 6, lane = t & 63, li = lane & 31, h = lane >> 5;
-    const int wr = w * 32 * TI;
-    const float *arow[TI];
-#pragma unroll
-    for (int i = 0; i < TI; ++i) arow[i] = A + (size_t)min(m0 + wr + 32 * i + li, M - 1) * lda + 8 * h;
-    // weight DMA: 24 wave-instructions (1 KiB = 16 rows x 4 chunks each) per double slab, 6 per wave.
-    // Instruction e of wave w fills plane q = (6w + e) / 8, rows 16 p .. 16 p + 15 (p = (6w + e) % 8);
-    // lane -> row 16 p + (lane >> 2), LDS chunk lane & 3 holding source chunk (lane & 3) ^ ((row >> 2) & 3).
-    // weight DMA: 24 wave-instructions (1 KiB = 16 rows x 4 chunks each) per double slab, 6 per wave.
-    // Instruction e of wave w fills plane q = (6w + e) / 8, rows 16 p .. 16 p + 15 (p = (6w + e) % 8);
-    // lane -> row 16 p + (lane >> 2), LDS chunk lane & 3 holding source chunk (lane & 3) ^ ((row >> 2) & 3).
-    unsigned voff[6];
-#pragma unroll
-    for (int e = 0; e < 6; ++e) {
-        const int x = 6 * w + e, q = x >> 3, p = x & 7, row = 16 * p + (lane >> 2);
-        const int ch = (lane & 3) ^ ((row >> 2) & 3);
-        voff[e] = (unsigned)(((size_t)q * N * K + (size_t)min(n0 + row, N - 1) * K + 8 * ch) * 2);
-    }
-    auto issueW = [&](int d, int buf) {
-        const char *base = reinterpret_cast<const char *>(Wp) + (size_t)d * 64;
-#pragma unroll
-        for (int e = 0; e < 6; ++e) {
-            const int x = 6 * w + e;
-            glds16_async_s(base, voff[e], &lds_w[buf][x >> 3][64 * (x & 7)]);
-        }
-    };
-    f32x16v acc[TI][4];
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x16v{};
-    // raw A of one double slab per register set: [tile][2 step + half]; PF sets, A(d) in set d % PF
-    float4 ra[PF][TI][4];
-    auto loadA = [&](int d, float4 (&r)[TI][4]) {
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                r[i][e] = *reinterpret_cast<const float4 *>(arow[i] + 32 * d + 16 * (e >> 1) + 4 * (e & 1));
-    };
-    const int sw = (li >> 2) & 3;
-    const int nd = K / 32;
-#pragma unroll
-    for (int p = 0; p < PF; ++p)
-        if (p < nd) loadA(p, ra[p]);
-    issueW(0, 0);
-    wait_vmcnt<0>();
-    barrier_lds();
-    // per double slab d: split A(d), issue W(d+1) and A(d+PF) (into A(d)'s set), MFMAs of d, wait
-    // for W(d+1) (vector-memory counts retire in issue order, so A(d+PF) may still fly), barrier
-    auto iter = [&](int d, float4 (&r)[TI][4]) {
-        const int buf = d & 1;
-        bf16x8 fa[TI][2][3];
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const Split8 sp = split8(r[i][2 * u], r[i][2 * u + 1]);
-#pragma unroll
-                for (int q = 0; q < 3; ++q) fa[i][u][q] = __builtin_bit_cast(bf16x8, sp.p[q]);
-            }
-        __builtin_amdgcn_sched_barrier(0);
-        const bool more = d + 1 < nd, fill = d + PF < nd;
-        if (!(MSAT_GEMM_ABL & 1) && more) issueW(d + 1, buf ^ 1);
-        if (!(MSAT_GEMM_ABL & 2) && fill) loadA(d + PF, r);
-        __builtin_amdgcn_sched_barrier(0);
-        if (!(MSAT_GEMM_ABL & 8)) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    bf16x8 fb[3];
-#pragma unroll
-                    for (int q = 0; q < 3; ++q)
-                        fb[q] = __builtin_bit_cast(bf16x8, lds_w[buf][q][(32 * j + li) * 4 + ((2 * u + h) ^ sw)]);
-#pragma unroll
-                    for (int i = 0; i < TI; ++i) {
-                        f32x16v c = acc[i][j];
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][2], fb[0], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][1], fb[1], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][0], fb[2], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][1], fb[0], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][0], fb[1], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][u][0], fb[0], c, 0, 0, 0);
-                        acc[i][j] = c;
-                    }
-                }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (fill && !(MSAT_GEMM_ABL & 2)) wait_vmcnt<4 * TI>();
-        else wait_vmcnt<0>();
-        barrier_lds();
-    };
-    if constexpr (PF == 1) {
-        for (int d = 0; d < nd; ++d) iter(d, ra[0]);
-    } else {
-        int d = 0;
-        for (; d + 1 < nd; d += 2) {
-            iter(d, ra[0]);
-            iter(d + 1, ra[1]);
-        }
-        if (d < nd) iter(d, ra[0]);
-    }
-    float *ldsf = reinterpret_cast<float *>(&lds_w[0][0][0]);  // 48 KiB: four 8 KiB wave stages
-    if (vec_out) {
-        float *stage = ldsf + w * 32 * 64;
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-            for (int hc = 0; hc < 2; ++hc) {  // columns 64 hc .. 64 hc + 63 of the wave's 32 rows
-#pragma unroll
-                for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-                    for (int reg = 0; reg < 16; ++reg)
-                        stage[((reg & 3) + 8 * (reg >> 2) + 4 * h) * 64 + 32 * jj + li] = acc[i][2 * hc + jj][reg];
-                __syncthreads();
-                const int col = n0 + 64 * hc + (lane & 15) * 4;
-                float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (bias && col < N) bv = *reinterpret_cast<const float4 *>(bias + col);
-#pragma unroll
-                for (int it = 0; it < 8; ++it) {
-                    const int r = it * 4 + (lane >> 4);
-                    const int row = m0 + wr + 32 * i + r;
-                    float4 v = *reinterpret_cast<const float4 *>(stage + r * 64 + (lane & 15) * 4);
-                    v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-                    if (row < M && col < N) {
-                        float4 *c = reinterpret_cast<float4 *>(C + (size_t)row * ldc + col);
-                        if (accumulate) {
-                            const float4 o = *c;
-                            v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
-                        }
-                        *c = v;
-                    }
-                }
-                __syncthreads();
-            }
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int col = n0 + 32 * j + li;
-            if (col >= N) continue;
-            const float bv = bias ? bias[col] : 0.0f;
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int row = m0 + wr + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
                 if (row >= M) continue;
                 float *c = C + (size_t)row * ldc + col;
                 const float v = acc[i][j][reg] + bv;
@@ -465,10 +283,10 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
         }
         __builtin_amdgcn_sched_barrier(0);
         const bool more = d + 1 < nd;
-        if (!(MSAT_GEMM_ABL & 1) && more) issueW(d + 1, buf ^ 1);
-        if (!(MSAT_GEMM_ABL & 2) && more) loadA(d + 1);
+        if (more) issueW(d + 1, buf ^ 1);
+        if (more) loadA(d + 1);
         __builtin_amdgcn_sched_barrier(0);
-        if (!(MSAT_GEMM_ABL & 8)) {
+        {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 bf16x8 fb[3];
@@ -489,7 +307,7 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (more && !(MSAT_GEMM_ABL & 2)) wait_vmcnt<2 * RT>();
+        if (more) wait_vmcnt<2 * RT>();
         else wait_vmcnt<0>();
         barrier_lds();
     }
@@ -579,9 +397,6 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
 // 16x16x32 block instead of six bf16.  If the weight split overflowed (*wbad), the kernel runs the
 // bf16x3 body on the bf16x3 planes instead (same grid and LDS).
 constexpr int kDgW = 10;  // weight scale 2^10: |W| < 32 fits
-#ifndef MSAT_DG_PF
-#define MSAT_DG_PF 2
-#endif
 
 template <int RT, int NP>
 __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int lda, const int *__restrict__ rexp,
@@ -627,8 +442,8 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
     // activations two double slabs ahead in two register sets (plain loads: hipcc tracks them and
     // waits for A(d) just before its split; its count ignores the asm weight DMAs, which only makes
     // that wait stricter, and W(d) has landed by then anyway)
-    // the bf16x3 body keeps one set (its split needs the registers); MSAT_DG_PF=1: one set for both (A/B)
-    constexpr int PF = (NP == 2 && MSAT_DG_PF == 2) ? 2 : 1;
+    // the bf16x3 body keeps one set (its split needs the registers)
+    constexpr int PF = NP == 2 ? 2 : 1;
     float4 ras[PF][RT][2];
     auto loadA = [&](int d, float4 (&ra)[RT][2]) {
 #pragma unroll
@@ -1005,15 +820,7 @@ wgrad_x3_kernel(const float *__restrict__ A, int lda, const float *__restrict__ 
 // IL: the split and LDS store of slab s + 1 are interleaved with slab s's MFMAs by scheduling groups
 // (one MFMA, then a few vector instructions; an LDS store every few MFMAs), so the split fills the
 // MFMA issue gaps instead of running as its own phase between the MFMA phase and the barrier.
-//
-// diagnostic ablations (timing only, wrong results; never set in the product build): bit 0 no
-// operand loads after the prologue, 1 no MFMAs, 2 no split / LDS store after it
-#ifndef MSAT_WW_ABL
-#define MSAT_WW_ABL 0
-#endif
-#ifndef MSAT_WW_PF
-#define MSAT_WW_PF 2  // raw slab sets of the fp16x2 form (2, 3 or 4: measured equal or slower)
-#endif
+
 constexpr int kWWT = 512;
 constexpr int kWWN = 384;  // widest N
 
@@ -1157,10 +964,9 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
     if (ns > 0) {
         // NPF register sets of raw slabs: at iteration s they hold slabs s + 1 .. s + NPF - 1 (in flight or
         // landed) and the set of slab s (stored at the end of iteration s - 1) receives slab s + NPF.
-        // fp16x2: MSAT_WW_PF sets (three or four, 96-128 KiB in flight per CU, measured 1 % slower than
-        // two: the kernel is not latency-bound on its loads); bf16x3 keeps two (its split needs the
-        // registers).
-        constexpr int NPF = NP == 2 ? MSAT_WW_PF : 2;
+        // Two sets (three or four, 96-128 KiB in flight per CU, measured 1 % slower for the fp16x2 form:
+        // the kernel is not latency-bound on its loads).
+        constexpr int NPF = 2;
         Stage R[NPF];
 #pragma unroll
         for (int k = 0; k < NPF; ++k) load(k < ns ? k : ns - 1, R[k]);
@@ -1171,11 +977,11 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
         // measured 5 % slower on the dual launch, profiles/r02_ab_wgrad_stg.log)
         auto iter = [&](int s, const Stage &Rn, Stage &Rf) {
             const int buf = s & 1;
-            if (!(MSAT_WW_ABL & 1)) load(s + NPF < ns ? s + NPF : ns - 1, Rf);
+            load(s + NPF < ns ? s + NPF : ns - 1, Rf);
             __builtin_amdgcn_sched_barrier(0);
-            if (!(MSAT_WW_ABL & 2)) slab(buf);
+            slab(buf);
             if constexpr (IL) {
-                if (!(MSAT_WW_ABL & 4)) store(s + 1, Rn, buf ^ 1);
+                store(s + 1, Rn, buf ^ 1);
                 constexpr int NM = 6 * NP;  // MFMAs per wave and slab
                 __builtin_amdgcn_sched_group_barrier(0x100, 10 * NP, 0);  // the fragment reads first
 #pragma unroll
@@ -1290,34 +1096,15 @@ extern "C" int msat_gemm_x3(const float *A, int32_t lda, const void *Wplanes, fl
                  "gemm_x3: K %% 16, lda %% 4 and 16-byte aligned operands required");
     const int ntn = (N + kX3M - 1) / kX3M;
     const int vec = (N % 4 == 0 && ldc % 4 == 0 && a16x3(C) && (!bias || a16x3(bias))) ? 1 : 0;
-    const char *e = getenv("MARLSAT_GEMM_X3_TI");  // 32-row tiles per wave: 2 (128-row tile) or 4 (256)
     const __bf16 *Wb = reinterpret_cast<const __bf16 *>(Wplanes);
-    // register-A kernels (K % 32 == 0): 16 = 16x16x32 MFMA, 128-row tiles (default); 32 = the same
-    // with 256-row tiles; 1 = 32x32x16; 0 = off
-    const char *r = getenv("MARLSAT_GEMM_X3_R");
-    const int rv = r ? atoi(r) : 16;
-    if ((rv == 1 || rv == 16 || rv == 32) && K % 32 == 0) {
-        const int rows = rv == 32 ? 256 : 128, ntm = (M + rows - 1) / rows;
-        if (rv == 16)
-            hipLaunchKernelGGL((gemm_x3r16_kernel<2>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
-                               Wb, C, ldc, bias, M, N, K, accumulate, ntn, vec);
-        else if (rv == 32)
-            hipLaunchKernelGGL((gemm_x3r16_kernel<4>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
-                               Wb, C, ldc, bias, M, N, K, accumulate, ntn, vec);
-        else
-            hipLaunchKernelGGL((gemm_x3r_kernel<1, 1>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda,
-                               Wb, C, ldc, bias, M, N, K, accumulate, ntn, vec);
-        return check_launch("gemm_x3r_kernel");
-    }
-    if (e && atoi(e) == 4) {
-        const int ntm = (M + 255) / 256;
-        hipLaunchKernelGGL((gemm_x3_kernel<4>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda, Wb, C,
+    const int ntm = (M + 127) / 128;
+    if (K % 32 == 0) {  // register-A kernel on 16x16x32 MFMAs, 128-row tiles
+        hipLaunchKernelGGL((gemm_x3r16_kernel<2>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda, Wb, C,
                            ldc, bias, M, N, K, accumulate, ntn, vec);
-    } else {
-        const int ntm = (M + 127) / 128;
-        hipLaunchKernelGGL((gemm_x3_kernel<2>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda, Wb, C,
-                           ldc, bias, M, N, K, accumulate, ntn, vec);
+        return check_launch("gemm_x3r16_kernel");
     }
+    hipLaunchKernelGGL((gemm_x3_kernel<2>), dim3(ntm * ntn), dim3(kX3T), 0, (hipStream_t)stream, A, lda, Wb, C, ldc,
+                       bias, M, N, K, accumulate, ntn, vec);
     return check_launch("gemm_x3_kernel");
 }
 
@@ -1337,8 +1124,6 @@ int msat_wgrad_x3_launch(const float *A, int lda, const float *G, int ldg, float
 
 // Whole-row weight gradient (wgrad_w_kernel): N <= 384 besides the x3 conditions.
 bool msat_wgrad_x3w_ok(const float *A, int lda, const float *G, int ldg, int K, int N) {
-    const char *e = getenv("MARLSAT_WGRAD_W");  // 0: the 128 x 128 tile kernel (A/B measurements)
-    if (e && e[0] == '0') return false;
     return N <= kWWN && msat_wgrad_x3_ok(A, lda, G, ldg, K, N);
 }
 
@@ -1348,21 +1133,12 @@ int msat_wgrad_x3w_splits(int M, int K) {
     return std::max(1, std::min(256 / ktiles, (M + 511) / 512));
 }
 
-static bool wgrad_interleave() {
-    const char *e = getenv("MARLSAT_WGRAD_WI");  // 0: split as its own phase after the MFMAs (A/B)
-    return !(e && e[0] == '0');
-}
-
 int msat_wgrad_x3w_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int rot,
                           int splits, hipStream_t s) {
     const int ktiles = (K + kX3M - 1) / kX3M;
     const int rows = (M + splits - 1) / splits, rows16 = ((rows + 15) / 16) * 16;
-    if (wgrad_interleave())
-        hipLaunchKernelGGL((wgrad_w_kernel<3, true>), dim3(ktiles * splits), dim3(kWWT), 0, s, A, lda, G, ldg, nullptr,
-                           part, M, K, N, rot, rows16, ktiles, nullptr);
-    else
-        hipLaunchKernelGGL((wgrad_w_kernel<3, false>), dim3(ktiles * splits), dim3(kWWT), 0, s, A, lda, G, ldg, nullptr,
-                           part, M, K, N, rot, rows16, ktiles, nullptr);
+    hipLaunchKernelGGL((wgrad_w_kernel<3, true>), dim3(ktiles * splits), dim3(kWWT), 0, s, A, lda, G, ldg, nullptr,
+                       part, M, K, N, rot, rows16, ktiles, nullptr);
     return check_launch("wgrad_w_kernel<3> (bf16x3)");
 }
 

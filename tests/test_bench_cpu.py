@@ -60,3 +60,26 @@ def test_host_cpu_record(monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "2")
     h = bench.host_cpu()
     assert h["cores"] == min(2, h["affinity_cores"]) and h["cap_source"] == "OMP_NUM_THREADS"
+
+
+def test_mappo_legs_fit_the_driver_tail():
+    """Two compact MAPPO legs at 8 ranks close the line within the driver's 2,000-character tail."""
+    import json
+
+    import bench
+
+    kern = "gru_ln_fused_fwd_h2s_kernel (fp16x2, + x3r fixup launch)"
+    full = {"metric": "MAPPO updates/sec", "value": 1 / 27.6123456, "unit": "updates/s", "s_per_update": 27.6123456,
+            "samples_per_s": 296.712345, "adam_steps_per_s": 0.579123,
+            "phase_ms": {"rollout": 1618.1123, "gae": 122.7123, "ppo_update": 25631.7123, "metrics": 244.5123},
+            "config": {"workload": "uf200-860", "num_agents": 25, "max_vars_per_agent": 8, "envs_per_gpu": 4096,
+                       "NUM_STEPS": 2, "UPDATE_EPOCHS": 4, "MINIBATCH_SIZE": 2048, "GNN_HIDDEN_DIM": 128,
+                       "GNN_NUM_MESSAGE_PASSING_STEPS": 16,
+                       "parallelism": "dp8 (env shards; RCCL gradient all-reduce per minibatch)"},
+            "roofline": {"bound": "hbm", "achieved": 3107.123456, "peak": 8000.0, "unit": "GB/s", "frac": 0.3884123,
+                         "traffic": 3.6e9 * 1.17123, "kernel": kern, "kernel_ms": 1.3168123,
+                         "mfma": {"frac": 0.27123}, "per_rank_kernel_ms": [1.3168123 + i * 1e-3 for i in range(8)]}}
+    leg = bench.compact_leg(full, "gpurun_out/bench_mappo_uf200-860_n8_rank0.json")
+    tail = json.dumps({"mappo_other_legs": [leg], "mappo": leg})
+    assert len(tail) < 1900, len(tail)
+    assert leg["roofline"]["kernel"] == "gru_ln_fused_fwd_h2s_kernel" and leg["config"]["parallelism"] == "dp8"

@@ -115,6 +115,14 @@ DEPTH_CASES = [  # the reference's depth (MAPPO_CONFIG.yaml:23-24: H = 128, L = 
 ]
 
 
+# elementwise bar of the depth tests: |err| <= 1e-5 |ref| + factor x E32 (E32 = the largest error of the
+# same oracle run in float32 on the CPU).  Measured on MI355X (profiles/r03_parity_depth.txt): forward
+# outputs <= FWD ratio, gradients up to ~3.9 x on the device fp32 path itself (two independent fp32
+# summation orders: the elementwise maximum of one can exceed the other's by that much)
+FWD_FACTOR = 2.0
+GRAD_FACTOR = 4.0
+
+
 def _fp32_yardstick(P, L, args, av, am, mode, wl, wv):
     """The same oracle evaluated in float32 on the CPU: the reference's own arithmetic class.  Returns
     its logits, value and parameter gradients for the cotangents (wl, wv)."""
@@ -137,7 +145,8 @@ def _close_yard(dev, ref, yard, factor, what, report, kink=None):
     e32 = np.abs(yard[fin] - ref[fin]).max() if fin.any() else 0.0
     err = np.abs(dev[fin] - ref[fin])
     extra = np.zeros_like(ref) if kink is None else np.asarray(kink, np.float64)
-    report.append((what, float(err.max() / max(e32, 1e-300)) if err.size else 0.0))
+    plain = extra[fin] == 0  # the ratio is reported over the elements without a ReLU-kink allowance
+    report.append((what, float(err[plain].max() / max(e32, 1e-300)) if plain.any() else 0.0))
     bound = 1e-5 * np.abs(ref[fin]) + factor * e32 + extra[fin]
     assert (err <= bound).all(), f"{what}: max err {err.max():.3g}, worst ratio {(err / bound).max():.3g}"
 
@@ -168,7 +177,7 @@ def test_depth16_matches_oracle(V, C, vpa, H, L, S, mode, path, monkeypatch):
     float64 oracle.
 
     Bar: normwise 1e-5 (max |err| <= 1e-5 max |ref| per tensor) AND elementwise
-    |err| <= 1e-5 |ref| + atol, atol = 4x (forward) / 8x (gradients) the largest error of the same
+    |err| <= 1e-5 |ref| + atol, atol = FWD_FACTOR (forward) / GRAD_FACTOR (gradients) x the largest error of the same
     oracle run in float32 on the CPU.  A pure elementwise 1e-5 relative bar is beyond fp32 itself:
     the float32 oracle misses it on 1-5 % of the logits at these depths (tests/probe_parity_depth.py,
     profiles/r02_parity_depth.txt), so the fp32 rounding of the reference's own arithmetic is the
@@ -215,17 +224,18 @@ def _depth_check(V, C, vpa, H, L, S, mode, path):
     report = []
     _close_norm(logits.cpu().numpy(), rl, 1e-5, "logits")
     _close_norm(value.cpu().numpy(), rv, 1e-5, "value")
-    _close_yard(logits.cpu().numpy(), rl, y_l, 4.0, "logits", report)
-    _close_yard(value.cpu().numpy(), rv, y_v, 4.0, "value", report)
+    _close_yard(logits.cpu().numpy(), rl, y_l, FWD_FACTOR, "logits", report)
+    _close_yard(value.cpu().numpy(), rv, y_v, FWD_FACTOR, "value", report)
     net.grads.zero_()
     net.backward(b, state, wl.float().cuda().contiguous(), wv.float().cuda().contiguous())
     got = net.to_flax(grads=True)
     for name, p in P.items():
         ref = p.grad.numpy() if p.grad is not None else np.zeros(p.shape)
-        _close_yard(got[name], ref, y_g[name], 8.0, f"grad {name}", report, kink[name])
+        _close_yard(got[name], ref, y_g[name], GRAD_FACTOR, f"grad {name}", report, kink[name])
+    fwd = {w: round(r, 2) for w, r in report[:2]}
     report.sort(key=lambda t: -t[1])
-    print(f"depth16 {path} V={V} mode={mode}: {n_kink} ReLU inputs within 3e-5 of 0; worst err / fp32-oracle err",
-          [(w, round(r, 2)) for w, r in report[:5]])
+    print(f"depth16 {path} V={V} mode={mode}: {n_kink} ReLU inputs within 3e-5 of 0; err / fp32-oracle err: "
+          f"forward {fwd}; worst gradients", [(w, round(r, 2)) for w, r in report[:5] if w.startswith("grad")])
 
 
 def test_critic_only_batch_matches_full():
