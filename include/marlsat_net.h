@@ -143,25 +143,8 @@ int msat_gru_ln_fused_fwd(const float *x0, int32_t ld0, int32_t w0, const float 
                           const float *wi, const float *bi, const float *wh, const float *bh,
                           const float *ln_scale, const float *ln_bias, float *out, int32_t ldo, float *g4,
                           int32_t ldg, int32_t R, int32_t H, void *stream);
-/* Same cell with transposed weights wiT (3H, Kp) / whT (3H, H), Kp = Kx rounded up to 16 and
- * zero-padded (msat_transpose_pad): k-major operand images read with ds_read_b128 fragments.
- * H = 64 or 128. */
-int msat_transpose_pad(const float *W, int32_t K, int32_t N, int32_t ldw, float *out, int32_t Kp, void *stream);
-int msat_gru_ln_fused_fwd_t(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
-                            const float *x2, int32_t ld2, int32_t w2, const float *hprev, int32_t ldp,
-                            const float *wiT, const float *bi, const float *whT, const float *bh,
-                            const float *ln_scale, const float *ln_bias, float *out, int32_t ldo, float *g4,
-                            int32_t ldg, int32_t R, int32_t H, void *stream);
-/* Same cell on the bf16 matrix cores (exact bf16x3 split, fp32-accurate; H = 128): weights
- * given as msat_split_bf16x3 planes of Wi zero-padded to kxp rows (kxp >= Kx, multiple of 16)
- * and of Wh. */
-int msat_gru_ln_fused_fwd_x3(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
-                             const float *x2, int32_t ld2, int32_t w2, const float *hprev, int32_t ldp,
-                             const void *wi_planes, int32_t kxp, const float *bi, const void *wh_planes,
-                             const float *bh, const float *ln_scale, const float *ln_bias, float *out, int32_t ldo,
-                             float *g4, int32_t ldg, int32_t R, int32_t H, void *stream);
-/* Register-A form of msat_gru_ln_fused_fwd_x3 (16x16x32 bf16 MFMAs; activations read straight into
- * registers, only the weights staged): weights given as msat_split_bf16x3_t planes of Wi^T zero-padded
+/* Same cell on the bf16 matrix cores (exact bf16x3 split, fp32-accurate; H = 128; register-A on
+ * 16x16x32 bf16 MFMAs: activations read straight into registers, only the weights staged): weights given as msat_split_bf16x3_t planes of Wi^T zero-padded
  * to kxp columns (kxp >= Kx, multiple of 32) and of Wh^T (kxp = H).  g4 rows 16-byte aligned. */
 int msat_gru_ln_fused_fwd_x3r(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
                               const float *x2, int32_t ld2, int32_t w2, const float *hprev, int32_t ldp,

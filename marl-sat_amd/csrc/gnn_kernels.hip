@@ -181,18 +181,11 @@ gru_ln_fwd_kernel(const float *__restrict__ Gi, int ldi, const float *__restrict
 // NF > 0: the partials also carry feature-weighted gate sums for the input-matrix rows of NF
 // per-row features (feat, ld ldf): part[block][NQ + 3k + g] = sum_rows feat[r][k] * dG_g[r]
 // (g = r, z, n gate) -- the weight gradient of those input rows without another pass over dGi.
-#ifndef MSAT_BWD_OCC6
-#define MSAT_BWD_OCC6 1  // workgroups per CU the NF = 6 (var cell) form is compiled for (1: no bound)
-#endif
-// MSAT_BWD_VEC: for PER >= 2 a lane owns PER adjacent columns (PER * lane + u), loaded and stored as one
-// PER-wide vector access, instead of columns lane + 64 u (one dword access each).  The per-column
-// partials keep their row order; only the row sums behind the LayerNorm statistics change order.
-#ifndef MSAT_BWD_VEC
-#define MSAT_BWD_VEC 1
-#endif
-#ifndef MSAT_BWD_VEC_ALL
-#define MSAT_BWD_VEC_ALL 0  // A/B only: the vector layout for every cell form, not just the var cell
-#endif
+// VEC (the var cell, NF = 6, PER >= 2): a lane owns PER adjacent columns (PER * lane + u), loaded and
+// stored as one PER-wide vector access, instead of columns lane + 64 u (one dword access each).  The
+// per-column partials keep their row order; only the row sums behind the LayerNorm statistics change
+// order.  Measured -0.3..-2 % on the var cell and +16 % on the clause cell, which keeps the scalar
+// layout.
 template <int N>
 __device__ __forceinline__ void ldv(const float *__restrict__ p, float *o) {
     if constexpr (N == 1) {
@@ -319,7 +312,7 @@ __device__ __forceinline__ void bwd_row_vec(const float *__restrict__ gi, const 
 }
 
 template <int PER, bool G4, int NQ = 2, int NF = 0, bool VEC = false>
-__global__ void __launch_bounds__(kRowThreads, NF == 6 ? MSAT_BWD_OCC6 : 1)
+__global__ void __launch_bounds__(kRowThreads, 1)
 gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
                   const float *__restrict__ scale, float *__restrict__ dGi, int lddi, float *__restrict__ dGh, int lddh,
@@ -633,10 +626,8 @@ using namespace msat;
 
 static int grid_rows(long rows) { return (int)std::min<long>((rows + 3) / 4, 8192); }
 // GRU/LN backward: at most 1024 blocks (16 waves per CU), so its per-block LN partials stay small
-#ifndef MSAT_BWD_MAXB
-#define MSAT_BWD_MAXB 1024  // GRU backward grid cap (partial-sum rows = blocks)
-#endif
-static int bwd_blocks(long rows) { return (int)std::min<long>((rows + 3) / 4, MSAT_BWD_MAXB); }
+constexpr long kBwdMaxBlocks = 1024;  // GRU backward grid cap (partial-sum rows = blocks)
+static int bwd_blocks(long rows) { return (int)std::min<long>((rows + 3) / 4, kBwdMaxBlocks); }
 constexpr int kPartRows = 16;  // rows per first-stage block when reducing LN partials
 
 
@@ -798,13 +789,13 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
     // var cell 503-506 vs 510-517 us; the clause cell (nfeat = 2) ran 1310-1341 vs 1132-1135 us in this
     // layout, so it and the bias-less / feature-less forms keep the scalar layout.
     const int vper = H / 64, va = 4 * vper;
-    const bool vec = MSAT_BWD_VEC && (MSAT_BWD_VEC_ALL || nfeat == 6) && vper >= 2 && ((uintptr_t)dy | (uintptr_t)g4 | (uintptr_t)hprev |
+    const bool vec = nfeat == 6 && vper >= 2 && ((uintptr_t)dy | (uintptr_t)g4 | (uintptr_t)hprev |
                                                    (uintptr_t)ln_scale | (uintptr_t)dGi | (uintptr_t)dGh |
                                                    (uintptr_t)dhprev) % va == 0 &&
                      (ldy | ldg | ldp | lddi | lddh | lddp) % vper == 0;
 #define MSAT_BWD1(PER, Q, F)                                                                                      \
     if (vec)                                                                                                      \
-        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2 && (MSAT_BWD_VEC_ALL || F == 6)>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, \
+        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2 && F == 6>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, \
                            hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign,    \
                            packed, feat, ldf, rexp);                                                              \
     else                                                                                                          \

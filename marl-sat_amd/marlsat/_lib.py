@@ -118,7 +118,6 @@ def _load():
     sig["msat_assemble_graph_batch"] = (I, [I, I, I, I, I] + [P] * 26 + [I, I, P])
     sig["msat_clause_gather"] = (I, [P, I, P, P, I, I, I, I, P])
     sig["msat_var_gather"] = (I, [P, I, P, P, P, I, I, I, I, P])
-    sig["msat_transpose_pad"] = (I, [P, I, I, I, P, I, P])
     sig["msat_split_bf16x3"] = (I, [P, I, I, I, P, P])
     sig["msat_split_bf16x3_rot"] = (I, [P, I, I, I, I, P, P])
     sig["msat_gemm_x3"] = (I, [P, I, P, P, I, P, I, I, I, I, P])
@@ -135,8 +134,6 @@ def _load():
     sig["msat_var_gather2"] = (I, [P, P, I, P, P, P, P, I, I, I, I, P])
     sig["msat_gru_ln_fwd"] = (I, [P, I, P, I, P, I, P, P, P, I, I, I, P])
     sig["msat_gru_ln_fused_fwd"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, P, P, P, P, P, P, I, P, I, I, I, P])
-    sig["msat_gru_ln_fused_fwd_t"] = sig["msat_gru_ln_fused_fwd"]
-    sig["msat_gru_ln_fused_fwd_x3"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, I, P, P, P, P, P, P, I, P, I, I, I, P])
     sig["msat_gru_ln_fused_fwd_x3r"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, I, P, P, P, P, P, P, I, P, I, I, I, P])
     sig["msat_split_bf16x3_t"] = (I, [P, I, I, I, I, P, P])
     sig["msat_gru_ln_fused_fwd_h2r"] = (I, [P, I, I, P, I, I, P, I, I, P, I, P, P, P, P, I, P, P, P, P, P, I, P, I, I, I,
@@ -211,9 +208,6 @@ EXPORTED = (
     "msat_assemble_graph_batch",
     "msat_clause_gather",
     "msat_var_gather",
-    "msat_transpose_pad",
-    "msat_gru_ln_fused_fwd_t",
-    "msat_gru_ln_fused_fwd_x3",
     "msat_gru_ln_fused_fwd_x3r",
     "msat_split_bf16x3_t",
     "msat_gru_ln_fused_fwd_h2r",

@@ -26,6 +26,14 @@ from .graphs import GraphBatch
 
 L_ = _lib.lib
 
+# Arithmetic of the matrix work (README "Kernel-path switches"): "fp16x2" (default) runs the GRU
+# forward and the backward's data / weight gradients on fp16 MFMAs with a two-way fp32 split, falling
+# back per tile to "bf16x3" (three-way bf16 split) where fp16's range fails; "bf16x3" runs that
+# fallback throughout; "fp32" keeps every product on fp32 MFMA (the accuracy reference path).
+PRECISION = os.environ.get("MARLSAT_PRECISION", "fp16x2")
+if PRECISION not in ("fp16x2", "bf16x3", "fp32"):
+    raise ValueError(f"MARLSAT_PRECISION must be fp16x2, bf16x3 or fp32, got {PRECISION!r}")
+
 
 def _chk(rc, what):
     if rc:
@@ -162,18 +170,11 @@ class GNNActorCritic:
 
     def _gemm64(self, A, lda, transA, B, ldb, transB, C, ldc, M, N, K, acc=0):
         """fp64-accumulated small product, one rounding per element (the folded weights, gemm.hip)."""
-        mode = os.environ.get("MARLSAT_FOLD_F64", "1")
-        if mode == "0" or mode == ("bwd" if transA or transB else "fwd"):  # A/B: plain fp32 GEMMs (pre-r02)
-            if transA:
-                self._wgrad(A, lda, B, ldb, C, ldc, K, M, N, acc)
-            else:
-                self._gemm(A, lda, B, ldb, transB, C, ldc, None, M, N, K, acc)
-            return
         _chk(L_.msat_gemm_f64acc(A, lda, transA, B, ldb, transB, C, ldc, M, N, K, acc, self.stream),
              "msat_gemm_f64acc")
 
     # fp32-accurate bf16x3 split GEMM for the backward's C (+)= dG @ W^T products (gemm_x3.hip)
-    use_x3 = os.environ.get("MARLSAT_GEMM_X3", "1") != "0"
+    use_x3 = PRECISION != "fp32"
 
     def _split_weights(self, mats):
         """bf16x3 planes of each (rows, 3H) weight block (once per backward): {key: planes tensor}.
@@ -189,10 +190,11 @@ class GNNActorCritic:
         return out
 
     # fp16x2 data gradients of the packed backward rows (gemm_x3.hip gemm_h2r16_kernel)
-    use_dgrad_h2 = os.environ.get("MARLSAT_DGRAD_H2", "1") != "0"
+    use_dgrad_h2 = PRECISION == "fp16x2"
 
-    # a cell's two data gradients / two weight gradients in one launch each (gemm_x3.hip *_dual_kernel)
-    use_dual = os.environ.get("MARLSAT_DUAL", "1") != "0"
+    # a cell's two data gradients / two weight gradients in one launch each (gemm_x3.hip *_dual_kernel;
+    # the fp16x2 path always takes them: -4 % against separate launches, round 2)
+    use_dual = True
 
     def _dgrad_dual(self, p0, p1, rexp, M, K):
         """p = (A, lda, fp16x2 planes, bf16x3 planes, wbad pointer, C, ldc, N, accumulate): both
@@ -259,7 +261,7 @@ class GNNActorCritic:
         ws = self.scr.get_ws(int(L_.msat_gemm_wgrad_workspace_bytes(M, K, N)))
         if K <= 8:
             label = "wgrad_skinny + reduce (K <= 8)"
-        elif N <= 384 and os.environ.get("MARLSAT_WGRAD_W", "1") != "0":
+        elif N <= 384:
             label = "wgrad_w_kernel<3> + reduce (bf16x3)"
         else:
             label = "wgrad_x3_kernel + reduce (bf16x3)"
@@ -269,7 +271,7 @@ class GNNActorCritic:
 
     # fp16x2 whole-row weight gradients of the GRU backward's packed rows (gemm_x3.hip wgrad_w_kernel<2>):
     # the backward writes each row's scale exponent, the kernel scales G per row split
-    use_wgrad_h2 = os.environ.get("MARLSAT_WGRAD_H2", "1") != "0"
+    use_wgrad_h2 = PRECISION == "fp16x2"
 
     def _wgrad_h2(self, A, lda, G, ldg, rexp, W, ldw, M, K, N, acc=1, rot=0):
         """W[:, (n + rot) % N] (+)= (A^T G)[:, n] in fp16x2; rexp: G's row scale exponents."""
@@ -288,12 +290,9 @@ class GNNActorCritic:
         ws = self.scr.get_part(int(L_.msat_colsum_workspace_floats(M, N)))
         _chk(L_.msat_colsum(G, ldg, M, N, out, acc, ws.data_ptr(), self.stream), "msat_colsum")
 
-    # bf16x3 split GRU kernel (fp32-accurate, bf16 matrix cores) for the fused encoder at H = 128
-    use_gru_x3 = os.environ.get("MARLSAT_GRU_X3", "1") != "0"
-
-    # register-A bf16x3 GRU kernel on 16x16x32 MFMAs (gru_fused.hip x3r): 5-8 % faster than the x3
-    # kernel without the tape (rollout), 3-4 % with it (training); default (MARLSAT_GRU_X3R=0: x3)
-    use_gru_x3r = os.environ.get("MARLSAT_GRU_X3R", "1") != "0"
+    # split GRU kernels (fp32-accurate, 16x16x32 MFMAs, register-A) for the fused encoder at H = 128:
+    # bf16x3 (gru_fused.hip x3r), and the fp16x2 kernel below with x3r as its fixup; else fp32 MFMA
+    use_gru_x3 = PRECISION != "fp32"
 
     def _split_weights_t(self, mats):
         """{key: (K, 3H) matrix} -> {key: (W^T bf16x3 planes (3, 3H, Kp), Kp)}, Kp = K rounded up to 32
@@ -311,7 +310,7 @@ class GNNActorCritic:
     # fp16x2 operands for the register-A GRU forward (gru_fused.hip kRH2: three fp16 MFMAs per product
     # instead of six bf16 ones, two weight planes instead of three; tiles whose activations leave fp16's
     # range are recomputed in bf16x3 by the same launch pair); MARLSAT_GRU_H2=0 keeps bf16x3 throughout
-    use_gru_h2 = os.environ.get("MARLSAT_GRU_H2", "1") != "0"
+    use_gru_h2 = PRECISION == "fp16x2"
 
     def _split_weights_h2(self, cells):
         """{cell: (Wi (Kx, 3H), Wh (H, 3H))} -> ({cell: (wi planes, wh planes)}, wbad (cells, 2) int32):
@@ -331,16 +330,12 @@ class GNNActorCritic:
             out[key] = (bufs[0], bufs[1], self._ptr(bad[c]))
         return out, bad
 
-    # transposed-weight GRU kernel (k-major images, ds_read_b128 fragments): measured equal to the
-    # [K][3H] form (profiles/gru_bench.py: 855-3060 vs 888-3049 us) plus the per-forward transposes,
-    # so it is opt-in (MARLSAT_GRU_T=1)
-    use_gru_t = os.environ.get("MARLSAT_GRU_T", "0") == "1"
-
     def _gru(self, cell: str, segs, hprev: torch.Tensor, ln_row: torch.Tensor, out: torch.Tensor,
              g4: Optional[torch.Tensor], R: int, wi: Optional[torch.Tensor] = None, wt=None):
         """One fused GRU cell + LayerNorm (msat_gru_ln_fused_fwd): segs = [(ptr, ld, width)] of x;
         wi overrides the cell's input matrix (the phi-folded matrices of the fused encoder);
-        wt = (wiT, whT) selects the transposed-weight kernel."""
+        wt = {"wi": (W^T planes, kxp), "wh": planes[, "h2": fp16x2 planes]} selects the register-A
+        bf16x3 kernel (msat_gru_ln_fused_fwd_x3r) or, with "h2", the fp16x2 one + its bf16x3 fixup."""
         H = self.H
         segs = list(segs) + [(0, 0, 0)] * (3 - len(segs))
         kx = sum(w for _, _, w in segs)
@@ -360,7 +355,7 @@ class GNNActorCritic:
                                              wbad, self.stream),
                 "msat_gru_ln_fused_fwd_h2r"), nb)
             return
-        if isinstance(wt, dict) and wt.get("x3r"):  # register-A kernel: W^T planes {"wi": (planes, kxp), "wh"}
+        if isinstance(wt, dict):  # register-A bf16x3 kernel: W^T planes {"wi": (planes, kxp), "wh": planes}
             self._timed("gru_ln_fused_fwd_x3r_kernel (bf16x3)", 2.0 * R * 3 * H * (H + kx), lambda: _chk(
                 L_.msat_gru_ln_fused_fwd_x3r(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
                                              wt["wi"][0].data_ptr(), wt["wi"][1],
@@ -369,23 +364,6 @@ class GNNActorCritic:
                                              self._ptr(ln_row, H), out.data_ptr(), H,
                                              g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
                 "msat_gru_ln_fused_fwd_x3r"), 4.0 * R * (kx + 2 * H + (4 * H if g4 is not None else 0)))
-            return
-        if isinstance(wt, dict):  # bf16x3 planes {"wi": (planes, kxp), "wh": planes}
-            _chk(L_.msat_gru_ln_fused_fwd_x3(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
-                                             wt["wi"][0].data_ptr(), wt["wi"][1],
-                                             self.p(f"enc.{cell}_bi").data_ptr(), wt["wh"].data_ptr(),
-                                             self.p(f"enc.{cell}_bh").data_ptr(), self._ptr(ln_row),
-                                             self._ptr(ln_row, H), out.data_ptr(), H,
-                                             g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
-                 "msat_gru_ln_fused_fwd_x3")
-            return
-        if wt is not None:
-            _chk(L_.msat_gru_ln_fused_fwd_t(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
-                                            wt[0].data_ptr(), self.p(f"enc.{cell}_bi").data_ptr(),
-                                            wt[1].data_ptr(), self.p(f"enc.{cell}_bh").data_ptr(),
-                                            self._ptr(ln_row), self._ptr(ln_row, H), out.data_ptr(), H,
-                                            g4.data_ptr() if g4 is not None else 0, 4 * H, R, H, self.stream),
-                 "msat_gru_ln_fused_fwd_t")
             return
         _chk(L_.msat_gru_ln_fused_fwd(p0, l0, w0, p1, l1, w1, p2, l2, w2, hprev.data_ptr(), H,
                                       (self.p(f"enc.{cell}_wi") if wi is None else wi).data_ptr(),
@@ -445,20 +423,16 @@ class GNNActorCritic:
     # different fp32 association: parity is the 1e-5 fp32 bar, not bitwise.
     fuse_phi = os.environ.get("MARLSAT_FUSE_PHI", "1") != "0"
 
-    def _fold_views(self, padded: bool = False):
-        """Views of the folded matrices F_c (2H+4 rows), F_v+, F_v- (H+8 rows) and of their gradients.
-        Each block is followed by zero rows up to a multiple of 16 (padded=True returns those
-        views: the bf16x3 GRU kernel reads whole 16-row slabs)."""
+    def _fold_views(self):
+        """Views of the folded matrices F_c (2H+4 rows), F_v+, F_v- (H+8 rows) and of their gradients
+        (each block 16-row aligned in one buffer, zero rows between)."""
         H = self.H
         c, v = 2 * H + 4, H + 8
         cp, vp = (c + 15) // 16 * 16, (v + 15) // 16 * 16
         if getattr(self, "_F", None) is None:
             self._F = torch.zeros((cp + 2 * vp, 3 * H), dtype=torch.float32, device=self.device)
             self._gF = torch.zeros_like(self._F)
-        if padded:
-            sl = lambda T: (T[:cp], T[cp:cp + vp], T[cp + vp:cp + 2 * vp])
-        else:
-            sl = lambda T: (T[:c], T[cp:cp + v], T[cp + vp:cp + vp + v])
+        sl = lambda T: (T[:c], T[cp:cp + v], T[cp + vp:cp + vp + v])
         return sl(self._F), sl(self._gF)
 
     def _fold_weights(self):
@@ -504,17 +478,6 @@ class GNNActorCritic:
             self._gemm64(pp(bv, half * H), H, 1, pp(gF[H + 4 + half]), W3, 0, gwi.data_ptr(), W3, H, W3, 1, 1)
             self._colsum(pp(gF[H]), 4 * W3, 1, 4 * W3, pp(gwi[H]))  # the x / svf rows map 1:1
 
-    def _transposed_weights(self, mats):
-        """{key: (K, 3H) matrix} -> {key: (3H, Kp) transposed, zero-padded to Kp = K rounded up to 16}."""
-        out = {}
-        for key, Wm in mats.items():
-            K, N = Wm.shape
-            Kp = (K + 15) // 16 * 16
-            T = torch.empty((N, Kp), dtype=torch.float32, device=self.device)
-            _chk(L_.msat_transpose_pad(Wm.data_ptr(), K, N, N, T.data_ptr(), Kp, self.stream), "transpose_pad")
-            out[key] = T
-        return out
-
     def _encode_fused(self, b: GraphBatch, save: bool):
         H, dev = self.H, self.device
         Nv, Nc = b.Nv, b.Nc
@@ -523,10 +486,10 @@ class GNNActorCritic:
         self._fold_weights()
         (Fc, Fp, Fn), _ = self._fold_views()
         wt = {"gru_c": None, "gru_vp": None, "gru_vn": None}
-        if self.use_gru_x3r and H == 128:
+        if self.use_gru_x3 and H == 128:
             pl = self._split_weights_t({"c": Fc, "vp": Fp, "vn": Fn, "hc": self.p("enc.gru_c_wh"),
                                         "hvp": self.p("enc.gru_vp_wh"), "hvn": self.p("enc.gru_vn_wh")})
-            wt = {c: {"x3r": True, "wi": pl[k], "wh": pl[hk][0]}
+            wt = {c: {"wi": pl[k], "wh": pl[hk][0]}
                   for c, k, hk in (("gru_c", "c", "hc"), ("gru_vp", "vp", "hvp"), ("gru_vn", "vn", "hvn"))}
             if self.use_gru_h2:
                 h2, self._h2bad = self._split_weights_h2({
@@ -534,17 +497,6 @@ class GNNActorCritic:
                     "gru_vn": (Fn, self.p("enc.gru_vn_wh"))})
                 for c in wt:
                     wt[c]["h2"] = h2[c]
-        elif self.use_gru_x3 and H == 128:
-            (Pc, Pp, Pn), _ = self._fold_views(padded=True)
-            pl = self._split_weights({"c": (Pc, 0), "vp": (Pp, 0), "vn": (Pn, 0), "hc": (self.p("enc.gru_c_wh"), 0),
-                                      "hvp": (self.p("enc.gru_vp_wh"), 0), "hvn": (self.p("enc.gru_vn_wh"), 0)})
-            wt = {"gru_c": {"wi": (pl["c"], Pc.shape[0]), "wh": pl["hc"]},
-                  "gru_vp": {"wi": (pl["vp"], Pp.shape[0]), "wh": pl["hvp"]},
-                  "gru_vn": {"wi": (pl["vn"], Pn.shape[0]), "wh": pl["hvn"]}}
-        elif self.use_gru_t and H in (64, 128):
-            T = self._transposed_weights({"c": Fc, "vp": Fp, "vn": Fn, "hc": self.p("enc.gru_c_wh"),
-                                          "hvp": self.p("enc.gru_vp_wh"), "hvn": self.p("enc.gru_vn_wh")})
-            wt = {"gru_c": (T["c"], T["hc"]), "gru_vp": (T["vp"], T["hvp"]), "gru_vn": (T["vn"], T["hvn"])}
         Hp, Hn, Hc = self._embed(b)
         tape: List[StepTape] = []
         ln = self.p("enc.ln")

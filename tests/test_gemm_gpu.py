@@ -71,14 +71,14 @@ def test_gemm_wgrad(M, K, N):
             assert torch.equal(W, W1)  # bitwise reproducible
 
 
-@pytest.mark.parametrize("path", ["1", "0"])  # register-staged kernels / LDS-DMA fast path
 @pytest.mark.parametrize("M,N,K,transB", [(1, 4, 32, 0), (130, 132, 64, 0), (1000, 384, 256, 0), (257, 128, 384, 1),
-                                          (700, 260, 128, 1), (129, 256, 96, 0), (3, 128, 32, 1)])
-def test_gemm_fast_path_shapes(M, N, K, transB, path, monkeypatch):
-    """K % 32 == 0 shapes take the LDS-DMA kernel (tails in M and N: clamped reads, masked stores)."""
+                                          (700, 260, 128, 1), (129, 256, 96, 0), (3, 128, 32, 1), (77, 130, 36, 0),
+                                          (65, 6, 40, 1)])
+def test_gemm_fast_path_shapes(M, N, K, transB):
+    """K % 32 == 0 shapes take the LDS-DMA kernel (tails in M and N: clamped reads, masked stores); the
+    last two (K % 32 != 0, N % 4 != 0) the register-staged kernel."""
     from marlsat import _lib
 
-    monkeypatch.setenv("MARLSAT_GEMM", path)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + 7 * K)
     A = torch.randn(M, K, device="cuda", generator=g)
     B = torch.randn((N, K) if transB else (K, N), device="cuda", generator=g)
@@ -94,8 +94,8 @@ def test_gemm_fast_path_shapes(M, N, K, transB, path, monkeypatch):
         _ref_close(C, ref, absprod)
 
 
-# register-staged / fp32 LDS-DMA / bf16x3 128x128 tiles / bf16x3 whole-row (default for N <= 384)
-@pytest.mark.parametrize("path", ["1", "0", "x3", "x3w"])
+# fp32 MFMA tiles (MARLSAT_PRECISION=fp32) / bf16x3 (whole-row for N <= 384, 128 x 128 tiles above)
+@pytest.mark.parametrize("path", ["fp32", "x3"])
 @pytest.mark.parametrize("M,K,N", [(1, 4, 4), (33, 128, 384), (5000, 132, 384), (70001, 128, 128), (100, 256, 8),
                                    (407001, 128, 384), (9999, 256, 260), (17, 16, 4), (1000, 12, 36), (3000, 300, 384),
                                    (2049, 256, 512)])
@@ -104,10 +104,7 @@ def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
     kernels (transposed LDS reads) are held to the same fp32 bound as the fp32 MFMA kernels."""
     from marlsat import _lib
 
-    x3 = path in ("x3", "x3w")
-    monkeypatch.setenv("MARLSAT_GEMM", "0" if x3 else path)
-    monkeypatch.setenv("MARLSAT_WGRAD_X3", "1" if x3 else "0")
-    monkeypatch.setenv("MARLSAT_WGRAD_W", "1" if path == "x3w" else "0")
+    monkeypatch.setenv("MARLSAT_PRECISION", "fp32" if path == "fp32" else "fp16x2")
     g = torch.Generator(device="cuda").manual_seed(M + K + N)
     A = torch.randn(M, K, device="cuda", generator=g)
     G = torch.randn(M, N, device="cuda", generator=g)
@@ -122,21 +119,21 @@ def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
         _ref_close(W, ref, absprod)
 
 
-@pytest.mark.parametrize("path", ["x3w", "x3", "fp32"])
+@pytest.mark.parametrize("path", ["x3", "fp32"])
 @pytest.mark.parametrize("M,K,N,rot,ldg", [(5000, 128, 384, 256, 512), (70001, 256, 384, 256, 512), (999, 128, 128, 32, 128),
-                                           (300, 256, 384, 128, 384), (700001, 64, 192, 128, 192)])
+                                           (300, 256, 384, 128, 384), (5000, 128, 512, 256, 512),
+                                           (700001, 64, 192, 128, 192)])
 def test_wgrad_rot(M, K, N, rot, ldg, path, monkeypatch):
     """msat_gemm_wgrad_rot: W[:, (n + rot) % N] (+)= (A^T G)[:, n] (the packed GRU backward rows), on the
-    whole-row kernel's rotated store and on the two-range fallback (bf16x3 tiles, or fp32 MFMA tiles with
-    MARLSAT_WGRAD_X3=0); G read from a wider row (ld > N).  The H = 64, 700 K-row case: the fallback's
+    whole-row kernel's rotated store (N <= 384) and on the two-range fallback (bf16x3 tiles for N = 512, or
+    fp32 MFMA tiles with MARLSAT_PRECISION=fp32); G read from a wider row (ld > N).  The H = 64, 700 K-row case: the fallback's
     128-column sub-product takes more row splits than the full width, and the workspace
     (msat_gemm_wgrad_workspace_bytes) must hold them."""
     from marlsat import _lib
 
     if path == "fp32" and M < 700001:
         pytest.skip("the fp32 fallback is covered by the large-M case")
-    monkeypatch.setenv("MARLSAT_WGRAD_W", "1" if path == "x3w" else "0")
-    monkeypatch.setenv("MARLSAT_WGRAD_X3", "0" if path == "fp32" else "1")
+    monkeypatch.setenv("MARLSAT_PRECISION", "fp32" if path == "fp32" else "fp16x2")
     g = torch.Generator(device="cuda").manual_seed(M + K + N + rot)
     A = torch.randn(M, K, device="cuda", generator=g)
     Gw = torch.randn(M, ldg, device="cuda", generator=g)
@@ -289,22 +286,18 @@ def test_colsum_deterministic(M, N, ld, off):
     assert torch.equal(res[0][:oo], out0[:oo]) and torch.equal(res[0][oo + N:], out0[oo + N:])
 
 
-@pytest.mark.parametrize("ti", ["2", "4", "r1", "r16", "r32"])  # 128- / 256-row tiles; register-A 32x32x16, 16x16x32 (128 / 256 rows)
-@pytest.mark.parametrize("M,N,K", [(1, 4, 16), (130, 132, 64), (1000, 384, 384), (5000, 128, 384), (257, 256, 128),
-                                   (3, 7, 32)])
-def test_gemm_x3_fp32_accuracy(M, N, K, ti, monkeypatch):
+@pytest.mark.parametrize("M,N,K,lda", [(1, 4, 16, 16), (130, 132, 64, 64), (1000, 384, 384, 384), (5000, 128, 384, 384),
+                                       (257, 256, 128, 128), (3, 7, 32, 32), (77, 100, 48, 52), (5000, 128, 384, 512),
+                                       (1001, 256, 384, 384), (77, 100, 64, 68)])
+def test_gemm_x3_fp32_accuracy(M, N, K, lda):
     """bf16x3 split GEMM: C = A @ W^T (+ bias, + C) at fp32 accuracy (same bound as the f32 MFMA
-    kernels: 2e-6 of sum |a b|), including values spanning many binades."""
+    kernels: 2e-6 of sum |a b|), including values spanning many binades and strided A rows.  K % 32 == 0
+    takes the register-A 16x16x32 kernel, K % 32 == 16 the LDS-staged one."""
     from marlsat import _lib
 
-    if ti.startswith("r"):
-        monkeypatch.setenv("MARLSAT_GEMM_X3_R", ti[1:])
-    else:
-        monkeypatch.setenv("MARLSAT_GEMM_X3_R", "0")
-        monkeypatch.setenv("MARLSAT_GEMM_X3_TI", ti)
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
-    A = torch.randn(M, K, device="cuda", generator=g) * torch.exp2(torch.randint(-6, 7, (M, K), device="cuda",
-                                                                                generator=g).float())
+    A = torch.randn(M, lda, device="cuda", generator=g) * torch.exp2(torch.randint(-6, 7, (M, lda), device="cuda",
+                                                                                    generator=g).float())
     W = torch.randn(N, K, device="cuda", generator=g)
     bias = torch.randn(N, device="cuda", generator=g)
     C0 = torch.randn(M, N, device="cuda", generator=g)
@@ -314,45 +307,14 @@ def test_gemm_x3_fp32_accuracy(M, N, K, ti, monkeypatch):
     hi, mid, lo = (planes[i * N * K:(i + 1) * N * K].view(torch.bfloat16).float().view(N, K) for i in range(3))
     assert float(((hi.double() + mid.double() + lo.double()) - W.double()).abs().max()) <= \
         2.0 ** -24 * float(W.abs().max())
+    Ak = A[:, :K].double()
     for acc in (0, 1):
         C = C0.clone()
-        _lib.check(_lib.lib.msat_gemm_x3(A.data_ptr(), K, planes.data_ptr(), C.data_ptr(), N, bias.data_ptr(), M, N,
+        _lib.check(_lib.lib.msat_gemm_x3(A.data_ptr(), lda, planes.data_ptr(), C.data_ptr(), N, bias.data_ptr(), M, N,
                                          K, acc, s), "gemm_x3")
-        ref = A.double() @ W.double().t() + bias.double() + (C0.double() if acc else 0)
-        absprod = A.double().abs() @ W.double().abs().t() + bias.double().abs() + (C0.double().abs() if acc else 0)
+        ref = Ak @ W.double().t() + bias.double() + (C0.double() if acc else 0)
+        absprod = Ak.abs() @ W.double().abs().t() + bias.double().abs() + (C0.double().abs() if acc else 0)
         _ref_close(C, ref, absprod)
-
-
-@pytest.mark.parametrize("M,N,K,lda", [(5000, 128, 384, 512), (1001, 256, 384, 384), (77, 100, 64, 68)])
-def test_gemm_x3_register_a_bitwise(M, N, K, lda, monkeypatch):
-    """The 32x32x16 register-A kernel issues the register-staged kernel's MFMA sequence per output
-    tile, so its results are bitwise equal (strided A rows, both accumulate modes); the 16x16x32
-    form meets the fp32 bound on the same strided operands."""
-    from marlsat import _lib
-
-    g = torch.Generator(device="cuda").manual_seed(M + K)
-    A = torch.randn(M, lda, device="cuda", generator=g)
-    W = torch.randn(N, K, device="cuda", generator=g)
-    C0 = torch.randn(M, N, device="cuda", generator=g)
-    planes = torch.empty(3 * N * K + 8, dtype=torch.int16, device="cuda")
-    s = _lib.stream_ptr()
-    _lib.check(_lib.lib.msat_split_bf16x3(W.data_ptr(), N, K, K, planes.data_ptr(), s), "split")
-    for acc in (0, 1):
-        out = []
-        for r in ("0", "1"):
-            monkeypatch.setenv("MARLSAT_GEMM_X3_R", r)
-            C = C0.clone()
-            _lib.check(_lib.lib.msat_gemm_x3(A.data_ptr(), lda, planes.data_ptr(), C.data_ptr(), N, None, M, N, K,
-                                             acc, s), "gemm_x3")
-            out.append(C)
-        assert all(torch.equal(out[0], o) for o in out[1:])
-        monkeypatch.setenv("MARLSAT_GEMM_X3_R", "16")  # 16x16x32 form: same bound, another summation order
-        C = C0.clone()
-        _lib.check(_lib.lib.msat_gemm_x3(A.data_ptr(), lda, planes.data_ptr(), C.data_ptr(), N, None, M, N, K, acc, s),
-                   "gemm_x3")
-        Ak = A[:, :K].double()
-        _ref_close(C, Ak @ W.double().t() + (C0.double() if acc else 0),
-                   Ak.abs() @ W.double().abs().t() + (C0.double().abs() if acc else 0))
 
 
 @pytest.mark.parametrize("M,K1", [(1, 128), (4999, 128), (70001, 256)])

@@ -72,18 +72,16 @@ def _close_norm(dev, ref, rtol, what):
     _close(dev, ref, 0.0, rtol * max(np.abs(ref[fin]).max(), 1e-12), what)
 
 
-@pytest.mark.parametrize("fuse,x3", [(True, True), (True, False), (False, True), (True, "r")])
+@pytest.mark.parametrize("fuse,path", [(True, "default"), (True, "bf16x3"), (True, "fp32"), (False, "bf16x3"),
+                                       (False, "fp32")])
 @pytest.mark.parametrize("V,C,vpa,H,L,S,mode", CASES)
-def test_forward_backward_match_oracle(V, C, vpa, H, L, S, mode, fuse, x3, monkeypatch):
-    """fuse: phi folded into the GRU input matrices (else reference order); x3: bf16x3 data
-    gradients with packed backward rows and the bf16x3 GRU forward at H = 128 (else fp32 MFMA
-    GEMMs / GRU, separate dGi / dGh); "r": the same with the register-A GRU forward (x3r)."""
+def test_forward_backward_match_oracle(V, C, vpa, H, L, S, mode, fuse, path, monkeypatch):
+    """fuse: phi folded into the GRU input matrices (else the reference order); path: the arithmetic
+    (_set_path: fp16x2 / bf16x3 split kernels at H = 128, packed backward rows; fp32 MFMA)."""
     from marlsat.learners.gnn import GNNActorCritic
 
+    _set_path(monkeypatch, path)
     monkeypatch.setattr(GNNActorCritic, "fuse_phi", fuse)
-    monkeypatch.setattr(GNNActorCritic, "use_x3", bool(x3))
-    monkeypatch.setattr(GNNActorCritic, "use_gru_x3", bool(x3))
-    monkeypatch.setattr(GNNActorCritic, "use_gru_x3r", x3 == "r")
     net, b, P, batch, av, am, A, M = _setup(V, C, vpa, H, L, S, mode)
     logits, value, state = net.forward(b, save=True)
     ref_logits = onet.actor_logits(P, L, batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"], av,
@@ -153,19 +151,20 @@ def _close_yard(dev, ref, yard, factor, what, report, kink=None):
 
 def _set_path(monkeypatch, path):
     """'default': the bench's kernels (phi folded, fp16x2 GRU forward / data / weight gradients with
-    dual launches); 'bf16x3': phi folded, the four fp16x2 switches off (the bf16x3 register-A GRU
-    forward, bf16x3 data and weight gradients: the fallback wherever fp16's range fails); 'fp32': the
-    reference operation order on fp32 MFMA kernels."""
+    dual launches); 'bf16x3': phi folded, the fp16x2 kernels off (the bf16x3 register-A GRU forward,
+    bf16x3 data and weight gradients: the fallback wherever fp16's range fails; MARLSAT_PRECISION=bf16x3);
+    'fp32': the reference operation order on fp32 MFMA kernels (MARLSAT_PRECISION=fp32 + FUSE_PHI=0)."""
     from marlsat.learners.gnn import GNNActorCritic
 
     fast = path != "fp32"
     monkeypatch.setattr(GNNActorCritic, "fuse_phi", fast)
     monkeypatch.setattr(GNNActorCritic, "use_x3", fast)
     monkeypatch.setattr(GNNActorCritic, "use_gru_x3", fast)
-    monkeypatch.setattr(GNNActorCritic, "use_gru_x3r", fast)
     h2 = path == "default"
-    for sw in ("use_gru_h2", "use_dgrad_h2", "use_wgrad_h2", "use_dual"):
+    for sw in ("use_gru_h2", "use_dgrad_h2", "use_wgrad_h2"):
         monkeypatch.setattr(GNNActorCritic, sw, h2)
+    # the C-side weight-gradient choice (gemm.hip wgrad_x3) follows MARLSAT_PRECISION, read per call
+    monkeypatch.setenv("MARLSAT_PRECISION", {"default": "fp16x2", "bf16x3": "bf16x3", "fp32": "fp32"}[path])
 
 
 @pytest.mark.parametrize("path", ["default", "bf16x3", "fp32"])
@@ -179,11 +178,11 @@ def test_depth16_matches_oracle(V, C, vpa, H, L, S, mode, path, monkeypatch):
     Bar: normwise 1e-5 (max |err| <= 1e-5 max |ref| per tensor) AND elementwise
     |err| <= 1e-5 |ref| + atol, atol = FWD_FACTOR (forward) / GRAD_FACTOR (gradients) x the largest error of the same
     oracle run in float32 on the CPU.  A pure elementwise 1e-5 relative bar is beyond fp32 itself:
-    the float32 oracle misses it on 1-5 % of the logits at these depths (tests/probe_parity_depth.py,
+    the float32 oracle misses it on 1-5 % of the logits at these depths (profiles/archive_r02/probe_parity_depth.py,
     profiles/r02_parity_depth.txt), so the fp32 rounding of the reference's own arithmetic is the
     yardstick for the elements near zero.  Gradients also allow oracle.net.kink_bound: a ReLU input
     within 3e-5 (relative) of 0 may land on either side in fp32, and the two sides' gradients
-    differ by a whole term (tests/probe_head_bisect.py: one flipped flip-head unit moved its bias
+    differ by a whole term (profiles/archive_r02/probe_head_bisect.py: one flipped flip-head unit moved its bias
     gradient by 5e-3)."""
     _set_path(monkeypatch, path)
     _depth_check(V, C, vpa, H, L, S, mode, path)

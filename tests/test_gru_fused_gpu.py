@@ -61,18 +61,6 @@ def _setup(R, H, kind, seed):
     return segs, x, h, wi, bi, wh, bh, sc, lb
 
 
-def _transposed(W):
-    """msat_transpose_pad: W (K, N) -> W^T (N, Kp) zero-padded to Kp = K rounded up to 16."""
-    from marlsat import _lib
-
-    K, N = W.shape
-    Kp = (K + 15) // 16 * 16
-    out = torch.full((N, Kp), float("nan"), device="cuda")
-    _lib.check(_lib.lib.msat_transpose_pad(W.data_ptr(), K, N, N, out.data_ptr(), Kp, _lib.stream_ptr()),
-               "transpose_pad")
-    return out
-
-
 def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
     from marlsat import _lib
 
@@ -80,21 +68,6 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
     args = []
     for t, off, ld, w in segs + [(None, 0, 0, 0)] * (3 - len(segs)):
         args += [t.data_ptr() + 4 * off if t is not None else 0, ld, w]
-    if layout == "x3":  # bf16x3 split kernel (H = 128): weights as split planes, Wi zero-padded to kxp
-        K = wi.shape[0]
-        kxp = (K + 15) // 16 * 16
-        wip = torch.zeros(kxp, 3 * H, device="cuda")
-        wip[:K] = wi
-        pi = torch.empty(3 * kxp * 3 * H + 8, dtype=torch.int16, device="cuda")
-        ph = torch.empty(3 * H * 3 * H + 8, dtype=torch.int16, device="cuda")
-        _lib.check(_lib.lib.msat_split_bf16x3(wip.data_ptr(), kxp, 3 * H, 3 * H, pi.data_ptr(), _lib.stream_ptr()), "split")
-        _lib.check(_lib.lib.msat_split_bf16x3(wh.data_ptr(), H, 3 * H, 3 * H, ph.data_ptr(), _lib.stream_ptr()), "split")
-        _lib.check(_lib.lib.msat_gru_ln_fused_fwd_x3(*args, h.data_ptr(), H, pi.data_ptr(), kxp, bi.data_ptr(),
-                                                     ph.data_ptr(), bh.data_ptr(), sc.data_ptr(), lb.data_ptr(),
-                                                     out.data_ptr(), H, g4.data_ptr() if g4 is not None else 0, 4 * H,
-                                                     R, H, _lib.stream_ptr()), "gru_ln_fused_fwd_x3")
-        torch.cuda.synchronize()
-        return out
     if layout == "x3r":  # register-A bf16x3 kernel (16x16x32): transposed planes W^T, K padded to 32
         K = wi.shape[0]
         kxp = (K + 31) // 32 * 32
@@ -133,15 +106,6 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
         torch.cuda.synchronize()
         _fwd.last_flags = (flags[:(R + 127) // 128].cpu(), bad.cpu())
         return out
-    if layout == "t":  # transposed-weight kernel (k-major images, ds_read_b128 fragments)
-        wiT, whT = _transposed(wi), _transposed(wh)
-        assert bool((wiT[:, wi.shape[0]:] == 0).all()) and torch.equal(wiT[:, :wi.shape[0]], wi.t())
-        _lib.check(_lib.lib.msat_gru_ln_fused_fwd_t(*args, h.data_ptr(), H, wiT.data_ptr(), bi.data_ptr(),
-                                                    whT.data_ptr(), bh.data_ptr(), sc.data_ptr(), lb.data_ptr(),
-                                                    out.data_ptr(), H, g4.data_ptr() if g4 is not None else 0, 4 * H,
-                                                    R, H, _lib.stream_ptr()), "gru_ln_fused_fwd_t")
-        torch.cuda.synchronize()
-        return out
     _lib.check(_lib.lib.msat_gru_ln_fused_fwd(*args, h.data_ptr(), H, wi.data_ptr(), bi.data_ptr(), wh.data_ptr(),
                                               bh.data_ptr(), sc.data_ptr(), lb.data_ptr(), out.data_ptr(), H,
                                               g4.data_ptr() if g4 is not None else 0, 4 * H, R, H,
@@ -150,10 +114,9 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
 
 
 def _fwd_cases():
-    """(layout, H, R): the plain kernel at H 64 / 128 / 256, the transposed-weight kernel at H 64 /
-    128, the bf16x3 kernels (LDS-staged, register-A) and the fp16x2 register-A kernel at H 128; the
-    70,000-row case at the production width H = 128 only."""
-    widths = {"plain": (64, 128, 256), "t": (64, 128), "x3": (128,), "x3r": (128,), "h2r": (128,)}
+    """(layout, H, R): the fp32 kernel at H 64 / 128 / 256, the register-A bf16x3 and fp16x2 kernels at
+    H 128; the 70,000-row case at the production width H = 128 only."""
+    widths = {"plain": (64, 128, 256), "x3r": (128,), "h2r": (128,)}
     return [(lay, H, R) for lay, hs in widths.items() for H in hs for R in (0, 1, 77, 1000, 70000)
             if R != 70000 or H == 128]
 
