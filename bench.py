@@ -353,6 +353,7 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
         rk = torch.tensor(rank_ms, dtype=torch.float64, device="cuda")
         dist.all_reduce(rk)  # every rank fills its own slot: SUM = gather
         rank_ms = [float(v) for v in rk]
+    replicas = replica_check(net, dist)
     if type(comm).__name__ == "CapiComm":
         comm.destroy()
     n_mb = B * T // cfg["MINIBATCH_SIZE"]
@@ -381,6 +382,7 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
         "issued_gemm_tflops_over_cycle": gemm_tflops,
         "dtype": "f32 (fp32 accumulate; fp16x2 split MFMAs, bf16x3 where fp16's range does not hold)",
         "solve_rate": met["solve_rate"],
+        "replicas_identical": replicas,
         "peak_hbm_gb": torch.cuda.max_memory_allocated() / 1e9,
     }
     side = write_side_file(f"mappo_{workload}_n{world}_rank{rank}", full)
@@ -410,8 +412,26 @@ def compact_leg(full: dict, side: Optional[str]) -> dict:
                      "kernel": r["kernel"].split(" ")[0], "kernel_ms": _sig(r["kernel_ms"]),
                      "mfma_frac": _sig(r["mfma"]["frac"], 3),
                      "per_rank_kernel_ms": [_sig(v) for v in r["per_rank_kernel_ms"]]},
+        "replicas_identical": full.get("replicas_identical"),
         "detail": side,
     }
+
+
+def replica_check(net, dist):
+    """After the timed cycle every rank must hold bitwise the same parameters (the gradient all-reduce and
+    the identical Adam steps keep the replicas equal): an fp64 sum and an integer checksum of the flat
+    parameter bits, MIN- and MAX-reduced over ranks.  None at one rank."""
+    import torch
+
+    if dist is None:
+        return None
+    bits = net.params.view(torch.int32).to(torch.int64)
+    idx = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
+    v = torch.stack([net.params.double().sum(), (bits * idx).sum().double()])
+    lo, hi = v.clone(), v.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return bool(torch.equal(lo, hi))
 
 
 def write_side_file(name: str, obj) -> Optional[str]:

@@ -402,7 +402,7 @@ template <int RT, int NP>
 __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int lda, const int *__restrict__ rexp,
                                               const uint16_t *__restrict__ Wp, float *__restrict__ C, int ldc,
                                               const float *__restrict__ bias, int M, int N, int K, int accumulate,
-                                              int m0, int n0, int vec_out, uint4 (*lds_w)[3][kX3M * 4]) {
+                                              int m0, int n0, int vec_out, uint4 (*lds_w)[3][kX3M * 4], int kr = 0) {
     typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
     const int t = threadIdx.x, w = t >> 6, lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int wr = w * 16 * RT;
@@ -453,9 +453,13 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
     };
     const int slot = g ^ x3swz16((l16 >> 2) & 3);
     const int nd = K / 32;
-    loadA(0, ras[0]);
-    if (PF == 2 && nd > 1) loadA(1, ras[PF - 1]);
-    issueW(0, 0);
+    // the k walk starts at double slab kr (0 <= kr < nd) and wraps: the dual launch aligns its two
+    // products' walks over the packed rows they share, so sibling workgroups read the same columns of a
+    // row at the same time and the second read hits L2 (msat_gemm_h2_dual)
+    auto sl = [&](int d) { const int x = d + kr; return x >= nd ? x - nd : x; };
+    loadA(sl(0), ras[0]);
+    if (PF == 2 && nd > 1) loadA(sl(1), ras[PF - 1]);
+    issueW(sl(0), 0);
     wait_vmcnt<0>();
     barrier_lds();
     auto step = [&](int d, float4 (&ra)[RT][2]) {
@@ -478,8 +482,8 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
         }
         __builtin_amdgcn_sched_barrier(0);
         const bool more = d + 1 < nd;
-        if (more) issueW(d + 1, buf ^ 1);
-        if (d + PF < nd) loadA(d + PF, ra);  // this set was just split
+        if (more) issueW(sl(d + 1), buf ^ 1);
+        if (d + PF < nd) loadA(sl(d + PF), ra);  // this set was just split
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -631,6 +635,7 @@ struct DgradProblem {
     const int *wbad;
     float *C;
     int ldc, N, accumulate, vec_out, ntn;
+    int kr;  // first double slab of the k walk (aligns the two products' reads of the shared rows)
 };
 
 template <int RT>
@@ -645,10 +650,10 @@ gemm_h2r16_dual_kernel(DgradProblem p0, DgradProblem p1, const int *__restrict__
     const int n0 = (first ? sub : sub - p0.ntn) * kX3M;
     if (*p.wbad)
         gemm_r16_body<RT, 3>(p.A, p.lda, nullptr, p.Wx3, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0,
-                             p.vec_out, lds_w);
+                             p.vec_out, lds_w, p.kr);
     else
         gemm_r16_body<RT, 2>(p.A, p.lda, rexp, p.Wh2, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0, p.vec_out,
-                             lds_w);
+                             lds_w, p.kr);
 }
 
 // planes[q][r][c] = part q of 2^kDgW W[r][(c + rot) % cols] (fp16x2, q = 0, 1); *bad = 1 if a scaled
@@ -1237,6 +1242,16 @@ extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h
         p[i].accumulate = accs[i];
         p[i].vec_out = (Ns[i] % 4 == 0 && ldcs[i] % 4 == 0 && a16x3(Cs[i])) ? 1 : 0;
         p[i].ntn = (Ns[i] + kX3M - 1) / kX3M;
+        p[i].kr = 0;
+    }
+    // A GRU cell's packed rows D = [dan | dar | daz | dan r]: dh reads D[:, H:4H] (A0 = D + H), the input
+    // gradient D[:, 0:3H] (A1 = D).  Started H / 32 double slabs in, the input gradient's walk reads the
+    // columns the dh walk reads at the same step for the first 3H - H of its K, so the workgroups of a
+    // row block fetch those bytes from HBM once (their walks are otherwise offset by H columns, which at
+    // 96 resident workgroups per XCD and 2 KiB rows is enough to lose the L2 copy: 1.33x fetch, round 2).
+    {
+        const long off = (long)(A0 - A1);
+        if (lda0 == lda1 && off > 0 && off % 32 == 0 && off / 32 < K / 32) p[1].kr = (int)(off / 32);
     }
     const int ntm = (M + 127) / 128;
     hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(kX3T), 0,
