@@ -303,7 +303,9 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
                GNN_HIDDEN_DIM=H, GNN_NUM_MESSAGE_PASSING_STEPS=L, action_mode=0,
                MICROBATCH_BYTES=args.mappo_micro_gb * 1e9)
     env = SATEnv(V, C, max_steps=512, vars_per_agent=vpa)
-    pool = env.make_pool(generate_problem_pool(V, C, args.pool, size_id=size_id))
+    # instances leaving a variable in no clause are skipped: at zero-initialised biases that variable is a
+    # constant LayerNorm row whose gradient overflows fp32 in the reference too (generate_problem_pool doc)
+    pool = env.make_pool(generate_problem_pool(V, C, args.pool, size_id=size_id, skip_isolated=True))
     net = GNNActorCritic(H, L, env.num_agents, env.max_vars_per_agent, 0, V, device=env.device, seed=0)
     comm = dist if world > 1 else None
     if comm is not None and os.environ.get("MARLSAT_COLLECTIVES") == "capi":
@@ -375,6 +377,7 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
                    "envs_per_gpu": B, "global_envs": B * world, "NUM_STEPS": T, "UPDATE_EPOCHS": E,
                    "MINIBATCH_SIZE": cfg["MINIBATCH_SIZE"], "GNN_HIDDEN_DIM": H, "GNN_NUM_MESSAGE_PASSING_STEPS": L,
                    "micro_batch": learner.micro,
+                   "pool": f"{args.pool} instances, seeds 1000*{size_id}+i, instances with an unused variable skipped",
                    "parallelism": f"dp{world} (env shards; RCCL gradient all-reduce per minibatch"
                                   f"{', C-ABI communicator' if type(comm).__name__ == 'CapiComm' else ''})"},
         "roofline": roof,
@@ -382,7 +385,7 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
         "issued_gemm_tflops_over_cycle": gemm_tflops,
         "dtype": "f32 (fp32 accumulate; fp16x2 split MFMAs, bf16x3 where fp16's range does not hold)",
         "solve_rate": met["solve_rate"],
-        "replicas_identical": replicas,
+        "params_check": replicas,
         "peak_hbm_gb": torch.cuda.max_memory_allocated() / 1e9,
     }
     side = write_side_file(f"mappo_{workload}_n{world}_rank{rank}", full)
@@ -412,26 +415,29 @@ def compact_leg(full: dict, side: Optional[str]) -> dict:
                      "kernel": r["kernel"].split(" ")[0], "kernel_ms": _sig(r["kernel_ms"]),
                      "mfma_frac": _sig(r["mfma"]["frac"], 3),
                      "per_rank_kernel_ms": [_sig(v) for v in r["per_rank_kernel_ms"]]},
-        "replicas_identical": full.get("replicas_identical"),
+        "params_check": full.get("params_check"),
         "detail": side,
     }
 
 
 def replica_check(net, dist):
-    """After the timed cycle every rank must hold bitwise the same parameters (the gradient all-reduce and
-    the identical Adam steps keep the replicas equal): an fp64 sum and an integer checksum of the flat
-    parameter bits, MIN- and MAX-reduced over ranks.  None at one rank."""
+    """After the timed cycle: are the parameters finite, and (N > 1) does every rank hold bitwise the same
+    parameters (the gradient all-reduce and identical Adam steps keep the replicas equal)?  An fp64 sum
+    and an integer checksum of the flat parameter bits, MIN- and MAX-reduced over ranks."""
     import torch
 
+    finite = torch.isfinite(net.params).all().to(torch.float64).reshape(1)
     if dist is None:
-        return None
+        return {"finite": bool(finite.item()), "identical": None}
+    dist.all_reduce(finite, op=dist.ReduceOp.MIN)
     bits = net.params.view(torch.int32).to(torch.int64)
     idx = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
-    v = torch.stack([net.params.double().sum(), (bits * idx).sum().double()])
+    v = torch.stack([torch.nan_to_num(net.params.double()).sum(), (bits * idx).sum().double()])
     lo, hi = v.clone(), v.clone()
+    local = v.tolist()
     dist.all_reduce(lo, op=dist.ReduceOp.MIN)
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-    return bool(torch.equal(lo, hi))
+    return {"finite": bool(finite.item()), "identical": bool(torch.equal(lo, hi)), "checksum": local}
 
 
 def write_side_file(name: str, obj) -> Optional[str]:

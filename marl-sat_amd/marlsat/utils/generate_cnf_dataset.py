@@ -52,11 +52,30 @@ def generate_sat_clauses(num_vars: int, num_clauses: int, clause_size: int = 3,
     return np.asarray(_planted_clauses(num_vars, num_clauses, clause_size, rnd), dtype=np.int32)
 
 
+def has_isolated_variable(clauses: np.ndarray, num_vars: int) -> bool:
+    """True when some variable 1..num_vars occurs in no clause of the (C, k) literal array."""
+    return bool((np.bincount(np.abs(np.asarray(clauses)).ravel() - 1, minlength=num_vars) == 0).any())
+
+
 def generate_problem_pool(num_vars: int, num_clauses: int, num_problems: int, size_id: int = 0,
-                          clause_size: int = 3) -> np.ndarray:
-    """(N, C, k) int32 pool with seed = 1000*size_id + i (BASELINE.md §2 input spec)."""
-    return np.stack([generate_sat_clauses(num_vars, num_clauses, clause_size, 1000 * size_id + i)
-                     for i in range(num_problems)])
+                          clause_size: int = 3, skip_isolated: bool = False) -> np.ndarray:
+    """(N, C, k) int32 pool with seed = 1000*size_id + i (BASELINE.md §2 input spec).
+
+    skip_isolated: pass over the seeds whose instance leaves a variable in no clause (the generator allows
+    it: uf200-860 seed 3090 leaves variable 126 unused) and take the next ones.  Such a variable, assigned
+    0, is an all-zero row through every layer of the network while the biases are at their zero init:
+    each LayerNorm (learner:27-82, eps 1e-6) then scales its gradient by rsqrt(1e-6) = 1000, and at 16
+    layers the reference's gradient reaches ~1e44 (float64 oracle), past fp32 range -- the first Adam
+    step of a run that samples it is non-finite in the reference and here alike.
+    """
+    out, seed = [], 1000 * size_id
+    while len(out) < num_problems:
+        cl = generate_sat_clauses(num_vars, num_clauses, clause_size, seed)
+        seed += 1
+        if skip_isolated and has_isolated_variable(cl, num_vars):
+            continue
+        out.append(cl)
+    return np.stack(out)
 
 
 def generate_cnf_dataset_sat(num_files: int, num_vars: int, num_clauses: int, save_dir: str,

@@ -50,6 +50,7 @@ def test_two_rank_learner_equals_union(tmp_path):
     ranks = [torch.load(os.path.join(tmp_path, f"rank{k}.pt"), weights_only=True) for k in range(2)]
     # replicas stay identical
     assert torch.equal(ranks[0]["final"], ranks[1]["final"])
+    assert torch.isfinite(ranks[0]["final"]).all()
     for a, b in zip(ranks[0]["trace"], ranks[1]["trace"]):
         assert torch.equal(a["params"], b["params"]) and torch.equal(a["grads"], b["grads"])
     # union run, world 1
@@ -100,3 +101,25 @@ def test_two_rank_learner_equals_union(tmp_path):
         s_ = sums.cpu().numpy() / np.array([idx.numel(), idx.numel() * A, idx.numel() * A])
         e, k = divmod(s, losses_sharded.shape[1])
         np.testing.assert_allclose(losses_sharded[e, k].numpy(), s_, rtol=1e-5, atol=1e-8, err_msg=f"step {s}")
+
+
+@pytest.mark.parametrize("H", [64, 128])
+def test_two_rank_train_cycles_keep_replicas_identical(tmp_path, H):
+    """The bench's path at 2 ranks (own env shards and rollouts, two full train cycles, gradient
+    all-reduce before every Adam step): every Adam step starts from bitwise identical parameters on both
+    ranks and applies a bitwise identical all-reduced gradient, at H = 64 (fp32 kernels) and H = 128
+    (fp16x2 / bf16x3 kernels)."""
+    env = dict(os.environ, MARLSAT_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(HERE, "dist_replica_worker.py"),
+           str(tmp_path), str(H)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    ranks = [torch.load(os.path.join(tmp_path, f"rank{k}.pt"), weights_only=True) for k in range(2)]
+    assert torch.equal(ranks[0]["init"], ranks[1]["init"])
+    assert len(ranks[0]["trace"]) == len(ranks[1]["trace"]) > 0
+    for s, (a, b) in enumerate(zip(ranks[0]["trace"], ranks[1]["trace"])):
+        assert torch.equal(a["params"], b["params"]), f"Adam step {s}: parameters differ across ranks"
+        assert torch.equal(a["grads"], b["grads"]), f"Adam step {s}: all-reduced gradients differ across ranks"
+    assert torch.equal(ranks[0]["final"], ranks[1]["final"])
+    assert torch.isfinite(ranks[0]["final"]).all()
