@@ -80,6 +80,20 @@ __device__ __forceinline__ void glds16_async_s(const void *sbase, unsigned voff,
         : "memory");
 }
 
+// Two pieces: sbase0 -> lds, sbase1 -> lds + STEP bytes, same per-lane offset, M0 written once per pair.
+template <int STEP>
+__device__ __forceinline__ void glds16_async_s2(const void *sbase0, const void *sbase1, unsigned voff,
+                                                const void *lds) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+        "s_add_u32 m0, m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase0), "s"(sbase1), "s"(dst), "n"(STEP)
+        : "memory");
+}
+
 // s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory operations are done.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

@@ -377,18 +377,17 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     // (p = (NI w + e) % 8).  Lane -> unit 16 p + (lane >> 2), LDS chunk lane & 3 = source chunk
     // (lane & 3) ^ f((lane >> 4) & 3).
     const unsigned lpart = (unsigned)(lane >> 2) * 2u, chb = 16u * ((lane & 3) ^ gswz16((lane >> 4) & 3));
+    // piece x = NIW w + e covers W^T rows 16 x .. 16 x + 15 and LDS bytes [1 KiB x, +1 KiB) of the buffer:
+    // both linear in x, so the pieces go in pairs with one M0 setup and no per-piece index arithmetic
     auto issueW = [&](int s, int buf) {
         const bool hid = s < nsh;
-        const uint16_t *W = hid ? a.whT : a.wiT;
         const int Kp = hid ? H : a.kxp;
-        const int k0 = hid ? 32 * s : 32 * (s - nsh);
+        const uint16_t *bw = (hid ? a.whT + 32 * s : a.wiT + 32 * (s - nsh)) + (size_t)(16 * NIW * w) * Kp;
         const unsigned voff = lpart * (unsigned)Kp + chb;
 #pragma unroll
-        for (int e = 0; e < NIW; ++e) {
-            const int x = NIW * w + e, img = x >> 3, p = x & 7, q = img / 3, gt = img - 3 * q;
-            const uint16_t *base = W + ((size_t)q * 3 * H + gt * H + 16 * p) * Kp + k0;
-            glds16_async_s(base, voff, &Bs[(buf * NI + img) * IMG + 64 * p]);
-        }
+        for (int e = 0; e < NIW; e += 2)
+            glds16_async_s2<1024>(bw + (size_t)(16 * e) * Kp, bw + (size_t)(16 * e + 16) * Kp, voff,
+                                  &Bs[buf * NI * IMG + 64 * (NIW * w + e)]);
     };
     f32x4g acc[4][8];
 #pragma unroll
@@ -425,7 +424,22 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         dchunk[e] = (lane & 7) ^ ((r >> 1) & 5);
         dsrc[e] = nullptr;
     }
+    // full tiles whose step lies inside one segment: a wave-uniform base and per-lane 32-bit offsets
+    // (precomputed per source leading dimension); the last tile and a step straddling segments take the
+    // per-lane form below
+    const bool full = row0 + TR <= a.R;
     auto issueA = [&](int st) {
+        const int k = (st - nsh) * 32;
+        if (full && (st < nsh || k + 32 <= w0)) {
+            const bool h = st < nsh;
+            const int ld = h ? a.ldp : a.seg_ld[0];
+            const float *b = (h ? hp + 32 * st : sg0 + k) + (size_t)row0 * ld;
+            uint4 *dst = &As[(st % 3) * ASL + 64 * 2 * w];
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                glds16_async_s(b, (unsigned)(drow[e] * ld + 4 * dchunk[e]) * 4u, dst + 64 * e);
+            return;
+        }
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             const int rr = row0 + drow[e], rc = rr < a.R ? rr : a.R - 1;
