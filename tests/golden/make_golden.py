@@ -12,7 +12,15 @@ importable without JAX:
   * ``verify_solution`` / ``parse_cnf_file`` src/test/verify_solutions.py:5-81
       -> clause_truth.npz: per-clause truth (each clause checked alone),
       formula satisfiability and verify_solution verdicts for random and
-      satisfying assignments; parse_cnf.json: parsed clause lists.
+      satisfying assignments; parse_cnf.json: parsed clause lists;
+  * ``SATEnv._find_factors`` / ``_create_agent_groups`` / ``_calculate_obs_dim``
+      src/envs/multi_agent_sat_env.py:286-343 (pure Python methods, loaded
+      through ``ast`` from the class body -- the module imports jax) ->
+      agent_groups.json: the partition of every V in 1..256 for the explicit
+      VARS_PER_AGENT values and the auto mode, and the obs dim;
+  * ``parse_cnf`` src/utils/data_parser.py:8-42 (pure Python, loaded through
+      ``ast`` without the module's jax import) -> data_parser.json: the
+      clauses it returns for DIMACS texts the reference accepts.
 
 Usage:  python tests/golden/make_golden.py [--reference /root/reference]
 """
@@ -52,6 +60,22 @@ def load_generator(ref: str):
     ns: dict = {}
     exec(compile(ast.Module(body=keep, type_ignores=[]), path, "exec"), ns)
     return ns["generate_sat_cnf"]
+
+
+def load_defs(ref: str, rel: str, names, cls=None):
+    """Function definitions ``names`` (of class ``cls``'s body when given) compiled alone: none of the
+    module's imports run.  ``math`` and ``typing`` names are provided for their bodies / annotations."""
+    import math
+    import typing
+
+    path = os.path.join(ref, rel)
+    tree = ast.parse(open(path).read(), path)
+    body = tree.body if cls is None else next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == cls).body
+    keep = [n for n in body if isinstance(n, ast.FunctionDef) and n.name in names]
+    assert len(keep) == len(names), [n.name for n in keep]
+    ns: dict = {"math": math, **{k: getattr(typing, k) for k in ("Tuple", "List", "Dict", "Optional")}}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), path, "exec"), ns)
+    return [ns[n] for n in names]
 
 
 def load_module(ref: str, rel: str, name: str):
@@ -143,6 +167,61 @@ def main():
         os.unlink(tmp)
     with open(os.path.join(HERE, "parse_cnf.json"), "w") as f:
         json.dump({"text": text, "clauses": parsed}, f)
+    # ---- agent partitions (SATEnv._create_agent_groups, env:286-343) ------------------------------
+    import contextlib
+    import io
+
+    find_factors, create_groups, obs_dim = load_defs(
+        args.reference, "src/envs/multi_agent_sat_env.py",
+        ["_find_factors", "_create_agent_groups", "_calculate_obs_dim"], cls="SATEnv")
+
+    class _Env:  # the methods' `self`: only the attributes they read
+        _find_factors = find_factors
+        _create_agent_groups = create_groups
+        _calculate_obs_dim = obs_dim
+
+    parts = []
+    for V in range(1, 257):
+        for vpa in (None, 1, 2, 3, 4, 5, 7, 8, 10, 12, 16, 25, 64):
+            e = _Env()
+            with contextlib.redirect_stdout(io.StringIO()):  # the reference prints its mode
+                groups = e._create_agent_groups(V, vpa)
+            assert list(groups) == [f"agent_{i}" for i in range(len(groups))]
+            flat = [v for i in range(len(groups)) for v in groups[f"agent_{i}"]]
+            assert flat == list(range(V)), (V, vpa)  # contiguous, in agent order: the sizes say it all
+            runs = []  # run-length encoded group sizes [[size, count], ...]
+            for i in range(len(groups)):
+                n = len(groups[f"agent_{i}"])
+                if runs and runs[-1][0] == n:
+                    runs[-1][1] += 1
+                else:
+                    runs.append([n, 1])
+            parts.append({"V": V, "vpa": vpa, "runs": runs})
+    e = _Env()
+    e.num_vars, e.num_clauses = 200, 860
+    with open(os.path.join(HERE, "agent_groups.json"), "w") as f:
+        json.dump({"partitions": parts, "obs_dim_uf200": e._calculate_obs_dim(),
+                   "factors": {str(n): e._find_factors(n) for n in (1, 12, 36, 97, 200, 256)}}, f,
+                  separators=(",", ":"))
+
+    # ---- data_parser.parse_cnf (data_parser.py:8-42) ------------------------------------------------
+    (ref_parse,) = load_defs(args.reference, "src/utils/data_parser.py", ["parse_cnf"])
+    texts = ["c two comments\nc here\n" + gen(20, 91, 3, seed=5) + "\n",
+             gen(8, 20, 3, seed=7),  # no trailing newline
+             "p cnf 5 3\n  1 -2 3 0  \n-4 5 0\n c indented comment\n2 0\n",  # ragged clauses, spaces
+             "c x\np  cnf  3  2 \n1 2 -3 0\n-1 -2 3 0\n"]
+    out = []
+    for text in texts:
+        with tempfile.NamedTemporaryFile("w", suffix=".cnf", delete=False) as f:
+            f.write(text)
+            tmp = f.name
+        try:
+            V, C, clauses = ref_parse(tmp)
+        finally:
+            os.unlink(tmp)
+        out.append({"text": text, "num_vars": V, "num_clauses": C, "clauses": clauses})
+    with open(os.path.join(HERE, "data_parser.json"), "w") as f:
+        json.dump(out, f)
     print("golden fixtures written to", HERE)
 
 

@@ -136,3 +136,41 @@ def test_entropy_schedule_matches_oracle(cfg):
 
     for u in range(0, cfg["NUM_UPDATES"] + 3):
         assert ent_coef_at(u, cfg) == pytest.approx(om.ent_coef(u, cfg), rel=1e-12, abs=1e-15)
+
+
+def test_agent_partitions_match_reference_fixture():
+    """tests/golden/agent_groups.json: SATEnv._create_agent_groups / _find_factors / _calculate_obs_dim
+    (env:286-343) run from the reference's own source for every V in 1..256 and each VARS_PER_AGENT
+    (None = the auto mode): the build's partition and the oracle's, group for group."""
+    import math
+
+    from marlsat.envs.multi_agent_sat_env import _find_factors, create_agent_groups
+    from oracle.sat_env import create_agent_groups as oracle_groups
+
+    g = json.load(open(os.path.join(GOLDEN, "agent_groups.json")))
+    for rec in g["partitions"]:
+        V, vpa = rec["V"], rec["vpa"]
+        want, start = {}, 0
+        for n, count in rec["runs"]:
+            for _ in range(count):
+                want[f"agent_{len(want)}"] = list(range(start, start + n))
+                start += n
+        assert create_agent_groups(V, vpa) == want, (V, vpa)
+        assert oracle_groups(V, vpa) == want, (V, vpa)
+    for n, f in g["factors"].items():
+        assert _find_factors(int(n)) == f
+    assert g["obs_dim_uf200"] == 2 * 200 + 860
+    # the BASELINE configs (SURVEY.md §8 table): uf200 with VARS_PER_AGENT 8 -> 25 agents of 8
+    uf200 = next(r for r in g["partitions"] if r["V"] == 200 and r["vpa"] == 8)
+    assert uf200["runs"] == [[8, 25]] and math.ceil(200 / 8) == 25
+
+
+def test_parse_cnf_matches_reference_data_parser_fixture(tmp_path):
+    """tests/golden/data_parser.json: the reference's own ``parse_cnf`` (data_parser.py:8-42) on texts it
+    accepts (comments, no trailing newline, ragged clauses, extra spaces in the header and lines)."""
+    from marlsat.utils.data_parser import parse_cnf
+
+    for i, rec in enumerate(json.load(open(os.path.join(GOLDEN, "data_parser.json")))):
+        p = tmp_path / f"t{i}.cnf"
+        p.write_text(rec["text"])
+        assert parse_cnf(str(p)) == (rec["num_vars"], rec["num_clauses"], rec["clauses"]), i
