@@ -211,7 +211,11 @@ __device__ __forceinline__ void stv(float *__restrict__ p, const float *o) {
 }
 
 // One row of the backward in the vector column layout (columns PER * lane + u); same arithmetic per
-// element as the scalar body of gru_ln_bwd_kernel below.
+// element as the scalar body of gru_ln_bwd_kernel below.  Row means multiply by 1 / H (exact: H is a
+// power of two, so x * 2^-k == x / 2^k bit for bit) instead of an IEEE division each: var cell -3..-8 %,
+// clause cell -2..-3 % (profiles/r03_ab_gru_bwd_recip.log; profiles/r03_ab_gru_bwd_modes.log, mode 0).  Measured there and not kept: the
+// forward's v_exp / v_rcp gate forms (clause cell +5 %: the transcendental unit, not the division
+// sequence, is the contended resource) and DPP wave reductions instead of the shuffles (neutral).
 template <int PER, int NQ, int NF, int NQT>
 __device__ __forceinline__ void bwd_row_vec(const float *__restrict__ gi, const float *__restrict__ h,
                                             const float *__restrict__ g, const float *__restrict__ scale,
@@ -245,8 +249,8 @@ __device__ __forceinline__ void bwd_row_vec(const float *__restrict__ gi, const 
     }
     s1 = wave_sum_f32(s1);
     s2 = wave_sum_f32(s2);
-    const float mean = s1 / (float)H;
-    const float var = fmaxf(s2 / (float)H - mean * mean, 0.0f);
+    const float mean = s1 * (1.0f / (float)H);
+    const float var = fmaxf(s2 * (1.0f / (float)H) - mean * mean, 0.0f);
     const float rs = rsqrtf(var + 1e-6f);
     float xh[PER], dxh[PER];
     float a1 = 0.f, a2 = 0.f;
@@ -259,8 +263,8 @@ __device__ __forceinline__ void bwd_row_vec(const float *__restrict__ gi, const 
         pq[0][u] += dyv[u] * xh[u];
         pq[1][u] += dyv[u];
     }
-    a1 = wave_sum_f32(a1) / (float)H;
-    a2 = wave_sum_f32(a2) / (float)H;
+    a1 = wave_sum_f32(a1) * (1.0f / (float)H);
+    a2 = wave_sum_f32(a2) * (1.0f / (float)H);
     float rmax = 0.f;
     float o_an[PER], o_ar[PER], o_az[PER], o_anr[PER], o_dh[PER];
 #pragma unroll
@@ -362,8 +366,8 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
         }
         s1 = wave_sum_f32(s1);
         s2 = wave_sum_f32(s2);
-        const float mean = s1 / (float)H;
-        const float var = fmaxf(s2 / (float)H - mean * mean, 0.0f);
+        const float mean = s1 * (1.0f / (float)H);
+        const float var = fmaxf(s2 * (1.0f / (float)H) - mean * mean, 0.0f);
         const float rs = rsqrtf(var + 1e-6f);
         float xh[PER], dxh[PER];
         float a1 = 0.f, a2 = 0.f;
@@ -377,8 +381,8 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
             pq[0][u] += dyv[u] * xh[u];
             pq[1][u] += dyv[u];
         }
-        a1 = wave_sum_f32(a1) / (float)H;
-        a2 = wave_sum_f32(a2) / (float)H;
+        a1 = wave_sum_f32(a1) * (1.0f / (float)H);
+        a2 = wave_sum_f32(a2) * (1.0f / (float)H);
         float rmax = 0.f;  // largest |dG| of the row (rexp)
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
