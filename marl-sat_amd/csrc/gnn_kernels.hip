@@ -30,11 +30,16 @@ __global__ void __launch_bounds__(kRowThreads)
 clause_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ src_neg, int lds_,
                      const int *__restrict__ slots, float *__restrict__ dst, int ldd, int Nc, int H, int merged,
                      int accumulate) {
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
     const int W = merged ? H : 2 * H;
-    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < Nc; c += gridDim.x * 4) {
+    // two clause rows per wave, one per 32-lane half: twice the independent slot -> row load chains in
+    // flight per wave (the gather is latency-bound at full occupancy), and the merged form (W = H) keeps
+    // every lane busy
+    for (int c0 = 2 * (blockIdx.x * 4 + (threadIdx.x >> 6)); c0 < Nc; c0 += gridDim.x * 8) {
+        const int c = c0 + half;
+        if (c >= Nc) continue;
         const int s0 = slots[3 * (size_t)c], s1 = slots[3 * (size_t)c + 1], s2 = slots[3 * (size_t)c + 2];
-        for (int j = lane * 4; j < W; j += 256) {
+        for (int j = l32 * 4; j < W; j += 128) {
             const int want = j < H ? 0 : 1;  // split: first half positive literals, second negative
             const int col = j < H ? j : j - H;
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
