@@ -70,6 +70,64 @@ clause_gather_kernel(const float *__restrict__ src_pos, const float *__restrict_
     }
 }
 
+// Two var rows per wave (H % 128 == 0), one per 32-lane half: each half walks its row's whole entry
+// list in ascending order, eight entry rows in flight, and adds each into the positive or the negative
+// accumulator by the entry's sign bit -- per output the same adds in the same order as the kernel below
+// (bitwise equal), with twice the rows and the load chains of a wave in flight.
+__global__ void __launch_bounds__(kRowThreads)
+var_gather_hw_kernel(const float *__restrict__ src_pos, const float *__restrict__ src_neg, int lds_,
+                     const int *__restrict__ ptr, const int *__restrict__ inc, float *__restrict__ dst_pos,
+                     float *__restrict__ dst_neg, int ldd, int Nv, int H, int accumulate) {
+    __shared__ int s_idx[4][64];  // per wave: each half's current chunk of 32 entries
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
+    for (int v0 = 2 * (blockIdx.x * 4 + wv); v0 < Nv; v0 += gridDim.x * 8) {  // wave-uniform trip count
+        const int v = v0 + half;
+        const bool ok = v < Nv;
+        const int e0 = ok ? ptr[v] : 0, ne = ok ? ptr[v + 1] - e0 : 0;
+        const int nmax = max(__builtin_amdgcn_readlane(ne, 0), __builtin_amdgcn_readlane(ne, 32));
+        for (int col = l32 * 4; col < H; col += 128) {
+            float4 ap = make_float4(0.f, 0.f, 0.f, 0.f), an = ap;
+            for (int cb = 0; cb < nmax; cb += 32) {
+                const int n = min(32, ne - cb);  // this half's entries in the chunk (<= 0: none)
+                s_idx[wv][lane] = l32 < n ? inc[e0 + cb + l32] : 0;
+                const int nm = min(32, nmax - cb);
+                for (int k = 0; k < nm; k += 8) {
+                    float4 x[8];
+                    int sg[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int kk = k + u;
+                        const int sl = s_idx[wv][32 * half + (kk < 32 ? kk : 31)];
+                        sg[u] = kk < n ? (sl & 1) : -1;  // -1: no entry
+                        const float *src = (sl & 1) ? src_neg : src_pos;
+                        x[u] = sg[u] >= 0 ? *reinterpret_cast<const float4 *>(src + (size_t)(sl >> 1) * lds_ + col)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (sg[u] == 0) {
+                            ap.x += x[u].x; ap.y += x[u].y; ap.z += x[u].z; ap.w += x[u].w;
+                        } else if (sg[u] == 1) {
+                            an.x += x[u].x; an.y += x[u].y; an.z += x[u].z; an.w += x[u].w;
+                        }
+                    }
+                }
+            }
+            if (ok) {
+                float4 *dp = reinterpret_cast<float4 *>(dst_pos + (size_t)v * ldd + col);
+                float4 *dn = reinterpret_cast<float4 *>(dst_neg + (size_t)v * ldd + col);
+                if (accumulate) {
+                    const float4 o = *dp, q = *dn;
+                    ap.x += o.x; ap.y += o.y; ap.z += o.z; ap.w += o.w;
+                    an.x += q.x; an.y += q.y; an.z += q.z; an.w += q.w;
+                }
+                *dp = ap;
+                *dn = an;
+            }
+        }
+    }
+}
+
 // CSR over var rows: entries (clause_row << 1) | neg.  One wave per var row:
 //   dst_pos[v] (+)= sum_{pos entries} src_pos[c],  dst_neg[v] (+)= sum_{neg entries} src_neg[c]
 // (src_pos == src_neg: both halves gather the same H-wide clause rows).
@@ -717,6 +775,14 @@ extern "C" int msat_var_gather2(const float *src_pos, const float *src_neg, int3
                      ld_dst % 4 == 0 && a16(src_pos) && a16(src_neg) && a16(dst_pos) && a16(dst_neg) &&
                      ld_src >= H && ld_dst >= H,
                  "bad var_gather args");
+    // two rows per wave where a half-wave spans a row (profiles/r03_ab_var_gather_halfwave.log: forward
+    // 401 -> 359 us on the uf100 training batch shape, the backward's accumulating form unchanged)
+    if (H % 128 == 0) {
+        hipLaunchKernelGGL(var_gather_hw_kernel, dim3(grid_rows(num_var_rows)), dim3(kRowThreads), 0,
+                           (hipStream_t)stream, src_pos, src_neg, ld_src, ptr, inc, dst_pos, dst_neg, ld_dst,
+                           num_var_rows, H, accumulate);
+        return check_launch("var_gather_hw_kernel");
+    }
     hipLaunchKernelGGL(var_gather_kernel, dim3(grid_rows(num_var_rows)), dim3(kRowThreads), 0, (hipStream_t)stream,
                        src_pos, src_neg, ld_src, ptr, inc, dst_pos, dst_neg, ld_dst, num_var_rows, H, accumulate);
     return check_launch("var_gather_kernel");
