@@ -280,10 +280,13 @@ __device__ __forceinline__ float ftanh_fast(float x) {  // 2 sigma(2x) - 1, satu
 // W^T [2][3H][Kp] (Kp % 32 == 0) by LDS-DMA as per-(plane, gate) images [128 units][4 chunks of 8 k]
 // (64-byte rows, chunk c at slot c ^ f((u >> 2) & 3), f = {0, 2, 3, 1}), double-buffered.
 //
-// Operands: x = x1 + x2, x1 = fp16(x), x2 = fp16(x - x1) (22 significant bits, x - x1 exact); the
+// Operands: x = x1 + x2, x1 = fp16(x), x2 = fp16(x - x1) (x - x1 exact; 22 significant bits while x2
+// stays in fp16's normal range, i.e. |x| >~ 2^-3; the activations are not scaled, so for smaller |x| the
+// low half is subnormal and the representation error is absolute, <= 2^-25 per element); the
 // weights are scaled by 2^kH2Shift before their split (msat_split_f16x2_t) and the sums by 2^-kH2Shift
 // after (both exact).  Three MFMAs per (gate, column tile) block, a1b2 a2b1 a1b1; the dropped a2b2 and
-// the representation residuals are <= 3 * 2^-22 |ab| per product, under the fp32 accumulation error of
+// the representation residuals are <= 3 * 2^-22 |ab| per product (plus the absolute term above for small
+// activations), under the fp32 accumulation error of
 // a 288..416-deep dot product (tests/test_gnn_gpu.py at L = 16 bounds the network against the fp32 CPU
 // oracle).  Against bf16x3: half the MFMAs (3 vs 6), 48 instead of 72 KiB of weights per step.
 // fp16's range is checked, not assumed: a tile that loads an activation with |a| >= 2^15, or whose
