@@ -284,6 +284,13 @@ def mappo_roofline(dom: dict, workload: str) -> dict:
     return r
 
 
+def progress(rank: int, msg: str) -> None:
+    """A line on stderr per bench phase (rank 0): long silent stretches (the MAPPO legs run minutes without
+    output) are otherwise indistinguishable from a hang to a watchdog; stdout keeps only the JSON line."""
+    if rank == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
     """One timed MAPPO train cycle (after one warm-up cycle) on the stated config."""
     import torch
@@ -316,8 +323,10 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
     learner = MAPPOLearner(cfg, env, net, pool, dist=comm)
     rs = learner.init_runner_state(PRNGKey(77 + rank))
     gen = torch.Generator().manual_seed(99 + rank)
+    progress(rank, f"mappo {workload} x {B} envs, T = {T}: warm-up cycle (1 epoch)")
     learner.cfg["UPDATE_EPOCHS"] = 1  # warm-up cycle (every kernel and buffer shape), one epoch
     rs, _ = learner.train_cycle(rs, 0, gen)
+    progress(rank, f"mappo {workload}: timed cycle ({E} epochs)")
     learner.cfg["UPDATE_EPOCHS"] = E
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
@@ -579,6 +588,8 @@ def run_cpu_baselines(args) -> dict:
     leg's size (``mappo_cpu_baseline``)."""
     from marlsat.utils.generate_cnf_dataset import generate_problem_pool
 
+    progress(0, f"CPU baselines ({args.cpu_budget:g} s budget)")
+
     names = MIXED if args.workload == "mixed" else (args.workload,)
     rates = []
     for name in names:
@@ -682,6 +693,7 @@ def main():
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {dist.get_world_size()} ranks")
 
+    progress(rank, f"env leg: {args.workload}, {world} rank(s)")
     r = env_leg(args, rank, world, dist)
     legs = []
     for spec in filter(None, args.mappo.split(",")):
