@@ -387,7 +387,9 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
                   int packed, const float *__restrict__ feat, int ldf, int *__restrict__ rexp) {
     constexpr int NQT = NQ + 3 * NF, QC = NQ;  // partial rows; LDS reduction in chunks of QC rows
     __shared__ float s_part[4][QC * 64 * PER];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // w through readfirstlane: the row index r is then wave-uniform to the compiler, so every per-row base
+    // address (tape, h, dy, outputs, the features) is scalar arithmetic and the features scalar loads
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float pq[NQT][PER];
 #pragma unroll
     for (int q = 0; q < NQT; ++q)
