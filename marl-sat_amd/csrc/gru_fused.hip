@@ -343,12 +343,14 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 }
 
 // The activations go through LDS as well.  Each step's [128 rows][32 k] fp32 tile (16 KiB) is fetched by
-// LDS-DMA three steps ahead into one of three slots ([row][8 chunks of 16 B], chunk c of row r at slot
+// LDS-DMA three steps ahead into one of four slots ([row][8 chunks of 16 B], chunk c of row r at slot
 // c ^ ((r >> 1) & 5): conflict-free ds_read_b128 for the register-A lane map), and split from LDS in the
 // middle of the step before its use.  With no registers in flight across steps, the step end waits only
 // for the next step's weights and the activations of step s + 2 (vmcnt(2)): the activation fetches get
-// 2.5 steps of lead.  128-row tiles of 8 waves (16 rows each), one workgroup per CU: 96 KiB of
-// double-buffered weights + 48 KiB of activation slots.
+// 2.5 steps of lead.  The input steps run first and h's four quarters last, so at the epilogue the four
+// slots still hold h: the gate algebra reads it there instead of fetching the rows again (512 B per
+// row).  128-row tiles of 8 waves (16 rows each), one workgroup per CU: 96 KiB of double-buffered
+// weights + 64 KiB of activation slots, the whole LDS.
 //
 // Measured and not kept: activations to registers instead of LDS (-0.5..-1 %),
 // 64-row "ping-pong" tiles at two workgroups per CU (5-7 % slower), 16-wave tiles (5-9 % slower),
@@ -362,7 +364,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     constexpr int TR = 16 * NW;          // tile rows
     __shared__ uint4 Bs[2 * NI * IMG];   // 48 KiB per buffer
     constexpr int ASL = TR * 8;          // uint4 per activation slot (128 B per row)
-    __shared__ uint4 As[3 * ASL];
+    __shared__ uint4 As[4 * ASL];        // four activation slots: step s in slot s & 3
     const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int row0 = tile * TR, wr = 16 * w;
@@ -371,8 +373,10 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         if (t == 0) *flag = 1;
         return;
     }
+    // step order: the input steps 0 .. nin - 1 first, then the hidden steps (h's four 32-column quarters),
+    // whose activation slots still hold all of h at the epilogue (no refetch of h)
     constexpr int nsh = H / 32;
-    const int ns = nsh + a.kxp / 32;
+    const int nin = a.kxp / 32, ns = nin + nsh;
     const float *const hp = a.hp, *const sg0 = a.seg[0], *const sg1 = a.seg[1], *const sg2 = a.seg[2];
     const int w0 = a.seg_w[0], w01 = a.seg_w[0] + a.seg_w[1], kx_end = a.Kx;
     // weight DMA: 8 NI wave-instructions (1 KiB = 16 units x 4 chunks) per step, NI per wave;
@@ -383,9 +387,9 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     // piece x = NIW w + e covers W^T rows 16 x .. 16 x + 15 and LDS bytes [1 KiB x, +1 KiB) of the buffer:
     // both linear in x, so the pieces go in pairs with one M0 setup and no per-piece index arithmetic
     auto issueW = [&](int s, int buf) {
-        const bool hid = s < nsh;
+        const bool hid = s >= nin;
         const int Kp = hid ? H : a.kxp;
-        const uint16_t *bw = (hid ? a.whT + 32 * s : a.wiT + 32 * (s - nsh)) + (size_t)(16 * NIW * w) * Kp;
+        const uint16_t *bw = (hid ? a.whT + 32 * (s - nin) : a.wiT + 32 * s) + (size_t)(16 * NIW * w) * Kp;
         const unsigned voff = lpart * (unsigned)Kp + chb;
 #pragma unroll
         for (int e = 0; e < NIW; e += 2)
@@ -401,8 +405,8 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     float amax = 0.f;  // largest |activation| this lane split (range check)
     typedef float f4v __attribute__((ext_vector_type(4)));
     auto asplit = [&](int st, const f4v (&r)[2], uint4 (&f)[2]) {  // branch-free (selects)
-        const int kx = (st - nsh) * 32 + 8 * g;
-        const bool z0 = st >= nsh && kx >= kx_end, z1 = st >= nsh && kx + 4 >= kx_end;
+        const int kx = st * 32 + 8 * g;
+        const bool z0 = st < nin && kx >= kx_end, z1 = st < nin && kx + 4 >= kx_end;
         const f4v zero = {0.f, 0.f, 0.f, 0.f};
         const float4 v0 = __builtin_bit_cast(float4, z0 ? zero : r[0]);
         const float4 v1 = __builtin_bit_cast(float4, z1 ? zero : r[1]);
@@ -413,7 +417,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         f[0] = sp.p[0];
         f[1] = sp.p[1];
     };
-    uint4 fas[2][2];  // split activations of step s in fas[s & 1]
+    uint4 fas[1][2], fnx[2];  // split activations of this step / the next (moved over at the step end)
     // activation DMA, 16 wave-instructions (1 KiB = 8 rows x 8 chunks) per step, 2 per wave;
     // instruction e of wave w: rows 8 x .. 8 x + 7 (x = 2 w + e), lane -> row 8 x + (lane >> 3), LDS slot
     // lane & 7 holding chunk (lane & 7) ^ ((row >> 1) & 5).  Rows past R read row R - 1; k past Kx read
@@ -432,12 +436,12 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     // per-lane form below
     const bool full = row0 + TR <= a.R;
     auto issueA = [&](int st) {
-        const int k = (st - nsh) * 32;
-        if (full && (st < nsh || k + 32 <= w0)) {
-            const bool h = st < nsh;
+        const int k = st * 32;
+        if (full && (st >= nin || k + 32 <= w0)) {
+            const bool h = st >= nin;
             const int ld = h ? a.ldp : a.seg_ld[0];
-            const float *b = (h ? hp + 32 * st : sg0 + k) + (size_t)row0 * ld;
-            uint4 *dst = &As[(st % 3) * ASL + 64 * 2 * w];
+            const float *b = (h ? hp + 32 * (st - nin) : sg0 + k) + (size_t)row0 * ld;
+            uint4 *dst = &As[(st & 3) * ASL + 64 * 2 * w];
 #pragma unroll
             for (int e = 0; e < 2; ++e)
                 glds16_async_s(b, (unsigned)(drow[e] * ld + 4 * dchunk[e]) * 4u, dst + 64 * e);
@@ -447,21 +451,21 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         for (int e = 0; e < 2; ++e) {
             const int rr = row0 + drow[e], rc = rr < a.R ? rr : a.R - 1;
             const float *src;
-            if (st < nsh) {
-                src = hp + (size_t)rc * a.ldp + 32 * st + 4 * dchunk[e];
+            if (st >= nin) {
+                src = hp + (size_t)rc * a.ldp + 32 * (st - nin) + 4 * dchunk[e];
             } else {
-                const int kx = (st - nsh) * 32 + 4 * dchunk[e];
+                const int kx = st * 32 + 4 * dchunk[e];
                 if (kx < w0) src = sg0 + (size_t)rc * a.seg_ld[0] + kx;
                 else if (kx < w01) src = sg1 + (size_t)rc * a.seg_ld[1] + (kx - w0);
                 else if (kx < kx_end) src = sg2 + (size_t)rc * a.seg_ld[2] + (kx - w01);
-                else src = hp + (size_t)rc * a.ldp;  // padding k: any valid row, zeroed at the split
+                else src = hp;  // padding k: one fixed valid line (L2-resident: no HBM bytes), zeroed at the split
             }
-            glds16_async(src, &As[(st % 3) * ASL + 64 * (2 * w + e)]);
+            glds16_async(src, &As[(st & 3) * ASL + 64 * (2 * w + e)]);
         }
     };
     auto lsplit = [&](int st, uint4 (&f)[2]) {  // split step st's activations from its LDS slot
         const int r = wr + l16, sw = (r >> 1) & 5;
-        const uint4 *row = &As[(st % 3) * ASL + 8 * r];
+        const uint4 *row = &As[(st & 3) * ASL + 8 * r];
         f4v v[2];
         v[0] = __builtin_bit_cast(f4v, row[(2 * g) ^ sw]);
         v[1] = __builtin_bit_cast(f4v, row[(2 * g + 1) ^ sw]);
@@ -474,29 +478,12 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     wait_vmcnt<0>();
     barrier_lds();
     lsplit(0, fas[0]);
-    // HVE: the h values of the epilogue (h of each accumulator's (row, unit)) are fetched by LDS-DMA at
-    // the start of the last step, so their HBM latency runs under its MFMAs instead of at the epilogue
-    // (the rows' h passed through the activation slots in steps 0..3 and are long evicted).  In the last
-    // step the three activation slots and the other weight buffer are free: waves 0..5 put their 16 rows
-    // (8 KiB, [row][128]) in the slots, waves 6 and 7 in that buffer.
-    auto hbase = [&](int fb) -> float * {
-        return w < 6 ? reinterpret_cast<float *>(&As[512 * w]) : reinterpret_cast<float *>(&Bs[fb * NI * IMG + 512 * (w - 6)]);
-    };
-    auto issueH = [&](int fb, int z) {  // z = 0, passed from the step so nothing is hoisted into the loop
-        const uint4 *dst = reinterpret_cast<const uint4 *>(hbase(fb));
-        const float *sb = hp + (size_t)row0 * a.ldp;  // wave-uniform base, per-lane 32-bit offsets
-        const int rmax = a.R - 1 - row0;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {  // rows wr + 2 e + (lane >> 5), float4 (lane & 31)
-            const int rr = wr + 2 * e + (lane >> 5) + z, rc = rr < rmax ? rr : rmax;
-            glds16_async_s(sb, 4u * ((unsigned)rc * (unsigned)a.ldp + 4u * (unsigned)(lane & 31)), dst + 64 * e);
-        }
-    };
-    auto pstep = [&](int st, auto hidc, auto parc) {
+    // one 32-k step; two static copies (input, hidden): the weight buffer's parity is a runtime offset and
+    // the next step's split activations are moved into place at the step end, so the accumulators keep
+    // one register assignment through the whole loop (a copy per parity and step kind spilled them)
+    auto pstep = [&](int st, auto hidc) {
         constexpr bool hid = decltype(hidc)::value;
-        constexpr int PB = decltype(parc)::value;  // st & 1
-        const int buf = PB;
-        if (st + 1 == ns) issueH(buf ^ 1, ns - 1 - st);
+        const int buf = st & 1;
         // Stagger of SIMD partners (waves w and w + 4 share a SIMD): waves 4..7 issue the step's DMA
         // before block kDmaLate, so partners' DMA bursts do not coincide (profiles/ab_gru_dma.sh, tape
         // on: -2.9 % clause / -1.1 % var; blocks 4..16 -1..-2.5 %; delaying waves 0..3 too +2 %).
@@ -514,7 +501,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
             const int gt = n >> 3, j = n & 7;
             return Bs[(buf * NI + q * 3 + gt) * IMG + (16 * j + l16) * 4 + slot];
         };
-        uint4 (&fa)[2] = fas[PB];
+        uint4 (&fa)[2] = fas[0];
         {
             // fragments LA = 2 blocks ahead in LA rotating register sets (block n uses set n % LA; each
             // plane's register is refilled for block n + LA right after its last MFMA in block n)
@@ -537,7 +524,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
                 c = h2mma(fa[0], b0, c);  // a1 b1
                 if (n + LA < 24) b0 = bfrag(n + LA, 0);
                 acc[G][j] = c;
-                if (n == 7 && st + 1 < ns) lsplit(st + 1, fas[PB ^ 1]);
+                if (n == 7 && st + 1 < ns) lsplit(st + 1, fnx);
                 if (late && n + 1 == kDmaLate) dma();
                 __builtin_amdgcn_sched_barrier(0);  // keep the blocks in order (the reads lead by one)
             }
@@ -545,26 +532,22 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         // W(st + 1) and A(st + 2) landed (A(st + 3), issued last, may fly); no registers in flight
         if (st + 3 < ns) wait_vmcnt<2>();
         else wait_vmcnt<0>();
+        fas[0][0] = fnx[0];
+        fas[0][1] = fnx[1];
         barrier_lds();
     };
     {
         int st = 0;
 #pragma unroll 1
-        for (; st + 1 < nsh; st += 2) {
-            pstep(st, std::true_type{}, std::integral_constant<int, 0>{});
-            pstep(st + 1, std::true_type{}, std::integral_constant<int, 1>{});
-        }
-        // nsh = 4 is even: the input steps start at parity 0
+        for (; st < nin; ++st) pstep(st, std::false_type{});
 #pragma unroll 1
-        for (; st + 1 < ns; st += 2) {
-            pstep(st, std::false_type{}, std::integral_constant<int, 0>{});
-            pstep(st + 1, std::false_type{}, std::integral_constant<int, 1>{});
-        }
-        if (st < ns) pstep(st, std::false_type{}, std::integral_constant<int, 0>{});
+        for (; st < ns; ++st) pstep(st, std::true_type{});
     }
     {  // range check: |a| < 2^15 keeps a1 = fp16(a) finite with margin.  A ballot per wave and an
        // LDS-only barrier: __syncthreads_or's fence would also wait for the h DMA in flight.
-        __shared__ int wbadl[NW];
+        // the weight buffers are free past the last step's barrier: the flags sit in Bs's last 32 bytes,
+        // beyond the epilogue's stage (LDS is full: 96 KiB of weights + 64 KiB of activation slots)
+        int *const wbadl = reinterpret_cast<int *>(&Bs[2 * NI * IMG]) - NW;
         const bool wb = __ballot(!(amax < 32768.0f)) != 0;
         if (lane == 0) wbadl[w] = wb;
         barrier_lds();
@@ -581,15 +564,21 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     // ---- epilogue.  C/D map: unit u = 16 j + l16, row wr + 4 g + reg.
     float *stage = reinterpret_cast<float *>(Bs) + w * 16 * 132;  // [16 rows][132] per wave
     const bool tape = a.g4 != nullptr;
+    // h of each accumulator's (row, unit) from the hidden steps' slots: quarter q (units 32 q ..) is step
+    // nin + q in slot (nin + q) & 3, [row][8 chunks], chunk c of row r at c ^ ((r >> 1) & 5).  All four
+    // landed before the last step's barrier; the stage below lives in Bs, not in the slots.
     float hv[8][4];
     {
-        wait_vmcnt<0>();  // this wave's own h rows have landed
-        const float *hl = hbase(((ns - 1) & 1) ^ 1);
+        const float *Af = reinterpret_cast<const float *>(As);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < 8; ++j) {
+            const int kq = 16 * (j & 1) + l16, sb = ((nin + (j >> 1)) & 3) * ASL;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) hv[j][r] = hl[(4 * g + r) * H + 16 * j + l16];
-        barrier_lds();  // every wave has read its h before any wave's stage (over Bs) is written
+            for (int r = 0; r < 4; ++r) {
+                const int R = wr + 4 * g + r;
+                hv[j][r] = Af[4 * (sb + 8 * R + ((kq >> 2) ^ ((R >> 1) & 5))) + (kq & 3)];
+            }
+        }
     }
     constexpr float sc = 1.0f / (float)(1 << kH2Shift);  // exact power of two
     // packed fp32 (v_pk_mul / v_pk_add on row pairs): no MFMAs run here, so the packed forms halve the
