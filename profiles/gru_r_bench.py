@@ -70,6 +70,11 @@ for cell, R, segs_w, segs_ld in (("clause", RC, (2 * H, 4), (2 * H, 4)), ("var",
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / n
-            print(json.dumps({"cell": cell, "rows": R, "tape": tape, "kernel": name, "ms": round(ms, 4),
-                              "tflops_fp32_equiv": round(flop / ms / 1e9, 1),
-                              "flagged_tiles": int(flags.sum()) if name == "h2r" else None}), flush=True)
+            rec = {"cell": cell, "rows": R, "tape": tape, "kernel": name, "ms": round(ms, 4),
+                   "tflops_fp32_equiv": round(flop / ms / 1e9, 1),
+                   "flagged_tiles": int(flags.sum()) if name == "h2r" else None}
+            if os.environ.get("GRU_CHECKSUM"):  # bit checksums of the outputs (A/B builds must agree)
+                rec["out_bits"] = int(out.view(torch.int32).to(torch.int64).sum())
+                if tape:
+                    rec["g4_bits"] = int(g4.view(torch.int32).to(torch.int64).sum())
+            print(json.dumps(rec), flush=True)
