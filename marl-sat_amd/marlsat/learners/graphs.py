@@ -22,6 +22,7 @@ nothing), not the env's literal-0 quirk.
 from __future__ import annotations
 
 from dataclasses import dataclass
+from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -173,8 +174,11 @@ class GraphBatch:
 
 
 def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor, inst: torch.Tensor,
-             x: torch.Tensor, critic_only: bool = False) -> GraphBatch:
-    """Instantiate the templates for samples (inst (S,), x (S,V) uint8) on the device."""
+             x: torch.Tensor, critic_only: bool = False, totals: Optional[Tuple[int, int, int]] = None) -> GraphBatch:
+    """Instantiate the templates for samples (inst (S,), x (S,V) uint8) on the device.  ``totals`` =
+    the batch's (var rows, clause rows, incidences) when the caller already knows them (the learner
+    plans a minibatch's micro-batches at once, batch_totals): no device -> host read here, so the host
+    keeps queueing work instead of waiting for the GPU to drain."""
     S = int(inst.shape[0])
     G = 1 if critic_only else tpl.G
     dev = inst.device
@@ -185,8 +189,8 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
     tv, tc, te = (tpl.crit_v, tpl.crit_c, tpl.crit_e) if critic_only else (tpl.full_v, tpl.full_c, tpl.full_e)
     _lib.check(_lib.lib.msat_graph_bases(S, inst.data_ptr(), tv.data_ptr(), tc.data_ptr(), te.data_ptr(), sb.data_ptr(),
                                          tot.data_ptr(), _lib.stream_ptr(dev)), "msat_graph_bases")
-    Nv, Nc, nnz = tot.tolist()  # sizes the outputs (one small device -> host read)
-    if min(Nv, Nc, nnz) < 0:  # msat_graph_bases flags a total above INT32_MAX with -1
+    Nv, Nc, nnz = tot.tolist() if totals is None else totals  # sizes the outputs
+    if min(Nv, Nc, nnz) < 0 or max(Nv, Nc, nnz) > 2 ** 31 - 1:  # msat_graph_bases flags an overflow with -1
         raise ValueError(f"graph batch of {S} samples exceeds int32 row indices (var rows, clause rows, incidences "
                          f"= {Nv}, {Nc}, {nnz}; -1 = overflow): use smaller micro-batches")
     out = GraphBatch(S, G, Nv, Nc, nnz,
@@ -210,3 +214,17 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
         out.inc.data_ptr(), out.vbase.data_ptr(), out.nv.data_ptr(), out.cbase.data_ptr(), out.nc.data_ptr(),
         Nv, nnz, _lib.stream_ptr(dev)), "msat_assemble_graph_batch")
     return out
+
+
+def batch_totals(tpl: DeviceTemplates, inst: torch.Tensor, bounds: List[int]) -> List[Tuple[int, int, int]]:
+    """(var rows, clause rows, incidences) of the full-sample batches inst[bounds[i]:bounds[i+1]], the
+    totals msat_graph_bases computes for each, from ONE device -> host read for all of them
+    (int64 sums, so an int32 overflow shows up as a total above INT32_MAX, which assemble refuses)."""
+    if len(bounds) < 2:
+        return []
+    idx = inst.long()
+    cnt = torch.stack((tpl.full_v.index_select(0, idx), tpl.full_c.index_select(0, idx),
+                       tpl.full_e.index_select(0, idx)), 1).to(torch.int64)
+    cs = torch.cat((torch.zeros((1, 3), dtype=torch.int64, device=cnt.device), torch.cumsum(cnt, 0)))
+    at = cs.index_select(0, torch.tensor(bounds, dtype=torch.int64, device=cnt.device))
+    return [tuple(int(v) for v in r) for r in (at[1:] - at[:-1]).tolist()]

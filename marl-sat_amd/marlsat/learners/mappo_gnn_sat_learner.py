@@ -33,7 +33,7 @@ from ..envs.multi_agent_sat_env import ObsDict, ProblemPool, SATEnv, SATState
 from ..random import Key, as_key, split
 from .collectives import allreduce_grads, allreduce_sums, global_moments, world_size
 from .gnn import GNNActorCritic
-from .graphs import DeviceTemplates, GraphBatch, assemble, build_templates
+from .graphs import DeviceTemplates, GraphBatch, assemble, batch_totals, build_templates
 from .ops import gae as device_gae
 
 L_ = _lib.lib
@@ -193,8 +193,8 @@ class MAPPOLearner:
         obs, st = self.env.reset_from_pool(self.pool, self.B, k_reset)
         return RunnerState(st, obs, k_run, 0)
 
-    def _batch(self, pidx: torch.Tensor, x: torch.Tensor, critic_only: bool = False) -> GraphBatch:
-        return assemble(self.tpl, self.pool.packed, self.svf, pidx.contiguous(), x.contiguous(), critic_only)
+    def _batch(self, pidx: torch.Tensor, x: torch.Tensor, critic_only: bool = False, totals=None) -> GraphBatch:
+        return assemble(self.tpl, self.pool.packed, self.svf, pidx.contiguous(), x.contiguous(), critic_only, totals)
 
     def policy(self, st: SATState, key: Key, greedy: bool = False, critic: bool = True):
         """Actor (+ critic) on the current states (learner:391-403): actions, log_probs, values.
@@ -267,11 +267,15 @@ class MAPPOLearner:
         A, M = self.A, self.M
         idx = idx.to(torch.int32)
         net.grads.zero_()
-        for m0 in range(0, idx.numel(), self.micro):
-            mi = idx[m0:m0 + self.micro]
+        # every micro-batch's row totals from one device -> host read per minibatch (assemble would
+        # otherwise read each batch's totals back, and the GPU idled while the host caught up)
+        bounds = list(range(0, idx.numel(), self.micro)) + [idx.numel()]
+        sizes = batch_totals(self.tpl, self.tr["pidx"].reshape(-1).index_select(0, idx.long()), bounds)
+        for m0, m1, tot in zip(bounds[:-1], bounds[1:], sizes):
+            mi = idx[m0:m1]
             S = mi.numel()
             pidx, x, act, olp, g_, vold, tg = self.gather_rows(mi)
-            gb = self._batch(pidx, x)
+            gb = self._batch(pidx, x, totals=tot)
             logits, value, state = net.forward(gb, save=True)
             dlog = torch.empty_like(logits)
             dval = torch.empty_like(value)

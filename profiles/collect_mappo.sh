@@ -11,6 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o m -- python3 $R/bench.py --steps 20 --warmup 5 --cpu-budget 0 --mappo $LEG > $OUT/bench.log 2>&1
 W=${LEG%%:*}
 python3 $R/profiles/mappo_slice.py $OUT/m_kernel_trace.csv $OUT/bench.log $R/gpurun_out/keep/${TAG}_mappo_${W}_slice.json
+python3 $R/profiles/gaps.py $OUT/m_kernel_trace.csv ${GAP_WINDOW_S:-36} ${GAP_MIN_US:-3} > $R/gpurun_out/keep/${TAG}_mappo_${W}_gaps.txt || true
 cp $OUT/m_kernel_stats.csv $R/gpurun_out/keep/${TAG}_mappo_${W}_kernel_stats.csv
 grep '^{' $OUT/bench.log > $R/gpurun_out/keep/${TAG}_mappo_${W}_bench.json
 rm -rf $OUT

@@ -121,3 +121,33 @@ def test_graph_bases_flag_int32_overflow():
     _lib.check(_lib.lib.msat_graph_bases(S, di.data_ptr(), *[c.data_ptr() for c in dc], bases.data_ptr(),
                                          tot.data_ptr(), _lib.stream_ptr()), "graph_bases")
     assert tot.cpu().tolist() == [-1, 5 * S, 7 * S]
+
+
+@pytest.mark.parametrize("V,C,vpa,S,micro", [(20, 91, 10, 77, 20), (50, 218, 10, 64, 64), (100, 430, 10, 33, 7)])
+def test_batch_totals_match_the_device_totals(V, C, vpa, S, micro):
+    """The learner's per-minibatch size plan (graphs.batch_totals, one device -> host read for all its
+    micro-batches) equals what msat_graph_bases computes for each micro-batch, and a batch assembled
+    with the planned totals is identical to one assembled with the device read."""
+    from marlsat import SATEnv
+    from marlsat.learners.graphs import DeviceTemplates, assemble, batch_totals, build_templates
+    from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+
+    N = 16
+    pool = generate_problem_pool(V, C, N, size_id=5)
+    env = SATEnv(V, C, max_steps=10, vars_per_agent=vpa)
+    A = env.num_agents
+    dpool = env.make_pool(pool)
+    tpl = DeviceTemplates(build_templates(pool, V, A), A, "cuda")
+    rng = np.random.default_rng(V + S)
+    inst = torch.from_numpy(rng.integers(0, N, S).astype(np.int32)).cuda()
+    x = torch.from_numpy(rng.integers(0, 2, (S, V)).astype(np.uint8)).cuda()
+    bounds = list(range(0, S, micro)) + [S]
+    plan = batch_totals(tpl, inst, bounds)
+    assert len(plan) == len(bounds) - 1
+    svf = dpool.static_var_features()
+    for (m0, m1), tot in zip(zip(bounds[:-1], bounds[1:]), plan):
+        a = assemble(tpl, dpool.packed, svf, inst[m0:m1].contiguous(), x[m0:m1].contiguous())
+        b = assemble(tpl, dpool.packed, svf, inst[m0:m1].contiguous(), x[m0:m1].contiguous(), totals=tot)
+        assert (a.Nv, a.Nc, a.nnz) == tot
+        for f in ("vfeat", "cfeat", "cdeg", "slots", "ptr", "inc", "vbase", "nv", "cbase", "nc"):
+            assert torch.equal(getattr(a, f), getattr(b, f)), f
