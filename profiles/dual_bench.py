@@ -50,5 +50,8 @@ for name, f, nb in (("dual dgrad", fd, 4.0 * M * (4 * H + 2 * H + 2 * H + 1)),
     b.record()
     torch.cuda.synchronize()
     us = a.elapsed_time(b) / reps * 1e3
-    print(json.dumps({"what": name, "rows": M, "us": round(us, 1), "algorithmic_bytes": nb,
-                      "GBps": round(nb / us / 1e3, 1)}), flush=True)
+    rec = {"what": name, "rows": M, "us": round(us, 1), "algorithmic_bytes": nb, "GBps": round(nb / us / 1e3, 1)}
+    if os.environ.get("DUAL_CHECKSUM"):  # bit checksums of the outputs (A/B builds must agree)
+        outs = (dh, dx) if name == "dual dgrad" else (gW0, gW1)
+        rec["bits"] = [int(o.view(torch.int32).to(torch.int64).sum()) for o in outs]
+    print(json.dumps(rec), flush=True)
