@@ -36,6 +36,7 @@ import glob
 import json
 import os
 import socket
+import statistics
 import subprocess
 import sys
 import time
@@ -323,47 +324,53 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
     learner = MAPPOLearner(cfg, env, net, pool, dist=comm)
     rs = learner.init_runner_state(PRNGKey(77 + rank))
     gen = torch.Generator().manual_seed(99 + rank)
-    progress(rank, f"mappo {workload} x {B} envs, T = {T}: warm-up cycle (1 epoch)")
+    progress(rank, f"mappo {workload} x {B}, T {T}: warm-up")
     learner.cfg["UPDATE_EPOCHS"] = 1  # warm-up cycle (every kernel and buffer shape), one epoch
     rs, _ = learner.train_cycle(rs, 0, gen)
-    progress(rank, f"mappo {workload}: timed cycle ({E} epochs)")
+    progress(rank, f"mappo {workload}: {args.mappo_cycles} timed cycles")
     learner.cfg["UPDATE_EPOCHS"] = E
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
     GNNActorCritic.flops = 0
-    GNNActorCritic.ktimer = {}
-    t0 = time.perf_counter()
-    ev[0].record()
-    rs = learner.rollout(rs)
-    ev[1].record()
-    learner.compute_advantages(rs)
-    ev[2].record()
-    losses, ent = learner.ppo_update(1, gen)
-    ev[3].record()
-    met = learner.metrics(losses, ent)
-    ev[4].record()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    phases = [ev[i].elapsed_time(ev[i + 1]) for i in range(4)]
-    flops = float(GNNActorCritic.flops)
+    GNNActorCritic.ktimer = {}  # per-launch HIP events over every timed cycle
+    cycles = []  # (wall s, [rollout, gae, ppo_update, metrics] ms) per timed cycle
+    for _ in range(args.mappo_cycles):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev[0].record()
+        rs = learner.rollout(rs)
+        ev[1].record()
+        learner.compute_advantages(rs)
+        ev[2].record()
+        losses, ent = learner.ppo_update(1, gen)
+        ev[3].record()
+        met = learner.metrics(losses, ent)
+        ev[4].record()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        cycles.append((time.perf_counter() - t0, [ev[i].elapsed_time(ev[i + 1]) for i in range(4)]))
+    flops = float(GNNActorCritic.flops) / len(cycles)
     kernels = kernel_table(GNNActorCritic.ktimer)
     GNNActorCritic.ktimer = None
-    cycle_ms = sum(phases)
-    dom = next(k for k in kernels if k["peak"])  # the matrix kernel with the most time in the cycle
+    dom = next(k for k in kernels if k["peak"])  # the matrix kernel with the most time in the cycles
     rank_ms = [0.0] * world  # each rank's dominant-kernel average launch time
     rank_ms[rank] = dom["ms_avg"]
-    if dist is not None:
-        t = torch.tensor([elapsed] + phases, dtype=torch.float64, device="cuda")
+    per_cycle = [c[0] for c in cycles]
+    if dist is not None:  # the slowest rank's wall time and phases, per cycle
+        t = torch.tensor([v for c in cycles for v in [c[0]] + c[1]], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, phases = float(t[0]), [float(v) for v in t[1:]]
+        t = t.view(len(cycles), 5).tolist()
+        cycles = [(r[0], r[1:]) for r in t]
+        per_cycle = [c[0] for c in cycles]
         rk = torch.tensor(rank_ms, dtype=torch.float64, device="cuda")
         dist.all_reduce(rk)  # every rank fills its own slot: SUM = gather
         rank_ms = [float(v) for v in rk]
+    elapsed = statistics.median(per_cycle)
+    phases = [statistics.median(c[1][i] for c in cycles) for i in range(4)]
+    cycle_ms = sum(sum(c[1]) for c in cycles)
     replicas = replica_check(net, dist)
     if type(comm).__name__ == "CapiComm":
         comm.destroy()
@@ -378,6 +385,7 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
         "value": 1.0 / elapsed,
         "unit": "updates/s",
         "s_per_update": elapsed,
+        "s_per_update_cycles": per_cycle,
         "adam_steps_per_s": E * n_mb / elapsed,
         "samples_per_s": world * B * T / elapsed,
         "ppo_samples_per_s": world * E * B * T / (phases[2] * 1e-3),
@@ -406,25 +414,27 @@ def _sig(x, n=4):
 
 
 def compact_leg(full: dict, side: Optional[str]) -> dict:
-    """The MAPPO leg as it goes into the JSON line: ~0.8 KB, so both legs fit the driver's 2,000-character
-    tail of stdout.  The full record (per-kernel table, both roofline views) is in the side file."""
+    """The MAPPO leg as it goes into the JSON line: ~0.6 KB, so the env side legs and both MAPPO legs fit the
+    driver's 2,000-character tail (which also holds the run's stderr).  value = 1 / the median of the timed
+    cycles' s_per_update.  The full record (per-kernel table, both roofline views) is in the side file."""
     c, r = full["config"], full["roofline"]
+    ph = full["phase_ms"]
     return {
-        "metric": full["metric"], "value": _sig(full["value"]), "unit": full["unit"],
-        "s_per_update": _sig(full["s_per_update"]), "samples_per_s": _sig(full["samples_per_s"]),
+        "value": _sig(full["value"]),
+        "s_per_update": [_sig(v) for v in full.get("s_per_update_cycles", [full["s_per_update"]])],
+        "s_median": _sig(full["s_per_update"]), "samples_per_s": _sig(full["samples_per_s"]),
         "adam_steps_per_s": _sig(full["adam_steps_per_s"]),
-        "phase_ms": {k: round(v, 1) for k, v in full["phase_ms"].items()},
-        "config": {"workload": c["workload"], "agents": c["num_agents"], "m": c["max_vars_per_agent"],
-                   "envs_per_gpu": c["envs_per_gpu"], "T": c["NUM_STEPS"], "epochs": c["UPDATE_EPOCHS"],
-                   "minibatch": c["MINIBATCH_SIZE"], "H": c["GNN_HIDDEN_DIM"], "L": c["GNN_NUM_MESSAGE_PASSING_STEPS"],
-                   "parallelism": c["parallelism"].split(" ")[0]},
+        "phase_ms": [round(ph[k]) for k in ("rollout", "gae", "ppo_update", "metrics")],
+        "config": f"{c['workload']} A{c['num_agents']} m{c['max_vars_per_agent']} B{c['envs_per_gpu']}/gpu "
+                  f"T{c['NUM_STEPS']} E{c['UPDATE_EPOCHS']} mb{c['MINIBATCH_SIZE']} H{c['GNN_HIDDEN_DIM']} "
+                  f"L{c['GNN_NUM_MESSAGE_PASSING_STEPS']} {c['parallelism'].split(' ')[0]}",
         "roofline": {"bound": r["bound"], "achieved": _sig(r["achieved"]), "peak": r["peak"],
                      "unit": r["unit"].split(" ")[0], "frac": _sig(r["frac"], 3),
                      "traffic": _sig(r["traffic"]) if r["traffic"] else None,
                      "kernel": r["kernel"].split(" ")[0], "kernel_ms": _sig(r["kernel_ms"]),
                      "mfma_frac": _sig(r["mfma"]["frac"], 3),
-                     "per_rank_kernel_ms": [_sig(v) for v in r["per_rank_kernel_ms"]]},
-        "params_check": full.get("params_check"),
+                     "rank_ms": [_sig(v) for v in r["per_rank_kernel_ms"]]},
+        "params_check": {k: v for k, v in (full.get("params_check") or {}).items() if k != "checksum"},
         "detail": side,
     }
 
@@ -439,14 +449,20 @@ def replica_check(net, dist):
     if dist is None:
         return {"finite": bool(finite.item()), "identical": None}
     dist.all_reduce(finite, op=dist.ReduceOp.MIN)
+    # fp64 value sum, and an int64 checksum of the parameter bits reduced AS int64 (a double would keep only
+    # 53 of its bits: a one-ulp difference could vanish); the int64 sum wraps the same way on every rank
     bits = net.params.view(torch.int32).to(torch.int64)
     idx = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
-    v = torch.stack([torch.nan_to_num(net.params.double()).sum(), (bits * idx).sum().double()])
-    lo, hi = v.clone(), v.clone()
-    local = v.tolist()
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-    return {"finite": bool(finite.item()), "identical": bool(torch.equal(lo, hi)), "checksum": local}
+    vsum = torch.nan_to_num(net.params.double()).sum().reshape(1)
+    csum = (bits * idx).sum().reshape(1)
+    local = [float(vsum.item()), int(csum.item())]
+    same = True
+    for t in (vsum, csum):
+        lo, hi = t.clone(), t.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        same = same and bool(torch.equal(lo, hi))
+    return {"finite": bool(finite.item()), "identical": same, "checksum": local}
 
 
 def write_side_file(name: str, obj) -> Optional[str]:
@@ -466,8 +482,9 @@ def write_side_file(name: str, obj) -> Optional[str]:
 MIXED = ("uf50-218", "uf100-430", "uf200-860")  # BASELINE config 5 size classes (1024 envs per GPU of 8192)
 
 
-def env_leg(args, rank, world, dist):
-    """Time K fused env steps (+ auto-reset) over the local shard; returns the measurement dict."""
+def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optional[int] = None):
+    """Time K fused env steps (+ auto-reset) over the local shard; returns the measurement dict.
+    workload / envs override --workload / --envs (the side legs)."""
     import torch
 
     from marlsat import SATEnv
@@ -475,13 +492,15 @@ def env_leg(args, rank, world, dist):
     from marlsat.random import Key
     from marlsat.utils.generate_cnf_dataset import generate_problem_pool
 
-    mixed = args.workload == "mixed"
-    names = MIXED if mixed else (args.workload,)
+    workload = workload or args.workload
+    envs = envs or args.envs
+    mixed = workload == "mixed"
+    names = MIXED if mixed else (workload,)
     if mixed:
-        total = args.envs or 1024
+        total = envs or 1024
         sizes = [total // 3 + (1 if i < total % 3 else 0) for i in range(3)]
     else:
-        sizes = [args.envs or WORKLOADS[args.workload][3]]
+        sizes = [envs or WORKLOADS[workload][3]]
     obs_dtype = torch.int32 if args.obs_dtype == "int32" else torch.int8
     seed = 0x5EED0000 + rank
     classes, pools, pools_np = [], [], []
@@ -577,9 +596,24 @@ def env_leg(args, rank, world, dist):
         per_class.append({"workload": name, "num_vars": e.num_vars, "num_clauses": e.num_clauses,
                           "num_agents": e.num_agents, "vars_per_agent": WORKLOADS[name][2], "envs_per_gpu": b,
                           "algorithmic_bytes_per_env_step": pe})
-    return {"names": names, "sizes": sizes, "elapsed": elapsed, "kern_ms": kern_ms, "rank_ms": rank_ms, "K": K,
+    return {"workload": workload, "names": names, "sizes": sizes, "elapsed": elapsed, "kern_ms": kern_ms,
+            "rank_ms": rank_ms, "K": K,
             "kernel": kernel,
             "launch_bytes": launch_bytes, "per_class": per_class, "done_frac": done_frac, "resets": resets}
+
+
+def env_side_legs(args, rank, world, dist) -> list:
+    """BASELINE configs 3 and 5 beside the headline env leg (``--env-legs``, 'workload:envs_per_gpu,...'):
+    the same timed loop, compact records (whole-job env-steps/s, mean launch ms, HBM fraction)."""
+    out = []
+    for spec in filter(None, args.env_legs.split(",")):
+        wl, envs = spec.split(":")
+        r = env_leg(args, rank, world, dist, wl, int(envs))
+        B = sum(r["sizes"])
+        gbs = r["launch_bytes"] / (r["kern_ms"] * 1e-3) / 1e9
+        out.append({"workload": wl, "envs_per_gpu": B, "value": _sig(B * r["K"] * world / r["elapsed"]),
+                    "kernel_ms": _sig(r["kern_ms"]), "frac": _sig(gbs / HBM_PEAK_GBS, 3)})
+    return out
 
 
 def run_cpu_baselines(args) -> dict:
@@ -636,10 +670,21 @@ def launch_ranks(args) -> int:
             os.unlink(env["MARLSAT_BENCH_CPU_JSON"])
 
 
+def resolve_world(gpus: Optional[int], environ) -> "int | str | None":
+    """The run's world size: torchrun's WORLD_SIZE when set (``--gpus`` may be omitted; an explicit one that
+    disagrees -> None, an error), else ``--gpus`` (default 1); "launch" when N > 1 ranks must be started."""
+    if "WORLD_SIZE" in environ:
+        world = int(environ["WORLD_SIZE"])
+        return world if gpus is None or gpus == world else None
+    n = gpus or 1
+    return "launch" if n > 1 else n
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1,
-                    help="ranks, one per GPU; N > 1 without torchrun's env starts an N-rank torchrun child")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: torchrun's WORLD_SIZE, else 1); N > 1 without torchrun's env "
+                         "starts an N-rank torchrun child")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="uf200-860", choices=sorted(WORKLOADS) + ["mixed"],
@@ -653,16 +698,23 @@ def main():
                          "'mappo' (BASELINE config 3, the metric's 4096 envs), the others are 'mappo_other_legs' "
                          "(config 4: uf200-860, 25 agents, 4096 envs per GPU)")
     ap.add_argument("--mappo-micro-gb", type=float, default=240.0, help="activation budget per PPO micro-batch")
+    ap.add_argument("--mappo-cycles", type=int, default=2,
+                    help="timed train cycles per MAPPO leg (after one warm-up cycle); value = 1 / their median")
+    ap.add_argument("--env-legs", default="uf100-430:4096,mixed:1024,mixed:8192",
+                    help="env side legs 'workload:envs_per_gpu,...' ('' skips): BASELINE config 3 and config 5 "
+                         "(1024 envs per GPU = its 8-GPU share of 8192, and all 8192 on one GPU)")
     args = ap.parse_args()
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    world = resolve_world(args.gpus, os.environ)
+    if world == "launch":
         sys.exit(launch_ranks(args))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world is None:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks",
+              file=sys.stderr)
+        sys.exit(2)
+    args.gpus = world
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
-        sys.exit(2)
 
     base = None
     if rank == 0 and args.cpu_budget > 0:
@@ -682,6 +734,7 @@ def main():
     torch.cuda.set_device(dev_idx)
     dist = None
     backend = None
+    collectives = os.environ.get("MARLSAT_COLLECTIVES", "torch")
     if world > 1:
         import torch.distributed as dist
 
@@ -693,8 +746,9 @@ def main():
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {dist.get_world_size()} ranks")
 
-    progress(rank, f"env leg: {args.workload}, {world} rank(s)")
+    progress(rank, f"env legs, {world} rank(s)")
     r = env_leg(args, rank, world, dist)
+    side_env = env_side_legs(args, rank, world, dist)
     legs = []
     for spec in filter(None, args.mappo.split(",")):
         wl, envs, T = spec.split(":")
@@ -725,7 +779,9 @@ def main():
             "value": B * K * world / elapsed,
             "unit": "env-steps/s",
             "n_gpus": world,
-            "rccl_ranks": dist.get_world_size() if dist is not None else 1,
+            # ranks whose gradient all-reduce ran over RCCL (torch "nccl" or the C-ABI communicator); 0 for a
+            # single rank or a gloo rehearsal
+            "rccl_ranks": world if world > 1 and (backend == "nccl" or collectives == "capi") else 0,
             "dist_backend": backend,
             "steps": K,
             "warmup": args.warmup,
@@ -735,7 +791,8 @@ def main():
             "vs_baseline": None,
             "dtype": args.obs_dtype,
             "data": "synthetic (planted-solution random 3-SAT from the reference generator algorithm, "
-                    f"seed=1000*size_id+i (size_id {sids}), pool {args.pool}; random valid mode-0 actions)",
+                    f"seed=1000*size_id+i (size_id {sids}), pool {args.pool}; random valid mode-0 actions; the "
+                    "MAPPO pools pass over seeds leaving a variable in no clause, e.g. uf200 3090)",
             "config": cfg,
             "cpu_baseline": base["env"] if base else None,
             "mappo_cpu_baseline": base["mappo"] if base else None,
@@ -756,7 +813,8 @@ def main():
                 "algorithmic_bytes_per_launch": r["launch_bytes"],
                 "traffic_source": traffic_src,
             },
-            # the MAPPO legs close the line, so the driver's tail of stdout holds them
+            # the side legs close the line, so the driver's tail of stdout holds them
+            "env_other_legs": side_env,
             "mappo_other_legs": legs[1:],
             "mappo": mappo,
         }

@@ -81,6 +81,16 @@ int msat_gemm_wgrad_h2_dual(const float *A0, int32_t lda0, const float *G0, int3
 int msat_gemm_wgrad_rot(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
                         int32_t M, int32_t K, int32_t N, int32_t rot, int32_t accumulate, void *workspace,
                         void *stream);
+/* Arithmetic path of msat_gemm_wgrad / msat_gemm_wgrad_rot: MSAT_PRECISION_FP16X2 (default) and
+ * MSAT_PRECISION_BF16X3 run the fp32-accurate split kernels, MSAT_PRECISION_FP32 the fp32 MFMA tiles.
+ * Set once per process (the Python host calls it at import with its validated MARLSAT_PRECISION);
+ * until then the library reads MARLSAT_PRECISION once, and an unknown value there makes every weight
+ * gradient fail with MSAT_EBADARG instead of picking a path.  Unknown `mode`: MSAT_EBADARG. */
+#define MSAT_PRECISION_FP16X2 0
+#define MSAT_PRECISION_BF16X3 1
+#define MSAT_PRECISION_FP32 2
+int msat_set_precision(int32_t mode);
+int msat_get_precision(void); /* the mode in force, or MSAT_EBADARG if MARLSAT_PRECISION is unknown */
 
 /* ---- graph batch assembly (learner:148-195 features + the agents' local graphs) ----
  * Block per sample: instantiate the per-instance templates (marlsat/learners/graphs.py) at the
@@ -236,6 +246,13 @@ int msat_ppo_loss(const float *logits, int32_t S, int32_t A, int32_t M, int32_t 
                   float *dlogits, float *dvalue, float *row_terms, double *loss_sums, void *stream);
 int msat_adam(float *params, const float *grads, float *m, float *v, size_t n, float lr, float b1, float b2,
               float eps, int32_t count, float grad_scale, void *stream);
+/* msat_adam + a fail-loud guard: if an updated parameter is not finite, *first_bad = min(*first_bad,
+ * count) (device int32, the caller initialises it to INT32_MAX).  No host sync: the runner reads the
+ * flag once per train cycle (mappo_runner.py:313-317's loop) and raises, instead of carrying NaN
+ * parameters forward -- the hazard of an instance with a variable in no clause at zero-initialised
+ * biases (tests/test_isolated_variable.py). */
+int msat_adam_checked(float *params, const float *grads, float *m, float *v, size_t n, float lr, float b1, float b2,
+                      float eps, int32_t count, float grad_scale, int32_t *first_bad, void *stream);
 /* ---- collectives (RCCL over xGMI, one communicator per process) ----
  * The gradient is ONE flat fp32 buffer (the grads of every parameter, 16-B aligned tensors): before
  * msat_adam(..., grad_scale = 1 / world) every rank SUM-all-reduces it in place (learner:647-650 is the

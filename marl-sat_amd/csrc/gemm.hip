@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <stdlib.h>
 
+#include <atomic>
 #include <cstring>
 
 #include "common.h"
@@ -389,12 +390,34 @@ int msat_wgrad_h2w_launch(const float *A, int lda, const float *G, int ldg, cons
 int msat_wgrad_x3_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
                          int rows_per_split, hipStream_t s);
 
-// MARLSAT_PRECISION=fp32 (the accuracy reference path, README) keeps the weight gradients on fp32
-// MFMA; otherwise they run on the fp32-accurate bf16x3 split.  Read per call.
-static bool wgrad_x3() {
+// The arithmetic path (msat_set_precision): MSAT_PRECISION_FP32 (the accuracy reference path, README)
+// keeps the weight gradients on fp32 MFMA; the other two run the fp32-accurate split kernels.  Until a
+// host sets it, MARLSAT_PRECISION is read ONCE; an unknown value there is kept as an error state
+// (kPrecisionBad), so every weight gradient fails loudly instead of silently picking a path.
+constexpr int kPrecisionUnset = -100, kPrecisionBad = -101;
+static std::atomic<int> g_precision{kPrecisionUnset};
+
+static int precision_from_env() {
     const char *e = getenv("MARLSAT_PRECISION");
-    return !(e && std::strcmp(e, "fp32") == 0);
+    if (!e || !*e || std::strcmp(e, "fp16x2") == 0) return MSAT_PRECISION_FP16X2;
+    if (std::strcmp(e, "bf16x3") == 0) return MSAT_PRECISION_BF16X3;
+    if (std::strcmp(e, "fp32") == 0) return MSAT_PRECISION_FP32;
+    return kPrecisionBad;
 }
+
+static int precision_mode() {
+    int p = g_precision.load(std::memory_order_relaxed);
+    if (p == kPrecisionUnset) {
+        int expect = kPrecisionUnset;
+        g_precision.compare_exchange_strong(expect, precision_from_env());
+        p = g_precision.load(std::memory_order_relaxed);
+    }
+    return p;
+}
+
+#define MSAT_REQUIRE_PRECISION(pm)                                                                             \
+    MSAT_REQUIRE((pm) >= 0, "MARLSAT_PRECISION=%s: expected fp16x2, bf16x3 or fp32 (or msat_set_precision)", \
+                 getenv("MARLSAT_PRECISION") ? getenv("MARLSAT_PRECISION") : "")
 int msat_wgrad2_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
                        int rows_per_split, hipStream_t s);
 
@@ -474,8 +497,11 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
                                int32_t M, int32_t K, int32_t N, int32_t accumulate, void *workspace, void *stream) {
     MSAT_REQUIRE(A && G && W && workspace, "NULL operand");
     MSAT_REQUIRE(M >= 0 && K >= 1 && N >= 1 && lda >= K && ldg >= N && ldw >= N, "bad dims");
+    const int pm = precision_mode();
+    MSAT_REQUIRE_PRECISION(pm);
+    const bool x3 = pm != MSAT_PRECISION_FP32;
     hipStream_t s = (hipStream_t)stream;
-    if (wgrad_x3() && K > kSkinnyK && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
+    if (x3 && K > kSkinnyK && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
         const int splits = msat_wgrad_x3w_splits(M, K);
         const int rc = msat_wgrad_x3w_launch(A, lda, G, ldg, (float *)workspace, M, K, N, 0, splits, s);
         if (rc) return rc;
@@ -500,7 +526,7 @@ extern "C" int msat_gemm_wgrad(const float *A, int32_t lda, const float *G, int3
     const int splits = wgrad_splits(M, K, N);
     const int rows = (M + splits - 1) / splits;
     int rc;
-    if (wgrad_x3() && msat_wgrad_x3_ok(A, lda, G, ldg, K, N)) {
+    if (x3 && msat_wgrad_x3_ok(A, lda, G, ldg, K, N)) {
         const int rows16 = ((rows + 15) / 16) * 16;
         rc = msat_wgrad_x3_launch(A, lda, G, ldg, (float *)workspace, M, K, N, splits, rows16, s);
     } else if (msat_wgrad2_ok(A, lda, G, ldg, K, N)) {
@@ -527,8 +553,10 @@ extern "C" int msat_gemm_wgrad_rot(const float *A, int32_t lda, const float *G, 
     if (rot == 0) return msat_gemm_wgrad(A, lda, G, ldg, W, ldw, M, K, N, accumulate, workspace, stream);
     MSAT_REQUIRE(A && G && W && workspace, "NULL operand");
     MSAT_REQUIRE(M >= 0 && K >= 1 && N >= 1 && lda >= K && ldg >= N && ldw >= N, "bad dims");
+    const int pm = precision_mode();
+    MSAT_REQUIRE_PRECISION(pm);
     hipStream_t s = (hipStream_t)stream;
-    if (wgrad_x3() && K > kSkinnyK && rot % 4 == 0 && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
+    if (pm != MSAT_PRECISION_FP32 && K > kSkinnyK && rot % 4 == 0 && msat_wgrad_x3w_ok(A, lda, G, ldg, K, N)) {
         const int splits = msat_wgrad_x3w_splits(M, K);
         const int rc = msat_wgrad_x3w_launch(A, lda, G, ldg, (float *)workspace, M, K, N, rot, splits, s);
         if (rc) return rc;
@@ -596,4 +624,17 @@ extern "C" int msat_gemm_wgrad_h2_dual(const float *A0, int32_t lda0, const floa
     rc = wgrad_reduce(part0, splits, K0, N0, W0, ldw0, accumulate, s);
     if (rc) return rc;
     return wgrad_reduce(part1, splits, K1, N1, W1, ldw1, accumulate, s);
+}
+
+extern "C" int msat_set_precision(int32_t mode) {
+    MSAT_REQUIRE(mode == MSAT_PRECISION_FP16X2 || mode == MSAT_PRECISION_BF16X3 || mode == MSAT_PRECISION_FP32,
+                 "msat_set_precision: unknown mode %d (0 fp16x2, 1 bf16x3, 2 fp32)", mode);
+    g_precision.store(mode, std::memory_order_relaxed);
+    return MSAT_OK;
+}
+
+extern "C" int msat_get_precision(void) {
+    const int pm = precision_mode();
+    MSAT_REQUIRE_PRECISION(pm);
+    return pm;
 }

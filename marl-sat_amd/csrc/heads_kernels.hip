@@ -461,9 +461,11 @@ loss_sums_kernel(const float *__restrict__ row_terms, int R, int S, double *__re
 
 // ------------------------------------------------------------------- Adam ----
 // optax.adam: m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr * mhat / (sqrt(vhat) + eps)
+// first_bad (nullable): atomicMin(first_bad, count) where an updated parameter is not finite (a
+// vector-memory atomic on the rare failing lanes; the common path adds one compare)
 __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m,
                             float *__restrict__ v, size_t n, float lr, float b1, float b2, float eps, float bc1,
-                            float bc2, float gscale) {
+                            float bc2, float gscale, int *__restrict__ first_bad, int count) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float gi = g[i] * gscale;
@@ -472,7 +474,9 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g, 
     m[i] = mi;
     v[i] = vi;
     const float mh = mi / bc1, vh = vi / bc2;
-    p[i] = p[i] + (-lr) * (mh / (sqrtf(vh) + eps));
+    const float pn = p[i] + (-lr) * (mh / (sqrtf(vh) + eps));
+    p[i] = pn;
+    if (first_bad && !isfinite(pn)) atomicMin(first_bad, count);
 }
 
 }  // namespace msat
@@ -620,13 +624,19 @@ extern "C" int msat_ppo_loss(const float *logits, int32_t S, int32_t A, int32_t 
     return check_launch("loss_sums_kernel");
 }
 
-extern "C" int msat_adam(float *params, const float *grads, float *m, float *v, size_t n, float lr, float b1, float b2,
-                         float eps, int32_t count, float grad_scale, void *stream) {
+extern "C" int msat_adam_checked(float *params, const float *grads, float *m, float *v, size_t n, float lr, float b1,
+                                 float b2, float eps, int32_t count, float grad_scale, int32_t *first_bad,
+                                 void *stream) {
     MSAT_REQUIRE(params && grads && m && v && count >= 1, "bad adam args");
     if (!n) return MSAT_OK;
     const float bc1 = (float)(1.0 - pow((double)b1, (double)count));
     const float bc2 = (float)(1.0 - pow((double)b2, (double)count));
     hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, params, grads, m, v, n, lr,
-                       b1, b2, eps, bc1, bc2, grad_scale);
+                       b1, b2, eps, bc1, bc2, grad_scale, first_bad, count);
     return check_launch("adam_kernel");
+}
+
+extern "C" int msat_adam(float *params, const float *grads, float *m, float *v, size_t n, float lr, float b1, float b2,
+                         float eps, int32_t count, float grad_scale, void *stream) {
+    return msat_adam_checked(params, grads, m, v, n, lr, b1, b2, eps, count, grad_scale, nullptr, stream);
 }

@@ -161,6 +161,9 @@ def _load():
     sig["msat_ppo_loss"] = (I, [P, I, I, I, I, I, I, P, P, P, P, P, P, F, F, F, F, I, P, P, P, P, P])
     sig["msat_gemm_f64acc"] = (I, [P, I, I, P, I, I, P, I, I, I, I, I, P])
     sig["msat_adam"] = (I, [P, P, P, P, Z, F, F, F, F, I, F, P])
+    sig["msat_adam_checked"] = (I, [P, P, P, P, Z, F, F, F, F, I, F, P, P])
+    sig["msat_set_precision"] = (I, [I])
+    sig["msat_get_precision"] = (I, [])
     sig["msat_moments"] = (I, [P, Z, P, P, P])
     sig["msat_standardize"] = (I, [P, Z, F, F, P])
     sig["msat_comm_id_bytes"] = (Z, [])
@@ -249,6 +252,9 @@ EXPORTED = (
     "msat_sample_actions",
     "msat_ppo_loss",
     "msat_adam",
+    "msat_adam_checked",
+    "msat_set_precision",
+    "msat_get_precision",
     "msat_gemm",
     "msat_gemm_f64acc",
     "msat_gemm_wgrad_workspace_bytes",

@@ -31,8 +31,11 @@ L_ = _lib.lib
 # back per tile to "bf16x3" (three-way bf16 split) where fp16's range fails; "bf16x3" runs that
 # fallback throughout; "fp32" keeps every product on fp32 MFMA (the accuracy reference path).
 PRECISION = os.environ.get("MARLSAT_PRECISION", "fp16x2")
-if PRECISION not in ("fp16x2", "bf16x3", "fp32"):
+PRECISION_CODES = {"fp16x2": 0, "bf16x3": 1, "fp32": 2}  # MSAT_PRECISION_* (include/marlsat_net.h)
+if PRECISION not in PRECISION_CODES:
     raise ValueError(f"MARLSAT_PRECISION must be fp16x2, bf16x3 or fp32, got {PRECISION!r}")
+# the library's weight-gradient path follows the same validated value (set once, not re-read per call)
+_lib.check(L_.msat_set_precision(PRECISION_CODES[PRECISION]), "msat_set_precision")
 
 
 def _chk(rc, what):
@@ -932,8 +935,12 @@ class GNNActorCritic:
             self.actor_head_backward(b, ht, dlogits, dHp, dHn, dHc)
         self.encode_backward(b, tape, Hc, dHp, dHn, dHc)
 
-    def adam_step(self, lr: float, grad_scale: float = 1.0, b1=0.9, b2=0.999, eps=1e-8):
+    def adam_step(self, lr: float, grad_scale: float = 1.0, b1=0.9, b2=0.999, eps=1e-8,
+                  first_bad: Optional[torch.Tensor] = None):
+        """One optax.adam step.  first_bad (device int32 scalar, INT32_MAX when clean): set to the smallest
+        Adam count whose update left a parameter non-finite (msat_adam_checked; no host sync)."""
         self.adam_count += 1
-        _chk(L_.msat_adam(self.params.data_ptr(), self.grads.data_ptr(), self.adam_m.data_ptr(),
-                          self.adam_v.data_ptr(), self.size, float(lr), b1, b2, eps, self.adam_count,
-                          float(grad_scale), self.stream), "adam")
+        _chk(L_.msat_adam_checked(self.params.data_ptr(), self.grads.data_ptr(), self.adam_m.data_ptr(),
+                                  self.adam_v.data_ptr(), self.size, float(lr), b1, b2, eps, self.adam_count,
+                                  float(grad_scale), first_bad.data_ptr() if first_bad is not None else None,
+                                  self.stream), "adam")

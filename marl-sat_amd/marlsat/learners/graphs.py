@@ -21,6 +21,7 @@ nothing), not the env's literal-0 quirk.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -28,6 +29,9 @@ import numpy as np
 import torch
 
 from .. import _lib
+
+# MARLSAT_DEBUG=1: host-side consistency checks that cost a device -> host read (planned vs actual totals)
+DEBUG_CHECKS = os.environ.get("MARLSAT_DEBUG") == "1"
 
 
 def _agent_of(v, base, rem):
@@ -179,6 +183,8 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
     the batch's (var rows, clause rows, incidences) when the caller already knows them (the learner
     plans a minibatch's micro-batches at once, batch_totals): no device -> host read here, so the host
     keeps queueing work instead of waiting for the GPU to drain."""
+    if totals is not None and critic_only:  # batch_totals plans the full (actor + critic) graphs only
+        raise ValueError("assemble: planned totals are for the full graphs; critic_only batches size themselves")
     S = int(inst.shape[0])
     G = 1 if critic_only else tpl.G
     dev = inst.device
@@ -190,6 +196,8 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
     _lib.check(_lib.lib.msat_graph_bases(S, inst.data_ptr(), tv.data_ptr(), tc.data_ptr(), te.data_ptr(), sb.data_ptr(),
                                          tot.data_ptr(), _lib.stream_ptr(dev)), "msat_graph_bases")
     Nv, Nc, nnz = tot.tolist() if totals is None else totals  # sizes the outputs
+    if totals is not None and DEBUG_CHECKS and tuple(tot.tolist()) != tuple(totals):
+        raise AssertionError(f"assemble: planned totals {tuple(totals)} != msat_graph_bases {tuple(tot.tolist())}")
     if min(Nv, Nc, nnz) < 0 or max(Nv, Nc, nnz) > 2 ** 31 - 1:  # msat_graph_bases flags an overflow with -1
         raise ValueError(f"graph batch of {S} samples exceeds int32 row indices (var rows, clause rows, incidences "
                          f"= {Nv}, {Nc}, {nnz}; -1 = overflow): use smaller micro-batches")

@@ -37,6 +37,7 @@ from .graphs import DeviceTemplates, GraphBatch, assemble, batch_totals, build_t
 from .ops import gae as device_gae
 
 L_ = _lib.lib
+NO_BAD_STEP = 2 ** 31 - 1  # msat_adam_checked's "no non-finite update" value
 
 
 # ------------------------------------------------------------ schedules ----
@@ -184,6 +185,8 @@ class MAPPOLearner:
         self.last_val = z((B,), torch.float32)
         self.mom_ws = z((2 * 1024 + 2,), torch.float64)
         self.moments = z((2,), torch.float64)
+        # fail-loud guard: the smallest Adam count whose update left a parameter non-finite (INT32_MAX: none)
+        self.first_bad = torch.full((1,), NO_BAD_STEP, dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ helpers ----
     def init_runner_state(self, key) -> RunnerState:
@@ -328,7 +331,8 @@ class MAPPOLearner:
                 if self.trace is not None:
                     self.trace.append({"idx": idx.cpu(), "params": net.params.clone(),
                                        "grads": net.grads.clone() * scale, "lr": lr})
-                net.adam_step(lr, grad_scale=scale)
+                net.adam_step(lr, grad_scale=scale, first_bad=self.first_bad)
+        self.check_finite()
         # per-minibatch means over the UNION minibatch (learner:708-719 reports each minibatch's loss
         # triple over the whole minibatch): the row sums of every rank are added once per cycle, then
         # divided by the union's row counts (every rank's slice has MB rows)
@@ -338,6 +342,20 @@ class MAPPOLearner:
         losses[..., 1] /= MB * A * w
         losses[..., 2] /= n_ent * w
         return losses, ent
+
+    def check_finite(self) -> None:
+        """One read per cycle of the Adam guard (msat_adam_checked): raise instead of carrying non-finite
+        parameters into the next cycle (the loop of mappo_runner.py:313-317 would train on NaN silently, as
+        the reference does)."""
+        bad = int(self.first_bad.item())
+        if bad != NO_BAD_STEP:
+            self.first_bad.fill_(NO_BAD_STEP)
+            raise FloatingPointError(
+                f"MAPPO: Adam step {bad} left non-finite parameters.  A known cause: a pool instance with a variable "
+                f"in no clause -- assigned 0, that variable is a constant LayerNorm row at zero-initialised biases and "
+                f"its gradient grows ~1000x per message-passing layer past fp32 range, in the reference as here "
+                f"(tests/test_isolated_variable.py; filter the pool with generate_problem_pool(skip_isolated=True) or "
+                f"utils.generate_cnf_dataset.has_isolated_variable)")
 
     # ------------------------------------------------------------ metrics ----
     def metrics(self, losses, ent):

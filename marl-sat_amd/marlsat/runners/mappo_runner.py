@@ -40,6 +40,7 @@ from ..learners.mappo_gnn_sat_learner import MAPPOLearner
 from ..random import Key, PRNGKey, split
 from ..utils import checkpoints as ck
 from ..utils.data_parser import clauses_array, load_cnf_problems, split_train_eval
+from ..utils.generate_cnf_dataset import has_isolated_variable
 
 METRICS_HEADER = ("update,mean_return,solve_rate,avg_unsat_clauses,avg_solve_steps,explained_variance,"
                   "value_loss,actor_loss,policy_entropy\n")
@@ -168,6 +169,12 @@ def run(config: Dict, log=print) -> Dict:
         if (p["num_vars"], p["num_clauses"]) != (env.num_vars, env.num_clauses):
             raise ValueError(f"{p['name']} is V={p['num_vars']}, C={p['num_clauses']}; the config is "
                              f"V={env.num_vars}, C={env.num_clauses} (one size per run, as the reference)")
+    iso = [p["name"] for p in train_raw if has_isolated_variable(clauses_array(p), env.num_vars)]
+    if iso:  # the reference trains on them; its first Adam step on one is non-finite (learner check_finite)
+        log(f"warning: {len(iso)} training problem(s) leave a variable in no clause ({', '.join(iso[:5])}"
+            f"{', ...' if len(iso) > 5 else ''}): at zero-initialised biases such a variable is a constant LayerNorm "
+            f"row whose gradient overflows fp32 at depth (tests/test_isolated_variable.py); the learner stops with "
+            f"FloatingPointError if an update turns non-finite")
     train_pool = env.make_pool(np.stack([clauses_array(p) for p in train_raw]))
     eval_pool = env.make_pool(np.stack([clauses_array(p) for p in eval_raw])) if eval_raw else None
     net = GNNActorCritic(fc["GNN_HIDDEN_DIM"], fc["GNN_NUM_MESSAGE_PASSING_STEPS"], env.num_agents,

@@ -31,3 +31,17 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture
+def c_precision():
+    """Setter for the library's weight-gradient path (msat_set_precision: 'fp16x2' | 'bf16x3' | 'fp32');
+    restores the process's validated MARLSAT_PRECISION after the test."""
+    from marlsat import _lib
+    from marlsat.learners import gnn
+
+    def set_(name):
+        _lib.check(_lib.lib.msat_set_precision(gnn.PRECISION_CODES[name]), "msat_set_precision")
+
+    yield set_
+    set_(gnn.PRECISION)

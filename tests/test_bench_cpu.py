@@ -62,14 +62,29 @@ def test_host_cpu_record(monkeypatch):
     assert h["cores"] == min(2, h["affinity_cores"]) and h["cap_source"] == "OMP_NUM_THREADS"
 
 
-def test_mappo_legs_fit_the_driver_tail():
-    """Two compact MAPPO legs at 8 ranks close the line within the driver's 2,000-character tail."""
+def test_world_from_torchrun_without_gpus_flag():
+    """torchrun --nproc-per-node N bench.py (no --gpus) takes N from WORLD_SIZE; only an explicit --gpus that
+    disagrees is an error; without torchrun's env, --gpus N > 1 launches the ranks."""
+    import bench
+
+    assert bench.resolve_world(None, {"WORLD_SIZE": "8"}) == 8
+    assert bench.resolve_world(8, {"WORLD_SIZE": "8"}) == 8
+    assert bench.resolve_world(2, {"WORLD_SIZE": "8"}) is None
+    assert bench.resolve_world(None, {}) == 1
+    assert bench.resolve_world(1, {}) == 1
+    assert bench.resolve_world(4, {}) == "launch"
+
+
+def test_side_legs_fit_the_driver_tail():
+    """The env side legs and two compact MAPPO legs at 8 ranks close the line within the driver's
+    2,000-character tail, which also carries the run's stderr (progress lines, ~350 characters)."""
     import json
 
     import bench
 
     kern = "gru_ln_fused_fwd_h2s_kernel (fp16x2, + x3r fixup launch)"
     full = {"metric": "MAPPO updates/sec", "value": 1 / 27.6123456, "unit": "updates/s", "s_per_update": 27.6123456,
+            "s_per_update_cycles": [27.6123456, 27.7123456],
             "samples_per_s": 296.712345, "adam_steps_per_s": 0.579123,
             "phase_ms": {"rollout": 1618.1123, "gae": 122.7123, "ppo_update": 25631.7123, "metrics": 244.5123},
             "config": {"workload": "uf200-860", "num_agents": 25, "max_vars_per_agent": 8, "envs_per_gpu": 4096,
@@ -78,8 +93,12 @@ def test_mappo_legs_fit_the_driver_tail():
                        "parallelism": "dp8 (env shards; RCCL gradient all-reduce per minibatch)"},
             "roofline": {"bound": "hbm", "achieved": 3107.123456, "peak": 8000.0, "unit": "GB/s", "frac": 0.3884123,
                          "traffic": 3.6e9 * 1.17123, "kernel": kern, "kernel_ms": 1.3168123,
-                         "mfma": {"frac": 0.27123}, "per_rank_kernel_ms": [1.3168123 + i * 1e-3 for i in range(8)]}}
+                         "mfma": {"frac": 0.27123}, "per_rank_kernel_ms": [1.3168123 + i * 1e-3 for i in range(8)]},
+            "params_check": {"finite": True, "identical": True, "checksum": [123.4567890123, 1234567890123456789]}}
     leg = bench.compact_leg(full, "gpurun_out/bench_mappo_uf200-860_n8_rank0.json")
-    tail = json.dumps({"mappo_other_legs": [leg], "mappo": leg})
-    assert len(tail) < 1900, len(tail)
-    assert leg["roofline"]["kernel"] == "gru_ln_fused_fwd_h2s_kernel" and leg["config"]["parallelism"] == "dp8"
+    env = [{"workload": w, "envs_per_gpu": b, "value": bench._sig(1.234567e8), "kernel_ms": bench._sig(0.0267123),
+            "frac": bench._sig(0.612345, 3)} for w, b in (("uf100-430", 4096), ("mixed", 1024), ("mixed", 8192))]
+    tail = json.dumps({"env_other_legs": env, "mappo_other_legs": [leg], "mappo": leg})
+    assert len(tail) < 1600, len(tail)
+    assert leg["roofline"]["kernel"] == "gru_ln_fused_fwd_h2s_kernel" and leg["config"].endswith(" dp8")
+    assert leg["s_per_update"] == [27.61, 27.71] and leg["s_median"] == 27.61

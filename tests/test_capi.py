@@ -146,3 +146,43 @@ def test_library_does_not_link_rccl():
     out = subprocess.run(["readelf", "-d", lib], capture_output=True, text=True, check=True).stdout
     needed = [l for l in out.splitlines() if "(NEEDED)" in l]
     assert needed and not any("rccl" in l for l in needed), needed
+
+
+def test_precision_entry_points_validate():
+    """msat_set_precision / msat_get_precision (include/marlsat_net.h): the weight gradients' path is set
+    once and validated; an unknown mode is MSAT_EBADARG with a message, not a silent fallback."""
+    from marlsat import _lib
+    from marlsat.learners import gnn
+
+    L = _lib.lib
+    assert L.msat_get_precision() == gnn.PRECISION_CODES[gnn.PRECISION]
+    assert L.msat_set_precision(7) == -1
+    assert b"unknown mode" in L.msat_last_error()
+    assert L.msat_get_precision() == gnn.PRECISION_CODES[gnn.PRECISION]  # unchanged by the bad call
+    try:
+        for code in (2, 1, 0):
+            assert L.msat_set_precision(code) == 0
+            assert L.msat_get_precision() == code
+    finally:
+        L.msat_set_precision(gnn.PRECISION_CODES[gnn.PRECISION])
+
+
+def test_unknown_precision_env_fails_loudly_in_a_c_host():
+    """A C-ABI host that never calls msat_set_precision gets MARLSAT_PRECISION read once; a mistyped value
+    makes msat_get_precision (and every weight gradient) return MSAT_EBADARG naming the value."""
+    import subprocess
+    import sys
+
+    from marlsat import _lib
+
+    code = ("import ctypes; L = ctypes.CDLL(%r); L.msat_last_error.restype = ctypes.c_char_p; "
+            "rc = L.msat_get_precision(); print(rc, L.msat_last_error().decode())") % _lib.LIB_PATH
+    for val, want in (("fp16X2", None), ("fp32", "2"), ("bf16x3", "1"), ("", "0")):
+        env = dict(os.environ, MARLSAT_PRECISION=val)
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        rc, _, msg = out.stdout.strip().partition(" ")
+        if want is None:
+            assert rc == "-1" and "fp16X2" in msg, out.stdout
+        else:
+            assert rc == want, out.stdout

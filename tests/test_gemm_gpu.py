@@ -99,12 +99,12 @@ def test_gemm_fast_path_shapes(M, N, K, transB):
 @pytest.mark.parametrize("M,K,N", [(1, 4, 4), (33, 128, 384), (5000, 132, 384), (70001, 128, 128), (100, 256, 8),
                                    (407001, 128, 384), (9999, 256, 260), (17, 16, 4), (1000, 12, 36), (3000, 300, 384),
                                    (2049, 256, 512)])
-def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
+def test_wgrad_fast_path_shapes(M, K, N, path, c_precision):
     """Row tails (M % 32 != 0, splits of uneven length) go through zero-filled slabs; the bf16x3
     kernels (transposed LDS reads) are held to the same fp32 bound as the fp32 MFMA kernels."""
     from marlsat import _lib
 
-    monkeypatch.setenv("MARLSAT_PRECISION", "fp32" if path == "fp32" else "fp16x2")
+    c_precision("fp32" if path == "fp32" else "fp16x2")
     g = torch.Generator(device="cuda").manual_seed(M + K + N)
     A = torch.randn(M, K, device="cuda", generator=g)
     G = torch.randn(M, N, device="cuda", generator=g)
@@ -123,7 +123,7 @@ def test_wgrad_fast_path_shapes(M, K, N, path, monkeypatch):
 @pytest.mark.parametrize("M,K,N,rot,ldg", [(5000, 128, 384, 256, 512), (70001, 256, 384, 256, 512), (999, 128, 128, 32, 128),
                                            (300, 256, 384, 128, 384), (5000, 128, 512, 256, 512),
                                            (700001, 64, 192, 128, 192)])
-def test_wgrad_rot(M, K, N, rot, ldg, path, monkeypatch):
+def test_wgrad_rot(M, K, N, rot, ldg, path, c_precision):
     """msat_gemm_wgrad_rot: W[:, (n + rot) % N] (+)= (A^T G)[:, n] (the packed GRU backward rows), on the
     whole-row kernel's rotated store (N <= 384) and on the two-range fallback (bf16x3 tiles for N = 512, or
     fp32 MFMA tiles with MARLSAT_PRECISION=fp32); G read from a wider row (ld > N).  The H = 64, 700 K-row case: the fallback's
@@ -133,7 +133,7 @@ def test_wgrad_rot(M, K, N, rot, ldg, path, monkeypatch):
 
     if path == "fp32" and M < 700001:
         pytest.skip("the fp32 fallback is covered by the large-M case")
-    monkeypatch.setenv("MARLSAT_PRECISION", "fp32" if path == "fp32" else "fp16x2")
+    c_precision("fp32" if path == "fp32" else "fp16x2")
     g = torch.Generator(device="cuda").manual_seed(M + K + N + rot)
     A = torch.randn(M, K, device="cuda", generator=g)
     Gw = torch.randn(M, ldg, device="cuda", generator=g)

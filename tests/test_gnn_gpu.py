@@ -75,12 +75,12 @@ def _close_norm(dev, ref, rtol, what):
 @pytest.mark.parametrize("fuse,path", [(True, "default"), (True, "bf16x3"), (True, "fp32"), (False, "bf16x3"),
                                        (False, "fp32")])
 @pytest.mark.parametrize("V,C,vpa,H,L,S,mode", CASES)
-def test_forward_backward_match_oracle(V, C, vpa, H, L, S, mode, fuse, path, monkeypatch):
+def test_forward_backward_match_oracle(V, C, vpa, H, L, S, mode, fuse, path, monkeypatch, c_precision):
     """fuse: phi folded into the GRU input matrices (else the reference order); path: the arithmetic
     (_set_path: fp16x2 / bf16x3 split kernels at H = 128, packed backward rows; fp32 MFMA)."""
     from marlsat.learners.gnn import GNNActorCritic
 
-    _set_path(monkeypatch, path)
+    _set_path(monkeypatch, path, c_precision)
     monkeypatch.setattr(GNNActorCritic, "fuse_phi", fuse)
     net, b, P, batch, av, am, A, M = _setup(V, C, vpa, H, L, S, mode)
     logits, value, state = net.forward(b, save=True)
@@ -149,7 +149,7 @@ def _close_yard(dev, ref, yard, factor, what, report, kink=None):
     assert (err <= bound).all(), f"{what}: max err {err.max():.3g}, worst ratio {(err / bound).max():.3g}"
 
 
-def _set_path(monkeypatch, path):
+def _set_path(monkeypatch, path, c_precision):
     """'default': the bench's kernels (phi folded, fp16x2 GRU forward / data / weight gradients with
     dual launches); 'bf16x3': phi folded, the fp16x2 kernels off (the bf16x3 register-A GRU forward,
     bf16x3 data and weight gradients: the fallback wherever fp16's range fails; MARLSAT_PRECISION=bf16x3);
@@ -163,13 +163,13 @@ def _set_path(monkeypatch, path):
     h2 = path == "default"
     for sw in ("use_gru_h2", "use_dgrad_h2", "use_wgrad_h2"):
         monkeypatch.setattr(GNNActorCritic, sw, h2)
-    # the C-side weight-gradient choice (gemm.hip wgrad_x3) follows MARLSAT_PRECISION, read per call
-    monkeypatch.setenv("MARLSAT_PRECISION", {"default": "fp16x2", "bf16x3": "bf16x3", "fp32": "fp32"}[path])
+    # the C-side weight-gradient choice (gemm.hip, msat_set_precision)
+    c_precision({"default": "fp16x2", "bf16x3": "bf16x3", "fp32": "fp32"}[path])
 
 
 @pytest.mark.parametrize("path", ["default", "bf16x3", "fp32"])
 @pytest.mark.parametrize("V,C,vpa,H,L,S,mode", DEPTH_CASES)
-def test_depth16_matches_oracle(V, C, vpa, H, L, S, mode, path, monkeypatch):
+def test_depth16_matches_oracle(V, C, vpa, H, L, S, mode, path, monkeypatch, c_precision):
     """The reference's depth L = 16 at H = 128 on uf50 / uf100 / mode 1, on the kernels the bench
     runs ("default": phi folded, fp16x2 GRU forward and data / weight gradients, dual launches), on
     the bf16x3 path those kernels fall back to, and on the reference-order fp32 path, against the
@@ -184,7 +184,7 @@ def test_depth16_matches_oracle(V, C, vpa, H, L, S, mode, path, monkeypatch):
     within 3e-5 (relative) of 0 may land on either side in fp32, and the two sides' gradients
     differ by a whole term (profiles/archive_r02/probe_head_bisect.py: one flipped flip-head unit moved its bias
     gradient by 5e-3)."""
-    _set_path(monkeypatch, path)
+    _set_path(monkeypatch, path, c_precision)
     _depth_check(V, C, vpa, H, L, S, mode, path)
 
 
@@ -194,10 +194,10 @@ UF200_CASE = (200, 860, 8, 128, 16, 1, 0)
 
 
 @pytest.mark.parametrize("path", ["default", "fp32"])
-def test_uf200_network_matches_oracle(path, monkeypatch):
+def test_uf200_network_matches_oracle(path, monkeypatch, c_precision):
     """Config 4 (uf200, A = 25, m = 8) at H = 128, L = 16 against the float64 oracle, same bar as
     test_depth16_matches_oracle."""
-    _set_path(monkeypatch, path)
+    _set_path(monkeypatch, path, c_precision)
     _depth_check(*UF200_CASE, path)
 
 
