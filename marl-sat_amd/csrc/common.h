@@ -13,7 +13,53 @@ namespace msat {
 
 // ---------------------------------------------------------------- errors ----
 int fail(int code, const char *fmt, ...);  // sets the thread-local message, returns code
-int check_launch(const char *what);        // hipGetLastError -> MSAT_EHIP
+int check_launch_plain(const char *what);  // hipGetLastError -> MSAT_EHIP
+
+// ------------------------------------------------------------- debug build ----
+// libmarlsat_debug.so is every kernel built with -DMSAT_DEBUG: MSAT_DCHECK(idx, bound) records the first
+// index outside [0, bound) (source line, index, bound) in this translation unit's g_msat_dbg, and
+// check_launch() synchronises after every launch and turns a recorded failure into MSAT_EHIP naming the
+// launch and the line.  The kernels carry on after a failed check (no trap: the message is the result).
+// In the product build both compile to nothing.
+#ifdef MSAT_DEBUG
+struct MsatDbg {
+    int failed, line;
+    long long idx, bound;
+};
+static __device__ MsatDbg g_msat_dbg;
+
+#define MSAT_DCHECK(idx_, bound_)                                                                \
+    do {                                                                                         \
+        const long long _i = (long long)(idx_), _b = (long long)(bound_);                        \
+        if (_i < 0 || _i >= _b) {                                                                \
+            if (atomicCAS(&::msat::g_msat_dbg.failed, 0, 1) == 0) {                              \
+                ::msat::g_msat_dbg.line = __LINE__;                                              \
+                ::msat::g_msat_dbg.idx = _i;                                                     \
+                ::msat::g_msat_dbg.bound = _b;                                                   \
+            }                                                                                    \
+        }                                                                                        \
+    } while (0)
+
+static inline int check_launch(const char *what) {
+    int rc = check_launch_plain(what);
+    if (rc) return rc;
+    if (hipDeviceSynchronize() != hipSuccess) return check_launch_plain(what);
+    MsatDbg h{};
+    if (hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_msat_dbg), sizeof(h)) != hipSuccess) return check_launch_plain(what);
+    if (h.failed) {
+        const MsatDbg z{};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_msat_dbg), &z, sizeof(z));
+        return fail(MSAT_EHIP, "MSAT_DEBUG: %s: index %lld outside [0, %lld) at line %d of its source", what, h.idx,
+                    h.bound, h.line);
+    }
+    return MSAT_OK;
+}
+#define MSAT_DEBUG_BUILD 1
+#else
+#define MSAT_DCHECK(idx_, bound_) ((void)0)
+static inline int check_launch(const char *what) { return check_launch_plain(what); }
+#define MSAT_DEBUG_BUILD 0
+#endif
 
 #define MSAT_REQUIRE(cond, ...)                      \
     do {                                             \

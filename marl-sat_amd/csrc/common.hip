@@ -13,7 +13,7 @@ int fail(int code, const char *fmt, ...) {
     return code;
 }
 
-int check_launch(const char *what) {
+int check_launch_plain(const char *what) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MSAT_EHIP, "%s: %s", what, hipGetErrorString(e));
     return MSAT_OK;

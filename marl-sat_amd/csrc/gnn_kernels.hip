@@ -288,7 +288,10 @@ __device__ __forceinline__ void bwd_row_vec(const float *__restrict__ gi, const 
     const int j0 = PER * lane;
     float fw[NF > 0 ? NF : 1];
 #pragma unroll
-    for (int k = 0; k < NF; ++k) fw[k] = feat[k];
+    for (int k = 0; k < NF; ++k) {
+        fw[k] = feat[k];
+        MSAT_DCHECK(isfinite(fw[k]) ? 0 : -1, 1);  // debug: an unwritten (NaN-poisoned) feature row
+    }
     float rp[PER], zp[PER], np_[PER], ghn[PER], hv[PER], dyv[PER], sc[PER];
     ldv<PER>(gi + j0, rp);
     ldv<PER>(gi + H + j0, zp);
@@ -384,7 +387,7 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
                   const float *__restrict__ scale, float *__restrict__ dGi, int lddi, float *__restrict__ dGh, int lddh,
                   float *__restrict__ dh, int lddh_prev, float *__restrict__ part, int R, int H, int dh_assign,
-                  int packed, const float *__restrict__ feat, int ldf, int *__restrict__ rexp) {
+                  int packed, const float *__restrict__ feat, int ldf, int *__restrict__ rexp, long long part_cap) {
     constexpr int NQT = NQ + 3 * NF, QC = NQ;  // partial rows; LDS reduction in chunks of QC rows
     __shared__ float s_part[4][QC * 64 * PER];
     // w through readfirstlane: the row index r is then wave-uniform to the compiler, so every per-row base
@@ -407,7 +410,12 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
         }
         float fw[NF > 0 ? NF : 1];
 #pragma unroll
-        for (int k = 0; k < NF; ++k) fw[k] = feat[(size_t)r * ldf + k];
+        for (int k = 0; k < NF; ++k) {
+            fw[k] = feat[(size_t)r * ldf + k];
+            // debug: an unwritten feature row (the debug path poisons cdeg / vfeat with NaN before assembly)
+            // reports index -1 - r
+            MSAT_DCHECK(isfinite(fw[k]) ? r : -1 - r, R);
+        }
         float rg[PER], zg[PER], ng[PER], hn[PER], hv[PER], ghn[PER], dyv[PER];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -505,7 +513,13 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
         for (int j = threadIdx.x; j < QC * 64 * PER; j += kRowThreads) {
             const float v = (s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]);
             const int q = j / (64 * PER), jj = j - q * 64 * PER;
-            if (jj < H) part[(size_t)blockIdx.x * NQT * H + (q0 + q) * H + jj] = v;
+            if (jj < H) {
+                const size_t o = (size_t)blockIdx.x * NQT * H + (q0 + q) * H + jj;
+                // debug: inside the block partials (below the reduction workspace) and the caller's allocation
+                MSAT_DCHECK(o, (long long)gridDim.x * NQT * H);
+                MSAT_DCHECK(o, part_cap);
+                part[o] = v;
+            }
         }
     }
 }
@@ -829,9 +843,10 @@ extern "C" int msat_gru_ln_bwd(const float *dy, int32_t ldy, const float *Gi, in
     hipStream_t s = (hipStream_t)stream;
     const int nb = bwd_blocks(R);
     const dim3 g(nb), b(kRowThreads);
-    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0, nullptr);
-    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0, nullptr);
-    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0, nullptr);
+    const long long cap = (long long)msat_gru_ln_bwd_partial_floats(R, H);
+    if (H == 64) hipLaunchKernelGGL((gru_ln_bwd_kernel<1, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0, nullptr, cap);
+    else if (H == 128) hipLaunchKernelGGL((gru_ln_bwd_kernel<2, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0, nullptr, cap);
+    else hipLaunchKernelGGL((gru_ln_bwd_kernel<4, false>), g, b, 0, s, dy, ldy, Gi, ldi, Gh, ldh, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, 0, 0, nullptr, 0, nullptr, cap);
     int rc = check_launch("gru_ln_bwd_kernel");
     if (rc) return rc;
     return reduce_partials(partial, nb, 2 * H, dln_scale, accumulate_ln, partial + (size_t)nb * 2 * H, s);
@@ -855,6 +870,15 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
     const int nb = bwd_blocks(R);
     const dim3 g(nb), b(kRowThreads);
     const bool bias = dbi != nullptr;
+    const long long cap = (long long)msat_gru_ln_bwd_partial_floats(R, H);
+    if (MSAT_DEBUG_BUILD) {  // the partial buffer lies inside one device allocation of at least `cap` floats
+        hipDeviceptr_t base = nullptr;
+        size_t bytes = 0;
+        MSAT_REQUIRE(hipMemGetAddressRange(&base, &bytes, (hipDeviceptr_t)partial) == hipSuccess &&
+                         (const char *)partial + cap * sizeof(float) <= (const char *)base + bytes,
+                     "MSAT_DEBUG: gru_ln_bwd partial buffer smaller than msat_gru_ln_bwd_partial_floats(%d, %d)", R,
+                     H);
+    }
     const int dh_assign = (accumulate_ln >> 1) & 1;  // bit 1: dhprev = ..., else dhprev += ...
     const int packed = (accumulate_ln >> 2) & 1;     // bit 2: packed [dan | dar | daz | dan r] rows
     accumulate_ln &= 1;
@@ -874,11 +898,11 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
     if (vec)                                                                                                      \
         hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2 && F == 6>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, \
                            hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign,    \
-                           packed, feat, ldf, rexp);                                                              \
+                           packed, feat, ldf, rexp, cap);                                                              \
     else                                                                                                          \
         hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, hprev,   \
                            ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign, packed,   \
-                           feat, ldf, rexp)
+                           feat, ldf, rexp, cap)
 #define MSAT_BWD(PER)                                                                                             \
     if (!bias) { MSAT_BWD1(PER, 2, 0); }                                                                           \
     else if (nfeat == 0) { MSAT_BWD1(PER, 6, 0); }                                                                 \
@@ -894,6 +918,8 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
     // stage 1: 16-row float4 sums of the block partials; stage 2: fixed-order reduce of each column segment
     float *ws = partial + (size_t)nb * NQ * H;
     const int sp = (nb + kPartRows - 1) / kPartRows, width = NQ * H, W4 = width / 4;
+    // the reduction workspace follows the block partials without overlap and ends inside the allocation plan
+    MSAT_REQUIRE((long long)nb * NQ * H + (long long)sp * NQ * H <= cap, "gru_ln_bwd: partial plan overflow");
     MSAT_REQUIRE(a16(partial) && a16(dln_scale) && (!bias || (a16(dbi) && a16(dbh_n))) && (!nfeat || a16(dfeat)),
                  "gru_ln_bwd_g4: partial / gradient outputs must be 16-byte aligned");
     hipLaunchKernelGGL(colsum4_kernel, dim3((W4 + 15) / 16, sp), dim3(256), 0, s,

@@ -356,7 +356,16 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 // 64-row "ping-pong" tiles at two workgroups per CU (5-7 % slower), 16-wave tiles (5-9 % slower),
 // deeper fragment lookahead (+-0.5 %), a split stagger of SIMD partners (0..+0.5 %).
 constexpr int kDmaLate = 8;  // waves 4..7 issue the step's DMA before this block (SIMD-partner stagger)
-__device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
+//
+// PERSIST (gru_ln_fused_fwd_h2p_kernel): one workgroup per CU walks tiles; `pre` says the caller's previous
+// tile already issued this tile's first weight step and activation steps 0..2 (from its epilogue), and
+// next >= 0 asks this tile to do the same for tile `next` as soon as its epilogue has read h out of the
+// slots: the prologue's HBM round trip then overlaps this tile's gate / LayerNorm / store work instead of
+// following it (one workgroup fills the CU, so nothing else hides it).  The stage of the output flush
+// moves to weight buffer 1 (half rows, 34 KiB) because buffer 0 receives the next tile's step-0 weights.
+// Returns whether that prefetch was issued.
+template <bool PERSIST>
+__device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int next = -1, bool pre = false) {
     constexpr int NW = 8;                // waves (16 rows each)
     constexpr int H = 128, IMG = H * 4;  // uint4 per (plane, gate) image: 128 units x 4 chunks = 8 KiB
     constexpr int NI = 6;                // (plane, gate) images per step
@@ -365,13 +374,17 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     __shared__ uint4 Bs[2 * NI * IMG];   // 48 KiB per buffer
     constexpr int ASL = TR * 8;          // uint4 per activation slot (128 B per row)
     __shared__ uint4 As[4 * ASL];        // four activation slots: step s in slot s & 3
-    const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
+    int t = threadIdx.x;
+    // persistent: the thread index is laundered per tile, so the per-lane addressing derived from it is
+    // recomputed inside the tile loop instead of being hoisted out of it and held (spilled) across tiles
+    if constexpr (PERSIST) asm volatile("" : "+v"(t));
+    const int lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int row0 = tile * TR, wr = 16 * w;
     int *const flag = a.flags + tile;
     if (a.wbad[0] | a.wbad[1]) {  // weights out of fp16 range: the bf16x3 launch does every tile
         if (t == 0) *flag = 1;
-        return;
+        return false;
     }
     // step order: the input steps 0 .. nin - 1 first, then the hidden steps (h's four 32-column quarters),
     // whose activation slots still hold all of h at the epilogue (no refetch of h)
@@ -434,13 +447,14 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     // full tiles whose step lies inside one segment: a wave-uniform base and per-lane 32-bit offsets
     // (precomputed per source leading dimension); the last tile and a step straddling segments take the
     // per-lane form below
-    const bool full = row0 + TR <= a.R;
-    auto issueA = [&](int st) {
+    // (r0: the tile's first row -- this tile's, or the next tile's for the persistent prefetch)
+    auto issueA = [&](int st, int r0) {
         const int k = st * 32;
+        const bool full = r0 + TR <= a.R;
         if (full && (st >= nin || k + 32 <= w0)) {
             const bool h = st >= nin;
             const int ld = h ? a.ldp : a.seg_ld[0];
-            const float *b = (h ? hp + 32 * (st - nin) : sg0 + k) + (size_t)row0 * ld;
+            const float *b = (h ? hp + 32 * (st - nin) : sg0 + k) + (size_t)r0 * ld;
             uint4 *dst = &As[(st & 3) * ASL + 64 * 2 * w];
 #pragma unroll
             for (int e = 0; e < 2; ++e)
@@ -449,7 +463,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         }
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const int rr = row0 + drow[e], rc = rr < a.R ? rr : a.R - 1;
+            const int rr = r0 + drow[e], rc = rr < a.R ? rr : a.R - 1;
             const float *src;
             if (st >= nin) {
                 src = hp + (size_t)rc * a.ldp + 32 * (st - nin) + 4 * dchunk[e];
@@ -471,11 +485,14 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         v[1] = __builtin_bit_cast(f4v, row[(2 * g + 1) ^ sw]);
         asplit(st, v, f);
     };
-    issueA(0);
-    if (ns > 1) issueA(1);
-    if (ns > 2) issueA(2);
-    issueW(0, 0);
-    wait_vmcnt<0>();
+    auto prologue = [&](int r0) {  // step 0's weights and activation steps 0..2 of the tile at row r0
+        issueA(0, r0);
+        if (ns > 1) issueA(1, r0);
+        if (ns > 2) issueA(2, r0);
+        issueW(0, 0);
+    };
+    if (!PERSIST || !pre) prologue(row0);
+    wait_vmcnt<0>();  // (persistent: also the previous tile's output stores, issued after the prefetch)
     barrier_lds();
     lsplit(0, fas[0]);
     // one 32-k step; two static copies (input, hidden): the weight buffer's parity is a runtime offset and
@@ -490,7 +507,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         const bool late = w >= 4;
         auto dma = [&]() {
             if (st + 1 < ns) issueW(st + 1, buf ^ 1);
-            if (st + 3 < ns) issueA(st + 3);
+            if (st + 3 < ns) issueA(st + 3, row0);
         };
         if (!late) dma();
         // weight fragments carried across the 24 (gate, column tile) blocks: each plane is re-read
@@ -557,12 +574,15 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         if (t == 0) *flag = bad;
         if (bad) {
             wait_vmcnt<0>();  // no LDS-DMA may land after the workgroup's LDS is released
-            return;
+            return false;
         }
     }
 
     // ---- epilogue.  C/D map: unit u = 16 j + l16, row wr + 4 g + reg.
-    float *stage = reinterpret_cast<float *>(Bs) + w * 16 * 132;  // [16 rows][132] per wave
+    // stage: [16 rows][132] per wave in weight buffer 0; persistent: [16 rows][68] (half rows, flushed in two
+    // rounds) in weight buffer 1, below the range-check flags at its tail
+    constexpr int SW = PERSIST ? 68 : 132;
+    float *stage = reinterpret_cast<float *>(Bs) + (PERSIST ? NI * IMG * 4 : 0) + w * 16 * SW;
     const bool tape = a.g4 != nullptr;
     // h of each accumulator's (row, unit) from the hidden steps' slots: quarter q (units 32 q ..) is step
     // nin + q in slot (nin + q) & 3, [row][8 chunks], chunk c of row r at c ^ ((r >> 1) & 5).  All four
@@ -578,6 +598,17 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
                 const int R = wr + 4 * g + r;
                 hv[j][r] = Af[4 * (sb + 8 * R + ((kq >> 2) ^ ((R >> 1) & 5))) + (kq & 3)];
             }
+        }
+    }
+    bool prefetched = false;
+    if constexpr (PERSIST) {
+        if (next >= 0) {
+            // the slots' rows are this wave's own (its activation DMA and its reads cover rows wr .. wr + 15), so
+            // once its h reads have returned it may refill them; weight buffer 0 was last read before the k
+            // loop's final barrier
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            prologue(next * TR);
+            prefetched = true;
         }
     }
     constexpr float sc = 1.0f / (float)(1 << kH2Shift);  // exact power of two
@@ -598,14 +629,25 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     // wave-private and a wave's LDS operations complete in issue order, so waiting for its own stage
     // writes (lgkmcnt) is the only ordering needed: no workgroup barrier, whose release fence would
     // also drain the wave's global stores.
-    auto flush = [&](float *dst, int ld) {
+    // (persistent: the half rows of columns c0 .. c0 + 63: 4 rows of 16 float4 per instruction)
+    auto flush = [&](float *dst, int ld, int c0 = 0) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (PERSIST) {
 #pragma unroll
-        for (int it = 0; it < 8; ++it) {
-            const int rr = 2 * it + (lane >> 5), c4 = lane & 31;
-            const float4 v = *reinterpret_cast<const float4 *>(stage + rr * 132 + 4 * c4);
-            const int row = row0 + wr + rr;
-            if (row < a.R) *reinterpret_cast<float4 *>(dst + (size_t)row * ld + 4 * c4) = v;
+            for (int it = 0; it < 4; ++it) {
+                const int rr = 4 * it + (lane >> 4), c4 = lane & 15;
+                const float4 v = *reinterpret_cast<const float4 *>(stage + rr * SW + 4 * c4);
+                const int row = row0 + wr + rr;
+                if (row < a.R) *reinterpret_cast<float4 *>(dst + (size_t)row * ld + c0 + 4 * c4) = v;
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < 8; ++it) {
+                const int rr = 2 * it + (lane >> 5), c4 = lane & 31;
+                const float4 v = *reinterpret_cast<const float4 *>(stage + rr * SW + 4 * c4);
+                const int row = row0 + wr + rr;
+                if (row < a.R) *reinterpret_cast<float4 *>(dst + (size_t)row * ld + 4 * c4) = v;
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
@@ -678,23 +720,47 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         const float var = fmaxf(t2 / (float)H - mean[r] * mean[r], 0.0f);
         rs[r] = rsqrtf(var + 1e-6f);
     }
+    // the stage holds JH column tiles (64 columns) per flush round persistent, all 8 otherwise
+    constexpr int JH = PERSIST ? 4 : 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int u = 16 * j + l16;
-        const float scl = a.ln_scale[u], lb = a.ln_bias[u];
+    for (int j0 = 0; j0 < 8; j0 += JH) {
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const f2 hn = {acc[0][j][2 * p], acc[0][j][2 * p + 1]};
-            const f2 y = (hn - f2{mean[2 * p], mean[2 * p + 1]}) * (f2{rs[2 * p], rs[2 * p + 1]} * f2{scl, scl}) +
-                         f2{lb, lb};
-            stage[(4 * g + 2 * p) * 132 + u] = y.x;
-            stage[(4 * g + 2 * p + 1) * 132 + u] = y.y;
+        for (int j = j0; j < j0 + JH; ++j) {
+            const int u = 16 * j + l16;
+            const float scl = a.ln_scale[u], lb = a.ln_bias[u];
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const f2 hn = {acc[0][j][2 * p], acc[0][j][2 * p + 1]};
+                const f2 y = (hn - f2{mean[2 * p], mean[2 * p + 1]}) * (f2{rs[2 * p], rs[2 * p + 1]} * f2{scl, scl}) +
+                             f2{lb, lb};
+                stage[(4 * g + 2 * p) * SW + u - 16 * j0] = y.x;
+                stage[(4 * g + 2 * p + 1) * SW + u - 16 * j0] = y.y;
+            }
         }
+        flush(a.out, a.ldo, 16 * j0);
     }
-    flush(a.out, a.ldo);
+    return prefetched;
 }
 
-__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2s_kernel(GruX3rArgs a) { gru_h2s_tile(a, blockIdx.x); }
+__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2s_kernel(GruX3rArgs a) {
+    gru_h2s_tile<false>(a, blockIdx.x);
+}
+
+// Persistent form: one workgroup per CU (gridDim.x <= tiles) walks tiles tile0, tile0 + gridDim.x, ...
+// (the same XCD's tiles: workgroup b sits on XCD b % 8), each prefetching the next one's prologue.
+// The argument block is re-read from the kernarg segment per tile (the segment pointer is laundered), so its
+// ~40 SGPRs of pointers are not held across the tile loop.
+__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2p_kernel(GruX3rArgs a, int ntiles) {
+    bool pre = false;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int next = tile + (int)gridDim.x < ntiles ? tile + (int)gridDim.x : -1;
+        typedef __attribute__((address_space(4))) const GruX3rArgs KArgs;
+        KArgs *ka = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));
+        pre = gru_h2s_tile<true>(*(const GruX3rArgs *)ka, tile, next, pre);
+    }
+    (void)a;
+}
 
 
 // bf16x3 register-A kernel (the fp16x2 kernel above is fp16x2-only: instantiated for bf16x3 it computed
@@ -978,6 +1044,20 @@ __global__ void split_f16x2_t_kernel(const float *__restrict__ W, int K, int N, 
 
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// compute units of the current device (the persistent kernels' grid), read once
+static int device_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            n = v;
+        else
+            n = 256;
+    }
+    return n;
+}
+
 }  // namespace msat
 
 using namespace msat;
@@ -1145,8 +1225,15 @@ extern "C" int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w
     a.flags = tile_flags;
     a.wbad = wbad;
     const int tiles = (R + 127) / 128;
-    hipLaunchKernelGGL(gru_ln_fused_fwd_h2s_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
-    rc = check_launch("gru_ln_fused_fwd_h2s_kernel");
+    const char *pe = getenv("MARLSAT_GRU_PERSIST");  // A/B switch (round 4)
+    if (pe && pe[0] == '1') {
+        hipLaunchKernelGGL(gru_ln_fused_fwd_h2p_kernel, dim3(std::min(tiles, device_cus())), dim3(512), 0,
+                           (hipStream_t)stream, a, tiles);
+        rc = check_launch("gru_ln_fused_fwd_h2p_kernel");
+    } else {
+        hipLaunchKernelGGL(gru_ln_fused_fwd_h2s_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
+        rc = check_launch("gru_ln_fused_fwd_h2s_kernel");
+    }
     if (rc) return rc;
     a.wiT = reinterpret_cast<const uint16_t *>(wiT_x3);
     a.whT = reinterpret_cast<const uint16_t *>(whT_x3);

@@ -1,7 +1,7 @@
 // Diagnostics (not on the product path): a pure 16 B-per-lane streaming-store
 // kernel that prices the HBM write ceiling the obs pass is measured against.
 #include "common.h"
-#include "marlsat_debug.h"
+#include "marlsat_probe.h"
 
 namespace msat {
 template <bool kNt>
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(NT) fill_rows_kernel(int4 *__restrict__ dst, i
 }
 }  // namespace msat
 
-extern "C" int msat_debug_obs_expand(void *dst, int32_t E, int32_t A, int32_t D, const int32_t *inst,
+extern "C" int msat_probe_obs_expand(void *dst, int32_t E, int32_t A, int32_t D, const int32_t *inst,
                                      const uint32_t *vimg, const uint32_t *mimg, int32_t grid, void *stream) {
     MSAT_REQUIRE(dst && inst && vimg && mimg && E > 0 && A > 0 && D > 0 && D % 4 == 0 && grid != 0,
                  "bad expand args");
@@ -113,7 +113,7 @@ extern "C" int msat_debug_obs_expand(void *dst, int32_t E, int32_t A, int32_t D,
     return msat::check_launch("obs_expand_kernel");
 }
 
-extern "C" int msat_debug_fill_chunked(void *dst, size_t bytes, int32_t value, int32_t nontemporal, int32_t grid,
+extern "C" int msat_probe_fill_chunked(void *dst, size_t bytes, int32_t value, int32_t nontemporal, int32_t grid,
                                        void *stream) {
     MSAT_REQUIRE(dst && bytes % 16 == 0 && grid > 0, "bad fill args");
     const size_t n16 = bytes / 16, per = (n16 + grid - 1) / grid;
@@ -126,7 +126,7 @@ extern "C" int msat_debug_fill_chunked(void *dst, size_t bytes, int32_t value, i
     return msat::check_launch("fill_chunk_kernel");
 }
 
-extern "C" int msat_debug_fill(void *dst, size_t bytes, int32_t value, int32_t nontemporal, int32_t grid,
+extern "C" int msat_probe_fill(void *dst, size_t bytes, int32_t value, int32_t nontemporal, int32_t grid,
                                void *stream) {
     MSAT_REQUIRE(dst && bytes % 16 == 0 && grid > 0, "bad fill args");
     const size_t n16 = bytes / 16;
@@ -139,7 +139,7 @@ extern "C" int msat_debug_fill(void *dst, size_t bytes, int32_t value, int32_t n
     return msat::check_launch("fill_kernel");
 }
 
-extern "C" int msat_debug_fill_rows(void *dst, int32_t E, int32_t A, int32_t D16, int32_t amajor, int32_t value,
+extern "C" int msat_probe_fill_rows(void *dst, int32_t E, int32_t A, int32_t D16, int32_t amajor, int32_t value,
                                     int32_t threads, int32_t grid, void *stream) {
     MSAT_REQUIRE(dst && E > 0 && A > 0 && D16 > 0 && grid > 0 && (threads == 256 || threads == 512), "bad fill args");
     if (threads == 512)

@@ -180,24 +180,24 @@ def _load():
 
 lib = _load()
 
-_debug = None
+_probe = None
 
 
-def debug_lib():
-    """libmarlsat_debug.so: diagnostic entry points (csrc/marlsat_debug.h) for profiles/*.py only."""
-    global _debug
-    if _debug is None:
-        d = ctypes.CDLL(os.path.join(os.path.dirname(LIB_PATH), "libmarlsat_debug.so"))
+def probe_lib():
+    """libmarlsat_probe.so: diagnostic store / expansion probes (csrc/marlsat_probe.h) for profiles/*.py only."""
+    global _probe
+    if _probe is None:
+        d = ctypes.CDLL(os.path.join(os.path.dirname(LIB_PATH), "libmarlsat_probe.so"))
         P = c_void_p
-        for name, args in (("msat_debug_fill", [P, c_size_t, c_int32, c_int32, c_int32, P]),
-                           ("msat_debug_fill_chunked", [P, c_size_t, c_int32, c_int32, c_int32, P]),
-                           ("msat_debug_obs_expand", [P, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
-                           ("msat_debug_fill_rows", [P, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+        for name, args in (("msat_probe_fill", [P, c_size_t, c_int32, c_int32, c_int32, P]),
+                           ("msat_probe_fill_chunked", [P, c_size_t, c_int32, c_int32, c_int32, P]),
+                           ("msat_probe_obs_expand", [P, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
+                           ("msat_probe_fill_rows", [P, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                                      P])):
             fn = getattr(d, name)
             fn.restype, fn.argtypes = c_int32, args
-        _debug = d
-    return _debug
+        _probe = d
+    return _probe
 
 # Every symbol include/marlsat*.h declares (checked by tests/test_capi.py).
 EXPORTED = (

@@ -201,10 +201,11 @@ def assemble(tpl: DeviceTemplates, pool_packed: torch.Tensor, svf: torch.Tensor,
     if min(Nv, Nc, nnz) < 0 or max(Nv, Nc, nnz) > 2 ** 31 - 1:  # msat_graph_bases flags an overflow with -1
         raise ValueError(f"graph batch of {S} samples exceeds int32 row indices (var rows, clause rows, incidences "
                          f"= {Nv}, {Nc}, {nnz}; -1 = overflow): use smaller micro-batches")
-    out = GraphBatch(S, G, Nv, Nc, nnz,
-                     torch.empty((Nv, 8), dtype=torch.float32, device=dev),
-                     torch.empty((Nc, 3), dtype=torch.float32, device=dev),
-                     torch.empty((Nc, 4), dtype=torch.float32, device=dev),
+    # MARLSAT_DEBUG=1: the feature rows start as NaN, so a row the assembly kernel leaves unwritten shows up
+    # (libmarlsat_debug.so's GRU backward checks every feature it reads for finiteness)
+    feats = (lambda shape: torch.full(shape, float("nan"), device=dev)) if DEBUG_CHECKS else (
+        lambda shape: torch.empty(shape, dtype=torch.float32, device=dev))
+    out = GraphBatch(S, G, Nv, Nc, nnz, feats((Nv, 8)), feats((Nc, 3)), feats((Nc, 4)),
                      torch.empty((Nc, 3), dtype=torch.int32, device=dev),
                      torch.empty((Nv + 1,), dtype=torch.int32, device=dev),
                      torch.empty((max(nnz, 1),), dtype=torch.int32, device=dev),

@@ -36,7 +36,7 @@ def time_fill(nt, grid, n=40):
     e = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
     s = _lib.stream_ptr()
     for i in range(n):
-        e[i][0].record(); _lib.debug_lib().msat_debug_fill(obs.data_ptr(), nbytes - nbytes % 16, -1, nt, grid, s); e[i][1].record()
+        e[i][0].record(); _lib.probe_lib().msat_probe_fill(obs.data_ptr(), nbytes - nbytes % 16, -1, nt, grid, s); e[i][1].record()
     torch.cuda.synchronize()
     return statistics.median(a.elapsed_time(b) for a, b in e) * 1e3
 

@@ -15,7 +15,7 @@ inst = torch.randint(0, P, (E,), device="cuda", dtype=torch.int32, generator=g)
 vimg, mimg = bits(E * Dw), bits(P * A * Dw)
 out = torch.empty(E * A * D, dtype=torch.int32, device="cuda")
 s = _lib.stream_ptr()
-run = lambda grid: _lib.debug_lib().msat_debug_obs_expand(out.data_ptr(), E, A, D, inst.data_ptr(), vimg.data_ptr(),
+run = lambda grid: _lib.probe_lib().msat_probe_obs_expand(out.data_ptr(), E, A, D, inst.data_ptr(), vimg.data_ptr(),
                                                   mimg.data_ptr(), grid, s)
 d = torch.arange(D, device="cuda")
 for grid0 in (-4096, 4096):  # correctness on a sample of envs, both variants

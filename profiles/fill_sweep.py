@@ -15,7 +15,7 @@ def t(fn, nt, grid, n=30):
     return statistics.median(a.elapsed_time(b) for a, b in e) * 1e3
 res = {}
 for rnd in range(2):
-    for name, fn in (("stride", _lib.debug_lib().msat_debug_fill), ("chunk", _lib.debug_lib().msat_debug_fill_chunked)):
+    for name, fn in (("stride", _lib.probe_lib().msat_probe_fill), ("chunk", _lib.probe_lib().msat_probe_fill_chunked)):
         for nt in (0, 1):
             for grid in (512, 1024, 2048, 4096, 8192, 16384, 32768, 65536):
                 res.setdefault(f"{name}-nt{nt}-g{grid}", []).append(t(fn, nt, grid))

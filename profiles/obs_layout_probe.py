@@ -13,7 +13,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "marl-sat_amd")]
 import torch
 from marlsat import _lib
 
-D = _lib.debug_lib()
+D = _lib.probe_lib()
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 E, A, D16 = 4096, 25, 315
 buf = torch.empty(E * A * D16 * 4, dtype=torch.int32, device="cuda")
@@ -22,7 +22,7 @@ nbytes = buf.numel() * 4
 for amajor in (0, 1, 0, 1):
     for threads in (256, 512):
         for grid in (E, 2048, 1024):
-            f = lambda: D.msat_debug_fill_rows(buf.data_ptr(), E, A, D16, amajor, 7, threads, grid, s)
+            f = lambda: D.msat_probe_fill_rows(buf.data_ptr(), E, A, D16, amajor, 7, threads, grid, s)
             assert f() == 0
             torch.cuda.synchronize()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

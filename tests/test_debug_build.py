@@ -1,0 +1,102 @@
+"""SURVEY.md section 5's debug target (marl-sat_amd/Makefile `debug`).
+
+CPU: the C-ABI host glue built under AddressSanitizer (tests/capi_host_check.cpp linked against the library's
+objects compiled with -Xarch_host -fsanitize=address) rejects bad arguments through the error channel, with no
+ASan report.
+
+GPU: libmarlsat_debug.so (every kernel with -DMSAT_DEBUG device bounds checks; each launch synchronised and
+checked) runs the clause-cell GRU backward bitwise like the product library, and reports an undersized partial
+buffer and an unwritten (NaN-poisoned) feature row as errors naming the check.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+LIBDIR = os.path.join(ROOT, "marl-sat_amd", "marlsat", "lib")
+ASAN_BIN = os.path.join(ROOT, "marl-sat_amd", "build", "asan", "capi_host_check")
+
+
+def test_capi_host_glue_under_asan():
+    if not os.path.exists(ASAN_BIN):
+        pytest.skip("ASan driver not built (make -C marl-sat_amd debug; __graft_entry__.build() does)")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=23")
+    r = subprocess.run([ASAN_BIN], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "capi_host_check: ok" in r.stdout
+    assert "AddressSanitizer" not in r.stderr
+
+
+def _bwd_args(torch, R, H, nfeat, feat, part):
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(5)
+    dy = torch.randn(R, H, device=dev, generator=g)
+    g4 = torch.randn(R, 4 * H, device=dev, generator=g)
+    hp = torch.randn(R, H, device=dev, generator=g)
+    sc = torch.randn(H, device=dev, generator=g)
+    D = torch.empty(R, 4 * H, device=dev)
+    dh = torch.empty(R, H, device=dev)
+    dln = torch.zeros(2 * H, device=dev)
+    dbi = torch.zeros(3 * H, device=dev)
+    dbh = torch.zeros(3 * H, device=dev)
+    dfeat = torch.zeros(nfeat, 3 * H, device=dev)
+    rexp = torch.empty(R, dtype=torch.int32, device=dev)
+    keep = (dy, g4, hp, sc, D, dh, dln, dbi, dbh, dfeat, rexp, feat, part)
+    args = (dy.data_ptr(), H, g4.data_ptr(), 4 * H, hp.data_ptr(), H, sc.data_ptr(), D.data_ptr(), 4 * H,
+            D.data_ptr() + 4 * H, 4 * H, dh.data_ptr(), H, dln.data_ptr(), dln.data_ptr() + 4 * H, dbi.data_ptr(),
+            dbh.data_ptr() + 4 * 2 * H, feat.data_ptr(), feat.shape[1], nfeat, dfeat.data_ptr(), part.data_ptr(), R, H,
+            7, rexp.data_ptr())
+    return args, {"D": D, "dh": dh, "dln": dln, "dbi": dbi, "dbh": dbh, "dfeat": dfeat, "rexp": rexp}, keep
+
+
+@pytest.mark.gpu
+def test_debug_library_checks_the_gru_backward():
+    import torch
+
+    from marlsat import _lib
+
+    path = os.path.join(LIBDIR, "libmarlsat_debug.so")
+    if not os.path.exists(path):
+        pytest.skip("libmarlsat_debug.so not built")
+    dbg = ctypes.CDLL(path)
+    for lib in (dbg,):
+        lib.msat_gru_ln_bwd_g4fe.restype = ctypes.c_int32
+        lib.msat_gru_ln_bwd_g4fe.argtypes = _lib.lib.msat_gru_ln_bwd_g4fe.argtypes
+        lib.msat_gru_ln_bwd_partial_floats.restype = ctypes.c_size_t
+        lib.msat_gru_ln_bwd_partial_floats.argtypes = [ctypes.c_int32, ctypes.c_int32]
+        lib.msat_last_error.restype = ctypes.c_char_p
+    R, H, nfeat = 20000, 128, 2  # the clause cell's form (msat_gru_ln_bwd_g4fe, nfeat 2)
+    s = _lib.stream_ptr()
+    feat = torch.randint(0, 3, (R, 4), device="cuda").float()
+    cap = int(dbg.msat_gru_ln_bwd_partial_floats(R, H))
+    assert cap == int(_lib.lib.msat_gru_ln_bwd_partial_floats(R, H))
+    part = torch.empty(cap, device="cuda")
+    outs = {}
+    for name, lib in (("product", _lib.lib), ("debug", dbg)):
+        args, out, keep = _bwd_args(torch, R, H, nfeat, feat, part)
+        assert lib.msat_gru_ln_bwd_g4fe(*args, s) == 0, lib.msat_last_error()
+        torch.cuda.synchronize()
+        outs[name] = {k: v.clone() for k, v in out.items()}
+    for k in outs["product"]:
+        assert torch.equal(outs["product"][k], outs["debug"][k]), k
+    # an allocation smaller than msat_gru_ln_bwd_partial_floats: refused before the launch
+    small = torch.empty(cap // 2, device="cuda")
+    args, _, keep = _bwd_args(torch, R, H, nfeat, feat, small)
+    assert dbg.msat_gru_ln_bwd_g4fe(*args, s) == -1
+    assert b"partial buffer smaller" in dbg.msat_last_error()
+    # an unwritten feature row (NaN, as MARLSAT_DEBUG=1 assembly poisons them): the device check names its row
+    bad = feat.clone()
+    bad[12345, 1] = float("nan")
+    args, _, keep = _bwd_args(torch, R, H, nfeat, bad, part)
+    assert dbg.msat_gru_ln_bwd_g4fe(*args, s) == -2
+    msg = dbg.msat_last_error().decode()
+    assert "MSAT_DEBUG: gru_ln_bwd_kernel" in msg and "index -12346 outside [0, 20000)" in msg, msg
+    # the next call is clean again (the failure record is reset when reported)
+    args, out, keep = _bwd_args(torch, R, H, nfeat, feat, part)
+    assert dbg.msat_gru_ln_bwd_g4fe(*args, s) == 0, dbg.msat_last_error()
+    torch.cuda.synchronize()
+    assert np.array_equal(out["dfeat"].cpu().numpy(), outs["product"]["dfeat"].cpu().numpy())
