@@ -443,7 +443,7 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
     // waits for A(d) just before its split; its count ignores the asm weight DMAs, which only makes
     // that wait stricter, and W(d) has landed by then anyway)
     // the bf16x3 body keeps one set (its split needs the registers)
-    constexpr int PF = NP == 2 ? 2 : 1;
+    constexpr int PF = (NP == 2 && RT <= 2) ? 2 : 1;  // 256-row tiles: twice the MFMAs per step, one set ahead
     float4 ras[PF][RT][2];
     auto loadA = [&](int d, float4 (&ra)[RT][2]) {
 #pragma unroll
@@ -1252,6 +1252,13 @@ extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h
     {
         const long off = (long)(A0 - A1);
         if (lda0 == lda1 && off > 0 && off % 32 == 0 && off / 32 < K / 32) p[1].kr = (int)(off / 32);
+    }
+    const char *rte = getenv("MARLSAT_DGRAD_RT");  // A/B switch (round 4): 4 = 256-row tiles
+    if (rte && rte[0] == '4') {
+        const int ntm = (M + 255) / 256;
+        hipLaunchKernelGGL((gemm_h2r16_dual_kernel<4>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(kX3T), 0,
+                           (hipStream_t)stream, p[0], p[1], rexp, M, K);
+        return check_launch("gemm_h2r16_dual_kernel<4>");
     }
     const int ntm = (M + 127) / 128;
     hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(kX3T), 0,

@@ -382,7 +382,9 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int row0 = tile * TR, wr = 16 * w;
     int *const flag = a.flags + tile;
-    if (a.wbad[0] | a.wbad[1]) {  // weights out of fp16 range: the bf16x3 launch does every tile
+    // weights out of fp16 range: the bf16x3 launch does every tile (the persistent kernel checks this once,
+    // before its tile loop: a load here would make the compiler's wait for it drain the previous tile's stores)
+    if (!PERSIST && (a.wbad[0] | a.wbad[1])) {
         if (t == 0) *flag = 1;
         return false;
     }
@@ -491,8 +493,18 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
         if (ns > 2) issueA(2, r0);
         issueW(0, 0);
     };
-    if (!PERSIST || !pre) prologue(row0);
-    wait_vmcnt<0>();  // (persistent: also the previous tile's output stores, issued after the prefetch)
+    if (!PERSIST || !pre) {
+        prologue(row0);
+        wait_vmcnt<0>();
+    } else if (a.g4) {
+        // prefetched by the previous tile, whose epilogue then issued 136 stores (a full tile: 128 tape + 8 out)
+        // after it.  vmcnt counts in issue order and saturates at 63 in flight, so vmcnt(63) has the prefetch
+        // landed while the youngest stores keep draining under this tile's first step (its end-of-step wait
+        // retires them)
+        wait_vmcnt<63>();
+    } else {
+        wait_vmcnt<8>();  // the 8 output stores of the previous (full) tile's flush stay in flight
+    }
     barrier_lds();
     lsplit(0, fas[0]);
     // one 32-k step; two static copies (input, hidden): the weight buffer's parity is a runtime offset and
@@ -600,30 +612,48 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
             }
         }
     }
-    bool prefetched = false;
-    if constexpr (PERSIST) {
-        if (next >= 0) {
-            // the slots' rows are this wave's own (its activation DMA and its reads cover rows wr .. wr + 15), so
-            // once its h reads have returned it may refill them; weight buffer 0 was last read before the k
-            // loop's final barrier
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            prologue(next * TR);
-            prefetched = true;
-        }
-    }
     constexpr float sc = 1.0f / (float)(1 << kH2Shift);  // exact power of two
     // packed fp32 (v_pk_mul / v_pk_add on row pairs): no MFMAs run here, so the packed forms halve the
     // epilogue's vector issue instead of competing with matrix work
+    // LayerNorm scale / bias, loaded with the gate biases.  Persistent: parked in a per-wave LDS copy
+    // ([128 scale | 128 bias], weight buffer 1 past the stage) instead of 16 registers across the epilogue
+    float lsc[8], lbs[8];
+    float *const lnp = reinterpret_cast<float *>(Bs) + NI * IMG * 4 + NW * 16 * SW + w * 2 * H;
+    static_assert(!PERSIST || (NI * IMG * 4 + NW * 16 * SW + NW * 2 * H) * 4 <= (2 * NI * IMG * 16 - 32),
+                  "stage + LayerNorm copies fit weight buffer 1 below the range-check flags");
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int u = 16 * j + l16;
-        const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
-        const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
+        float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
+        float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
+        // persistent: the compiler counts only its own loads, so a wait for these placed after the prefetch
+        // (it sinks their consumers there) would also wait for the whole prefetch; passing them through an
+        // empty asm makes it wait for them here, ahead of the prefetch
+        if constexpr (PERSIST) asm volatile("" : "+v"(br), "+v"(bz), "+v"(bni), "+v"(bnh));
+        lsc[j] = a.ln_scale[u];
+        lbs[j] = a.ln_bias[u];
+        if (PERSIST && g == 0) {
+            lnp[u] = lsc[j];
+            lnp[H + u] = lbs[j];
+        }
         const f32x4g s4 = {sc, sc, sc, sc};
         acc[0][j] = acc[0][j] * s4 + f32x4g{br, br, br, br};
         acc[1][j] = acc[1][j] * s4 + f32x4g{bz, bz, bz, bz};
         acc[2][j] = acc[2][j] * s4 + f32x4g{bni, bni, bni, bni};
         acc[3][j] = acc[3][j] * s4 + f32x4g{bnh, bnh, bnh, bnh};
+    }
+    bool prefetched = false;
+    if constexpr (PERSIST) {
+        if (next >= 0) {
+            // the slots' rows are this wave's own (its activation DMA and its reads cover rows wr .. wr + 15), so
+            // once its h reads have returned it may refill them; weight buffer 0 was last read before the k
+            // loop's final barrier.  Issued after the epilogue's last global LOADS (the biases and LayerNorm
+            // parameters above, already consumed): vmcnt counts in issue order, so a load issued after the
+            // prefetch would make its consumer wait for the whole prefetch round trip.
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            prologue(next * TR);
+            prefetched = true;
+        }
     }
     // float4 rows of the wave's [16][128] stage -> dst (row stride ld), rows < R only.  The stage is
     // wave-private and a wave's LDS operations complete in issue order, so waiting for its own stage
@@ -727,7 +757,7 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
 #pragma unroll
         for (int j = j0; j < j0 + JH; ++j) {
             const int u = 16 * j + l16;
-            const float scl = a.ln_scale[u], lb = a.ln_bias[u];
+            const float scl = PERSIST ? lnp[u] : lsc[j], lb = PERSIST ? lnp[H + u] : lbs[j];
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
                 const f2 hn = {acc[0][j][2 * p], acc[0][j][2 * p + 1]};
@@ -751,6 +781,11 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2s_kernel(GruX3rArgs
 // The argument block is re-read from the kernarg segment per tile (the segment pointer is laundered), so its
 // ~40 SGPRs of pointers are not held across the tile loop.
 __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2p_kernel(GruX3rArgs a, int ntiles) {
+    if (a.wbad[0] | a.wbad[1]) {  // weights out of fp16 range: the bf16x3 launch does every tile
+        for (int tile = blockIdx.x + threadIdx.x * gridDim.x; tile < ntiles; tile += blockDim.x * gridDim.x)
+            a.flags[tile] = 1;
+        return;
+    }
     bool pre = false;
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int next = tile + (int)gridDim.x < ntiles ? tile + (int)gridDim.x : -1;

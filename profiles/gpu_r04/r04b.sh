@@ -12,3 +12,5 @@ timeout -k 10 300 python -u -m pytest tests/test_gru_fused_gpu.py -q --timeout 2
 echo "gru tests rc $?"; tail -3 gpurun_out/r04b_gru_tests.log
 timeout -k 10 200 python -u -m pytest tests/test_debug_build.py -q --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/r04b_debug_tests.log 2>&1
 echo "debug tests rc $?"; tail -3 gpurun_out/r04b_debug_tests.log
+timeout -k 10 400 python -u -m pytest tests/test_gru_bwd_reduction_gpu.py tests/test_mappo_gpu.py -q -k "reduction or every_adam_step" --timeout 350 --timeout-method thread -p no:cacheprovider --durations=5 > gpurun_out/r04b_parity_tests.log 2>&1
+echo "parity tests rc $?"; tail -12 gpurun_out/r04b_parity_tests.log

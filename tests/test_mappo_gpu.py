@@ -145,17 +145,25 @@ def _yard_close(dev, ref, yard, factor, what, rtol=1e-5, extra=None):
     assert (err <= bound).all(), f"{what}: max err {err.max():.3g}, worst ratio {(err / bound).max():.3g}"
 
 
-@pytest.mark.parametrize("V,C,vpa,H,L,mode", [
-    (50, 218, 10, 128, 16, 0),  # uf50-218, 5 agents, the reference's H = 128, L = 16
-    (23, 97, 10, 64, 2, 1),  # mode 1 with a padded variable slot (agents of 8, 8, 7)
-])
-def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode):
+# (V, C, vars_per_agent, H, L, mode, (T, B, MB, E))
+TRAIN_CYCLE_CASES = [
+    (50, 218, 10, 128, 16, 0, (2, 4, 4, 2)),  # uf50-218, 5 agents, the reference's H = 128, L = 16
+    (23, 97, 10, 64, 2, 1, (2, 4, 4, 2)),  # mode 1 with a padded variable slot (agents of 8, 8, 7)
+    # BASELINE config 4's network: uf200-860, 25 agents of m = 8, two samples, two Adam steps (the fp64
+    # oracle runs 25 dense masked 200 x 860 encoders per sample and step; L = 8 keeps it to seconds)
+    (200, 860, 8, 128, 8, 0, (1, 2, 1, 1)),
+]
+
+
+@pytest.mark.parametrize("V,C,vpa,H,L,mode,shape", TRAIN_CYCLE_CASES)
+def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode, shape):
     """Teacher-forced replay of a whole train cycle: for every Adam step the oracle starts from the
     parameters the device started from (recorded by ``MAPPOLearner.trace``), so each minibatch is
     checked at the north_star bar without the drift of an independent replay (next test):
-      * rollout log-probs and values, GAE targets: 1e-5 relative (+ 4x the fp32 oracle's error);
+      * rollout log-probs and values, GAE targets: 1e-5 relative (+ 2x the fp32 oracle's error);
       * the loss triple of EVERY minibatch (the first one included): 1e-5 relative;
-      * the gradient of every minibatch: 1e-5 relative + 8x the fp32 oracle's error per tensor;
+      * the gradient of every minibatch: 1e-5 relative + 4x the fp32 oracle's error per tensor (the
+        factors of the network depth tests, tests/test_gnn_gpu.py; round 3 allowed 4x / 8x);
       * the Adam step: the device's new parameters vs optax.adam applied in float64 to the device's
         own gradient (1e-5 relative).
     Mode 1 runs with a padded slot: the parameters must stay finite (the slot counts as 0)."""
@@ -165,10 +173,10 @@ def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode):
     from marlsat.random import PRNGKey
     from marlsat.utils.generate_cnf_dataset import generate_problem_pool
 
-    T, B, MB, E = 2, 4, 4, 2
+    T, B, MB, E = shape
     cfg = _cfg(NUM_ENVS=B, NUM_STEPS=T, MINIBATCH_SIZE=MB, UPDATE_EPOCHS=E, GNN_HIDDEN_DIM=H,
                GNN_NUM_MESSAGE_PASSING_STEPS=L, action_mode=mode)
-    pool = generate_problem_pool(V, C, 5, size_id=12)
+    pool = generate_problem_pool(V, C, 5, size_id=12, skip_isolated=True)
     env = SATEnv(V, C, max_steps=2, vars_per_agent=vpa, action_mode=mode)
     A, M = env.num_agents, env.max_vars_per_agent
     assert mode == 0 or V % A  # the mode-1 case must have padded slots
@@ -206,8 +214,8 @@ def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode):
     p_start = layout(learner.trace[0]["params"])
     lp64, v64 = rollout_terms(to_t(p_start, torch.float64))
     lp32, v32 = rollout_terms(to_t(p_start, torch.float32))
-    _yard_close(flat(tr["log_prob"]), lp64, lp32, 4.0, "rollout log_prob")
-    _yard_close(flat(tr["value"]), v64, v32, 4.0, "rollout value")
+    _yard_close(flat(tr["log_prob"]), lp64, lp32, 2.0, "rollout log_prob")
+    _yard_close(flat(tr["value"]), v64, v32, 2.0, "rollout value")
     adv, tgt = om.gae(tr["reward"], tr["value"], tr["done"].astype(bool), learner.last_val.cpu().numpy(),
                       cfg["GAMMA"], cfg["GAE_LAMBDA"])
     np.testing.assert_allclose(learner.targets.cpu().numpy(), tgt, rtol=1e-5, atol=1e-7)
@@ -243,7 +251,7 @@ def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode):
                                    err_msg=f"Adam step {s}: (value_loss, loss_actor, entropy)")
         g_dev = layout(rec["grads"])
         for k in P_s:
-            _yard_close(g_dev[k], out[torch.float64][1][k], out[torch.float32][1][k], 8.0, f"step {s} grad {k}",
+            _yard_close(g_dev[k], out[torch.float64][1][k], out[torch.float32][1][k], 4.0, f"step {s} grad {k}",
                         extra=kink[k])
         # optax.adam in float64 on the device's own gradient, from the device's own parameters
         gflat = rec["grads"].double().cpu()
