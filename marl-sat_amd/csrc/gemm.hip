@@ -228,6 +228,43 @@ __global__ void wgrad_reduce4_kernel(const float4 *__restrict__ part, int splits
     *w = a;
 }
 
+// Two wgrad_reduce4 launches in one (a GRU cell's dual weight gradient): blocks [0, nb0) reduce segment 0,
+// the rest segment 1; per element the same adds in the same order as wgrad_reduce4_kernel.
+struct Reduce4Seg {
+    const float4 *part;
+    float4 *W;
+    int splits, K, N4, ldw4, accumulate, blocks;
+};
+__global__ void wgrad_reduce4_dual_kernel(Reduce4Seg s0, Reduce4Seg s1) {
+    const bool second = (int)blockIdx.x >= s0.blocks;
+    const Reduce4Seg &q = second ? s1 : s0;
+    const int t = (blockIdx.x - (second ? s0.blocks : 0)) * blockDim.x + threadIdx.x;
+    const size_t KN4 = (size_t)q.K * q.N4;
+    if (t >= (int)KN4) return;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    int i = 0;
+    for (; i + 8 <= q.splits; i += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = q.part[(size_t)(i + u) * KN4 + t];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+        }
+    }
+    for (; i < q.splits; ++i) {
+        const float4 v = q.part[(size_t)i * KN4 + t];
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    const int k = t / q.N4, n4 = t - k * q.N4;
+    float4 *w = q.W + (size_t)k * q.ldw4 + n4;
+    if (q.accumulate) {
+        const float4 o = *w;
+        a.x = o.x + a.x; a.y = o.y + a.y; a.z = o.z + a.z; a.w = o.w + a.w;
+    }
+    *w = a;
+}
+
 // W[k][n] (+)= sum_s part[s][k][n]  (fixed split order -> reproducible)
 __global__ void wgrad_reduce_kernel(const float *__restrict__ part, int splits, int K, int N, float *__restrict__ W,
                                     int ldw, int accumulate) {
@@ -621,6 +658,25 @@ extern "C" int msat_gemm_wgrad_h2_dual(const float *A0, int32_t lda0, const floa
     int rc = msat_wgrad_h2_dual_launch(A0, lda0, G0, ldg0, part0, K0, N0, rot0, A1, lda1, G1, ldg1, part1, K1, N1, rot1,
                                        rexp, M, splits, flags, s);
     if (rc) return rc;
+    const bool v0 = N0 % 4 == 0 && ldw0 % 4 == 0 && (reinterpret_cast<uintptr_t>(W0) & 15) == 0;
+    const bool v1 = N1 % 4 == 0 && ldw1 % 4 == 0 && (reinterpret_cast<uintptr_t>(W1) & 15) == 0;
+    if (v0 && v1) {  // both reduces in one launch (one kernel boundary fewer per GRU cell)
+        Reduce4Seg q[2];
+        const float *parts[2] = {part0, part1};
+        float *Ws[2] = {W0, W1};
+        for (int i = 0; i < 2; ++i) {
+            q[i].part = reinterpret_cast<const float4 *>(parts[i]);
+            q[i].W = reinterpret_cast<float4 *>(Ws[i]);
+            q[i].splits = splits;
+            q[i].K = Ks[i];
+            q[i].N4 = Ns[i] / 4;
+            q[i].ldw4 = ldws[i] / 4;
+            q[i].accumulate = accumulate;
+            q[i].blocks = (int)(((size_t)Ks[i] * (Ns[i] / 4) + 255) / 256);
+        }
+        hipLaunchKernelGGL(wgrad_reduce4_dual_kernel, dim3(q[0].blocks + q[1].blocks), dim3(256), 0, s, q[0], q[1]);
+        return check_launch("wgrad_reduce4_dual_kernel");
+    }
     rc = wgrad_reduce(part0, splits, K0, N0, W0, ldw0, accumulate, s);
     if (rc) return rc;
     return wgrad_reduce(part1, splits, K1, N1, W1, ldw1, accumulate, s);

@@ -542,6 +542,46 @@ partial_reduce_kernel(const float *__restrict__ part, int nblocks, int width, fl
     }
 }
 
+// Up to four partial_reduce4 launches in one (the GRU backward's LN / gate-bias / feature gradients): block b
+// serves segment i while b < ends[i]; per column the same adds in the same order as partial_reduce4_kernel.
+struct PartialSeg4 {
+    const float4 *src[4];
+    float4 *dst[4];
+    int N4[4], accumulate[4], ends[4];
+    int nseg, nrows, ld4;
+};
+__global__ void __launch_bounds__(256)
+partial_reduce4_multi_kernel(PartialSeg4 p) {
+    __shared__ float4 red[16][16];
+    int i = 0, b0 = 0;
+    while (i + 1 < p.nseg && (int)blockIdx.x >= p.ends[i]) b0 = p.ends[i++];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int c = ((int)blockIdx.x - b0) * 16 + tx;
+    const int N4 = p.N4[i];
+    const float4 *part = p.src[i];
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < N4)
+        for (int r = ty; r < p.nrows; r += 16) {
+            const float4 v = part[(size_t)r * p.ld4 + c];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+    red[ty][tx] = a;
+    __syncthreads();
+    if (ty == 0 && c < N4) {
+        float4 t = red[0][tx];
+        for (int k = 1; k < 16; ++k) {
+            const float4 v = red[k][tx];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        float4 *dst = p.dst[i];
+        if (p.accumulate[i]) {
+            const float4 o = dst[c];
+            t.x = o.x + t.x; t.y = o.y + t.y; t.z = o.z + t.z; t.w = o.w + t.w;
+        }
+        dst[c] = t;
+    }
+}
+
 // Column sums of G (M x N): block (column chunk of 256, row split) partials, then partial_reduce.
 __global__ void __launch_bounds__(256)
 colsum_partial_kernel(const float *__restrict__ G, int ldg, int M, int N, int rows_per, float *__restrict__ part) {
@@ -926,21 +966,28 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
                        reinterpret_cast<const float4 *>(partial), W4, nb, W4, kPartRows, reinterpret_cast<float4 *>(ws));
     rc = check_launch("colsum4_kernel");
     if (rc) return rc;
+    // stage 2: the segments [dln (2H) | dbi (3H) | dbh_n (H) | dfeat (3 nfeat H, the input matrix's feature rows,
+    // accumulated)] of the reduced row, in ONE launch (partial_reduce4_multi_kernel)
     const float4 *ws4 = reinterpret_cast<const float4 *>(ws);
-    hipLaunchKernelGGL(partial_reduce4_kernel, dim3((2 * H / 4 + 15) / 16), dim3(256), 0, s, ws4, sp, 2 * H / 4, W4,
-                       reinterpret_cast<float4 *>(dln_scale), accumulate_ln);
+    PartialSeg4 ps{};
+    ps.nrows = sp;
+    ps.ld4 = W4;
+    auto add_seg = [&](int off4, int n4, float *dst, int acc) {
+        const int i = ps.nseg++;
+        ps.src[i] = ws4 + off4;
+        ps.dst[i] = reinterpret_cast<float4 *>(dst);
+        ps.N4[i] = n4;
+        ps.accumulate[i] = acc;
+        ps.ends[i] = (i ? ps.ends[i - 1] : 0) + (n4 + 15) / 16;
+    };
+    add_seg(0, 2 * H / 4, dln_scale, accumulate_ln);
     if (bias) {
-        hipLaunchKernelGGL(partial_reduce4_kernel, dim3((3 * H / 4 + 15) / 16), dim3(256), 0, s, ws4 + 2 * H / 4, sp,
-                           3 * H / 4, W4, reinterpret_cast<float4 *>(dbi), 1);
-        hipLaunchKernelGGL(partial_reduce4_kernel, dim3((H / 4 + 15) / 16), dim3(256), 0, s, ws4 + 5 * H / 4, sp, H / 4,
-                           W4, reinterpret_cast<float4 *>(dbh_n), 1);
+        add_seg(2 * H / 4, 3 * H / 4, dbi, 1);
+        add_seg(5 * H / 4, H / 4, dbh_n, 1);
     }
-    if (nfeat) {  // feature rows: nfeat x 3H contiguous (the rows of the input matrix, ld 3H), accumulated
-        const int fw4 = 3 * nfeat * H / 4;
-        hipLaunchKernelGGL(partial_reduce4_kernel, dim3((fw4 + 15) / 16), dim3(256), 0, s, ws4 + 6 * H / 4, sp, fw4, W4,
-                           reinterpret_cast<float4 *>(dfeat), 1);
-    }
-    return check_launch("partial_reduce4_kernel");
+    if (nfeat) add_seg(6 * H / 4, 3 * nfeat * H / 4, dfeat, 1);
+    hipLaunchKernelGGL(partial_reduce4_multi_kernel, dim3(ps.ends[ps.nseg - 1]), dim3(256), 0, s, ps);
+    return check_launch("partial_reduce4_multi_kernel");
 }
 
 extern "C" int msat_gru_ln_bwd_g4f(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev,

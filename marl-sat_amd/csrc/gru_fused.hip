@@ -780,7 +780,7 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2s_kernel(GruX3rArgs
 // (the same XCD's tiles: workgroup b sits on XCD b % 8), each prefetching the next one's prologue.
 // The argument block is re-read from the kernarg segment per tile (the segment pointer is laundered), so its
 // ~40 SGPRs of pointers are not held across the tile loop.
-__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2p_kernel(GruX3rArgs a, int ntiles) {
+__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2p_kernel(GruX3rArgs a, int ntiles, int prefetch) {
     if (a.wbad[0] | a.wbad[1]) {  // weights out of fp16 range: the bf16x3 launch does every tile
         for (int tile = blockIdx.x + threadIdx.x * gridDim.x; tile < ntiles; tile += blockDim.x * gridDim.x)
             a.flags[tile] = 1;
@@ -788,7 +788,7 @@ __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2p_kernel(GruX3rArgs
     }
     bool pre = false;
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int next = tile + (int)gridDim.x < ntiles ? tile + (int)gridDim.x : -1;
+        const int next = prefetch && tile + (int)gridDim.x < ntiles ? tile + (int)gridDim.x : -1;
         typedef __attribute__((address_space(4))) const GruX3rArgs KArgs;
         KArgs *ka = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(ka));
@@ -1261,9 +1261,9 @@ extern "C" int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w
     a.wbad = wbad;
     const int tiles = (R + 127) / 128;
     const char *pe = getenv("MARLSAT_GRU_PERSIST");  // A/B switch (round 4)
-    if (pe && pe[0] == '1') {
+    if (pe && (pe[0] == '1' || pe[0] == '2')) {  // 2: the persistent walk without the prefetch (ablation)
         hipLaunchKernelGGL(gru_ln_fused_fwd_h2p_kernel, dim3(std::min(tiles, device_cus())), dim3(512), 0,
-                           (hipStream_t)stream, a, tiles);
+                           (hipStream_t)stream, a, tiles, pe[0] == '1' ? 1 : 0);
         rc = check_launch("gru_ln_fused_fwd_h2p_kernel");
     } else {
         hipLaunchKernelGGL(gru_ln_fused_fwd_h2s_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
