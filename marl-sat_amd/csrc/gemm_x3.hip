@@ -15,9 +15,9 @@
 // LDS-DMA.  128x128 tile per 256-thread workgroup (wave = 64x64 = 2x2 MFMA tiles), 16-deep slabs,
 // double-buffered in LDS, A prefetched two slabs ahead in registers (the six bf16 MFMAs of a slab
 // are too short to cover an HBM load issued one slab ahead).
-#include <stdlib.h>
 
 #include <algorithm>
+#include <stdlib.h>
 
 #include "common.h"
 #include "split3.h"
@@ -656,6 +656,220 @@ gemm_h2r16_dual_kernel(DgradProblem p0, DgradProblem p1, const int *__restrict__
                              lds_w, p.kr);
 }
 
+// Resident-weight form of the dual data gradient (msat_gemm_h2_dual when K = 384, a GRU cell's 3H at
+// H = 128, and both N are multiples of 64).  The per-tile kernel above re-stages its 128 x K weight tile through LDS for every
+// 128-row block: four weight DMA pieces and a barrier per wave and k step beside 48 MFMAs, and the
+// stamps put 39 % of its wave cycles in issuing those memory operations.  Here one
+// 512-thread workgroup per CU keeps ONE 64-column tile of one product's weight planes in LDS for the
+// whole launch (NP x 64 x K halves: 96 KiB fp16x2, 144 KiB bf16x3 at K = 384) and walks 512-row blocks
+// (8 waves x 64 rows, register-A as above).  The k loop has no barrier and no DMA: per wave and step,
+// eight activation loads (prefetched PF steps ahead, across block boundaries), eight ds_read_b128 of the
+// resident image and 48 MFMAs.  The T = N0 / 64 + N1 / 64 tiles of a row block form a group; a group's
+// workgroups sit on one XCD (blockIdx % 8) and walk the same blocks in the same order, with the second
+// product's walk started kr slabs in as above, so the packed rows come from HBM once and from L2 for
+// the other T - 1 tiles.  The arithmetic per output element (split, MFMA sequence, k order, rescale,
+// accumulate) is the per-tile kernel's: the two forms agree bitwise (tests/test_gemm_gpu.py).
+constexpr int kRsT = 512, kRsRT = 2, kRsRows = 8 * 16 * kRsRT, kRsMaxD = 12;
+constexpr int kRsImg = 3 * kRsMaxD * 4 * 64;  // uint4s of the largest weight image (bf16x3, K = 384)
+
+struct DgradResident {
+    DgradProblem p[2];
+    int T0, T;   // 64-column tiles of product 0, of both
+    int gx, ng;  // groups of T workgroups per XCD in the XCD-aligned part; groups in all
+    int nrb;     // 512-row blocks
+};
+
+template <int NP, int PF, int ND>
+__device__ __forceinline__ void dgrad_resident_body(const DgradProblem &p, const int *__restrict__ rexp, int M,
+                                                    int n0, int grp, int ng, int nb, uint4 *lds) {
+    typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+    constexpr int RT = kRsRT, nd = ND, K = 32 * ND;
+    static_assert(ND <= kRsMaxD && ND % PF == 0, "resident image / prefetch ring");
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63, l16 = lane & 15, g = lane >> 4;
+    // the weight tile, once: image [q][d][j][lane] = 16 B of plane q, column n0 + 16 j + (lane & 15),
+    // k 32 d + 8 (lane >> 4) .. + 7 -- each ds_read_b128 below reads 1 KiB contiguous (no conflicts)
+    {
+        const uint16_t *Wp = NP == 2 ? p.Wh2 : p.Wx3;
+        constexpr int per = nd * 256;
+        static_assert((NP * per) % kRsT == 0, "whole fill rounds");
+#pragma unroll
+        for (int u = 0; u < NP * per / kRsT; ++u) {  // unrolled: the loads go out together
+            const int c = t + kRsT * u;
+            const int q = c / per, rem = c - q * per, d = rem >> 8, j = (rem >> 6) & 3, ln = rem & 63;
+            const int n = n0 + 16 * j + (ln & 15), k = 32 * d + 8 * (ln >> 4);
+            MSAT_DCHECK(((size_t)q * p.N + n) * K + k + 8, (size_t)NP * p.N * K + 1);
+            lds[c] = *reinterpret_cast<const uint4 *>(Wp + ((size_t)q * p.N + n) * K + k);
+        }
+    }
+    __syncthreads();
+    const int kr = p.kr;
+    auto sl = [&](int d) { const int x = d + kr; return x >= nd ? x - nd : x; };
+    auto rowof = [&](int b, int i) { return (grp + b * ng) * kRsRows + w * 16 * RT + 16 * i; };
+    auto loadA = [&](int b, int d, float4 (&ra)[RT][2]) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            const int r = min(rowof(b, i) + l16, M - 1);
+            const float *a = p.A + (size_t)r * p.lda + 8 * g + 32 * d;
+            ra[i][0] = *reinterpret_cast<const float4 *>(a);
+            ra[i][1] = *reinterpret_cast<const float4 *>(a + 4);
+        }
+    };
+    auto expof = [&](int b, int (&ea)[RT]) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            const int e = rexp[min(rowof(b, i) + l16, M - 1)];
+            ea[i] = e == kExpZero ? 0 : e;
+        }
+    };
+    float4 ras[PF][RT][2];
+#pragma unroll
+    for (int x = 0; x < PF; ++x) loadA(0, sl(x), ras[x]);
+    int ea[RT] = {};
+    if constexpr (NP == 2) expof(0, ea);
+    float *stage = reinterpret_cast<float *>(lds + kRsImg) + w * 256;  // 16 x 16 fp32 per wave (writes 2-way)
+    for (int b = 0; b < nb; ++b) {
+        // the next block's row exponents and this block's old C (accumulate), issued now: both land under the
+        // block's k walk (unconditional loads of clamped rows keep hipcc's vmcnt bookkeeping exact)
+        int ean[RT];
+        if constexpr (NP == 2) expof(min(b + 1, nb - 1), ean);
+        const int r0 = rowof(b, 0);
+        float4 old[RT][4];
+        if (p.accumulate) {
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                const float *oc = p.C + (size_t)min(r0 + 16 * i + (lane >> 2), M - 1) * p.ldc + n0 + 4 * (lane & 3);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) old[i][j] = *reinterpret_cast<const float4 *>(oc + 16 * j);
+            }
+        }
+        f32x4 acc[RT][4];
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+        auto step = [&](int dd, float4 (&ra)[RT][2]) {
+            const int d = sl(dd);
+            uint4 fa[RT][NP];
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                if constexpr (NP == 3) {
+                    const Split8 sp = split8(ra[i][0], ra[i][1]);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) fa[i][q] = sp.p[q];
+                } else {
+                    const float4 u = ra[i][0], v = ra[i][1];
+                    const int e = ea[i];
+                    const SplitH4 s0 = splith4(make_float4(ldexpf(u.x, e), ldexpf(u.y, e), ldexpf(u.z, e), ldexpf(u.w, e)));
+                    const SplitH4 s1 = splith4(make_float4(ldexpf(v.x, e), ldexpf(v.y, e), ldexpf(v.z, e), ldexpf(v.w, e)));
+                    fa[i][0] = make_uint4(s0.p[0].x, s0.p[0].y, s1.p[0].x, s1.p[0].y);
+                    fa[i][1] = make_uint4(s0.p[1].x, s0.p[1].y, s1.p[1].x, s1.p[1].y);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep each step's split, loads and MFMAs in their place
+            // this set was just split: refill it PF steps ahead (into the next block past the last step;
+            // the last block re-reads its own rows there, so every step issues the same loads and hipcc's
+            // vmcnt bookkeeping stays exact across the loop)
+            {
+                const bool in = dd + PF < nd;
+                loadA(in ? b : min(b + 1, nb - 1), sl(in ? dd + PF : dd + PF - nd), ra);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint4 fb[NP];
+#pragma unroll
+                for (int q = 0; q < NP; ++q) fb[q] = lds[((q * nd + d) * 4 + j) * 64 + lane];
+#pragma unroll
+                for (int i = 0; i < RT; ++i) {
+                    f32x4 c = acc[i][j];
+                    if constexpr (NP == 3) {
+                        auto m = [](const uint4 &a, const uint4 &bb, const f32x4 &c) {
+                            return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                                           __builtin_bit_cast(bf16x8, bb), c, 0, 0, 0);
+                        };
+                        c = m(fa[i][2], fb[0], c);
+                        c = m(fa[i][1], fb[1], c);
+                        c = m(fa[i][0], fb[2], c);
+                        c = m(fa[i][1], fb[0], c);
+                        c = m(fa[i][0], fb[1], c);
+                        c = m(fa[i][0], fb[0], c);
+                    } else {
+                        auto m = [](const uint4 &a, const uint4 &bb, const f32x4 &c) {
+                            return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8v, a),
+                                                                          __builtin_bit_cast(f16x8v, bb), c, 0, 0, 0);
+                        };
+                        c = m(fa[i][0], fb[1], c);  // h l
+                        c = m(fa[i][1], fb[0], c);  // l h
+                        c = m(fa[i][0], fb[0], c);  // h h
+                    }
+                    acc[i][j] = c;
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+#pragma unroll
+        for (int dd = 0; dd < nd; dd += PF) {
+#pragma unroll
+            for (int x = 0; x < PF; ++x) step(dd + x, ras[x]);
+        }
+        // epilogue: rescale rows by 2^-(e + kDgW) (the C/D map: lane (l16, g) holds rows 4 g + reg, column
+        // l16), then per 16 x 16 block through the wave's stage to float4 rows (+ the old C), stored
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            if constexpr (NP == 2) {
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) {
+                    const int sh = -(__shfl(ea[i], 4 * g + reg, 16) + kDgW);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[i][j][reg] = ldexpf(acc[i][j][reg], sh);
+                }
+            }
+            const int row = r0 + 16 * i + (lane >> 2);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) stage[(4 * g + reg) * 16 + l16] = acc[i][j][reg];
+                asm volatile("" ::: "memory");  // the wave's own LDS ops run in order; keep hipcc's order too
+                float4 v = *reinterpret_cast<const float4 *>(stage + (lane >> 2) * 16 + 4 * (lane & 3));
+                asm volatile("" ::: "memory");
+                if (p.accumulate) {
+                    const float4 &ov = old[i][j];
+                    v.x = ov.x + v.x; v.y = ov.y + v.y; v.z = ov.z + v.z; v.w = ov.w + v.w;
+                }
+                if (row < M) *reinterpret_cast<float4 *>(p.C + (size_t)row * p.ldc + n0 + 16 * j + 4 * (lane & 3)) = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RT; ++i) ea[i] = ean[i];
+    }
+}
+
+template <int PF>
+__global__ void __launch_bounds__(kRsT, 1) gemm_h2_dual_resident_kernel(DgradResident a, const int *__restrict__ rexp,
+                                                                         int M) {
+    __shared__ uint4 lds[kRsImg + 8 * 64];  // weight image + eight 1 KiB wave stages: 152 KiB
+    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+    int grp, tile;
+    if (local < a.gx * a.T) {
+        grp = (local / a.T) * 8 + xcd;
+        tile = local % a.T;
+    } else {  // the CUs an XCD has left over: groups spread over XCDs
+        const int e = (local - a.gx * a.T) * 8 + xcd;
+        grp = 8 * a.gx + e / a.T;
+        tile = e % a.T;
+        if (grp >= a.ng) return;
+    }
+    const int nb = grp < a.nrb ? (a.nrb - grp + a.ng - 1) / a.ng : 0;
+    if (nb == 0) return;
+    const bool first = tile < a.T0;
+    const DgradProblem &p = first ? a.p[0] : a.p[1];
+    const int n0 = (first ? tile : tile - a.T0) * 64;
+    if (*p.wbad)
+        dgrad_resident_body<3, 2, kRsMaxD>(p, rexp, M, n0, grp, a.ng, nb, lds);
+    else
+        dgrad_resident_body<2, PF, kRsMaxD>(p, rexp, M, n0, grp, a.ng, nb, lds);
+}
+
 // planes[q][r][c] = part q of 2^kDgW W[r][(c + rot) % cols] (fp16x2, q = 0, 1); *bad = 1 if a scaled
 // weight is outside (-2^15, 2^15) or not finite (msat_gemm_h2 then runs its bf16x3 body)
 __global__ void split_f16x2_rot_kernel(const float *__restrict__ W, int rows, int cols, int ldw, int rot,
@@ -1210,6 +1424,20 @@ extern "C" int msat_gemm_h2(const float *A, int32_t lda, const int32_t *rexp, co
     return check_launch("gemm_h2r16_kernel");
 }
 
+// compute units of the current device (the resident kernel's grid: 8 XCDs x cpx), read once
+static int dgrad_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v >= 8)
+            n = v;
+        else
+            n = 256;
+    }
+    return n;
+}
+
 // C0 (+)= A0 @ W0^T and C1 (+)= A1 @ W1^T over the same M rows (one row-exponent array), in one launch
 // (gemm_h2r16_dual_kernel).  Conditions of msat_gemm_h2 for each product; no bias.
 extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h2, const void *W0_x3,
@@ -1253,12 +1481,31 @@ extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h
         const long off = (long)(A0 - A1);
         if (lda0 == lda1 && off > 0 && off % 32 == 0 && off / 32 < K / 32) p[1].kr = (int)(off / 32);
     }
-    const char *rte = getenv("MARLSAT_DGRAD_RT");  // A/B switch (round 4): 4 = 256-row tiles
-    if (rte && rte[0] == '4') {
-        const int ntm = (M + 255) / 256;
-        hipLaunchKernelGGL((gemm_h2r16_dual_kernel<4>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(kX3T), 0,
-                           (hipStream_t)stream, p[0], p[1], rexp, M, K);
-        return check_launch("gemm_h2r16_dual_kernel<4>");
+    // the resident-weight form (opt-in, measured slower: DESIGN.md round 4): K = 384, 64-column tiles, float4
+    // rows out, T tiles no more than an XCD's CUs
+    const int cpx = dgrad_cus() / 8;
+    const char *ab = getenv("MARLSAT_DGRAD_RESIDENT");  // 1 (or the prefetch depth 2 / 3 / 4) = resident form
+    if (ab && ab[0] >= '1' && ab[0] <= '4' && K == 32 * kRsMaxD && N0 % 64 == 0 && N1 % 64 == 0 && p[0].vec_out &&
+        p[1].vec_out && N0 / 64 + N1 / 64 <= cpx) {
+        DgradResident r;
+        r.p[0] = p[0];
+        r.p[1] = p[1];
+        r.T0 = N0 / 64;
+        r.T = r.T0 + N1 / 64;
+        r.gx = cpx / r.T;
+        r.ng = 8 * r.gx + 8 * (cpx - r.gx * r.T) / r.T;
+        r.nrb = (M + kRsRows - 1) / kRsRows;
+        const int pf = ab && ab[0] >= '2' && ab[0] <= '4' ? ab[0] - '0' : 3;  // A/B: prefetch depth
+        if (pf == 2)
+            hipLaunchKernelGGL(gemm_h2_dual_resident_kernel<2>, dim3(8 * cpx), dim3(kRsT), 0, (hipStream_t)stream, r,
+                               rexp, M);
+        else if (pf == 4)
+            hipLaunchKernelGGL(gemm_h2_dual_resident_kernel<4>, dim3(8 * cpx), dim3(kRsT), 0, (hipStream_t)stream, r,
+                               rexp, M);
+        else
+            hipLaunchKernelGGL(gemm_h2_dual_resident_kernel<3>, dim3(8 * cpx), dim3(kRsT), 0, (hipStream_t)stream, r,
+                               rexp, M);
+        return check_launch("gemm_h2_dual_resident_kernel");
     }
     const int ntm = (M + 127) / 128;
     hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(kX3T), 0,

@@ -368,3 +368,57 @@ def test_dual_launches_match_fp64(M, K1):
                hx.double().abs().t() @ dgh.double().abs() + W0.double().abs(), rtol=4e-6)
     _ref_close(gW1, torch.roll(xx.double().t() @ dgi.double(), 2 * H, dims=1) + W1.double(),
                torch.roll(xx.double().abs().t() @ dgi.double().abs(), 2 * H, dims=1) + W1.double().abs(), rtol=4e-6)
+
+
+@pytest.mark.parametrize("M,K1,wbig", [(1, 128, 0), (255, 256, 0), (257, 128, 0), (70001, 256, 0), (131071, 128, 0),
+                                       (4999, 256, 1)])
+def test_dual_resident_matches_per_tile(M, K1, wbig, monkeypatch):
+    """msat_gemm_h2_dual's resident-weight kernel (MARLSAT_DGRAD_RESIDENT=1, gemm_h2_dual_resident_kernel: 64-column
+    weight tiles kept in LDS, 256-row blocks walked per workgroup) against the per-tile kernel (default): the same
+    split, MFMA sequence, k order and rescale per output element, so both outputs agree exactly -- ragged last
+    blocks, both GRU cell shapes (K1 = 128 / 256), dh accumulated onto its old value, and a weight past the
+    fp16x2 range (wbig: the bf16x3 planes, NP = 3 image)."""
+    from marlsat import _lib
+
+    H = 128
+    g = torch.Generator(device="cuda").manual_seed(M + K1 + wbig)
+    D = torch.randn(M, 4 * H, device="cuda", generator=g)
+    D *= torch.pow(10.0, torch.empty(M, 1, device="cuda").uniform_(-12, 1, generator=g))
+    D[::7] = 0
+    rexp = row_exp(D)
+    Wh = torch.randn(H, 3 * H, device="cuda", generator=g) * 0.1
+    F = torch.randn(K1, 3 * H, device="cuda", generator=g) * 0.1
+    if wbig:
+        F[5, 9] = 70.0
+    s = _lib.stream_ptr()
+    planes = []
+    for Wm in (Wh, F):
+        n, k = Wm.shape
+        p2 = torch.empty(2 * n * k + 8, dtype=torch.int16, device="cuda")
+        p3 = torch.empty(3 * n * k + 8, dtype=torch.int16, device="cuda")
+        bad = torch.empty(1, dtype=torch.int32, device="cuda")
+        rot = 0 if Wm is Wh else 2 * H
+        _lib.check(_lib.lib.msat_split_f16x2_rot(Wm.data_ptr(), n, k, k, rot, p2.data_ptr(), bad.data_ptr(), s), "s2")
+        _lib.check(_lib.lib.msat_split_bf16x3_rot(Wm.data_ptr(), n, k, k, rot, p3.data_ptr(), s), "s3")
+        planes.append((p2, p3, bad))
+    assert int(planes[1][2]) == wbig
+    C0 = torch.randn(M, H, device="cuda", generator=g)
+    outs = {}
+    for mode in (None, "1"):
+        if mode is None:
+            monkeypatch.delenv("MARLSAT_DGRAD_RESIDENT", raising=False)
+        else:
+            monkeypatch.setenv("MARLSAT_DGRAD_RESIDENT", mode)
+        dh = C0.clone()
+        dx = torch.full((M, K1), float("nan"), device="cuda")
+        _lib.check(_lib.lib.msat_gemm_h2_dual(
+            D.data_ptr() + 4 * H, 4 * H, planes[0][0].data_ptr(), planes[0][1].data_ptr(), planes[0][2].data_ptr(),
+            dh.data_ptr(), H, H, 1, D.data_ptr(), 4 * H, planes[1][0].data_ptr(), planes[1][1].data_ptr(),
+            planes[1][2].data_ptr(), dx.data_ptr(), K1, K1, 0, rexp.data_ptr(), M, 3 * H, s), "dual dgrad")
+        torch.cuda.synchronize()
+        outs[mode] = (dh, dx)
+    assert torch.equal(outs["1"][0], outs[None][0])
+    assert torch.equal(outs["1"][1], outs[None][1])
+    Fr = torch.roll(F.double(), -2 * H, dims=1)
+    dgi = D[:, :3 * H]
+    _ref_close(outs[None][1], dgi.double() @ Fr.t(), dgi.double().abs() @ Fr.abs().t())
