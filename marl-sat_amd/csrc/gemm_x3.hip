@@ -870,6 +870,197 @@ __global__ void __launch_bounds__(kRsT, 1) gemm_h2_dual_resident_kernel(DgradRes
         dgrad_resident_body<2, PF, kRsMaxD>(p, rexp, M, n0, grp, a.ng, nb, lds);
 }
 
+// Full-width form of the dual data gradient (msat_gemm_h2_dual for a GRU cell: N0 = 128, N1 = 128 / 256,
+// K = 384).  One 512-thread workgroup per 128-row block computes BOTH products over ALL N0 + N1 columns: each
+// wave holds 16 rows x 384 columns of accumulators (96 VGPRs), so every packed row is read from HBM once and
+// split once per k step for all columns, where the per-tile kernel reads and splits it once per 128-column
+// tile (three times) and leans on L2 for the re-reads.  Both products' weight slabs stream through LDS per
+// 32-deep step (48 KiB, double-buffered: 96 KiB fp16x2, 144 KiB bf16x3), LDS-DMA as above: per wave and
+// step 6 DMA pieces, 2 activation loads per operand, 48 ds_read_b128 and 72 MFMAs against the per-tile
+// kernel's 4 + 4 + 16 per 48 MFMAs.  The second product's k walk starts kr slabs in (host, as above), so for
+// kr = H / 32 the two products read the same packed columns for the first 3H - H of K: one split serves
+// both.  Per output element the arithmetic is the per-tile kernel's (split, MFMA order, k order, rescale,
+// accumulate): the two forms agree bitwise (tests/test_gemm_gpu.py).
+constexpr int kWdT = 512, kWdNR = 384;  // threads (8 waves x 16 rows); image rows per plane (N0 + N1 max)
+
+template <int NP, int J0, int J1>
+__device__ __forceinline__ void dgrad_wide_body(const DgradProblem &p0, const DgradProblem &p1,
+                                                const int *__restrict__ rexp, int M, int m0,
+                                                uint4 (*lds_w)[3][kWdNR * 4]) {
+    typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+    constexpr int nd = 12, K = 32 * nd, NR = 16 * (J0 + J1), PPW = NP * NR / 128;
+    static_assert(NR <= kWdNR && (NP * NR) % 128 == 0, "image rows / DMA pieces per wave");
+    const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: the DMA bases stay in SGPRs
+    const int row = min(m0 + 16 * w + l16, M - 1);  // this lane's activation row (register-A)
+    int ea = 0;
+    if constexpr (NP == 2) {
+        const int e = rexp[row];
+        ea = e == kExpZero ? 0 : e;
+    }
+    // weight DMA: piece x -> plane q, image rows 16 pp .. + 15 (product 0 below 16 J0, product 1 above)
+    unsigned voff[PPW];
+    const uint16_t *pbase[PPW];
+#pragma unroll
+    for (int e = 0; e < PPW; ++e) {
+        const int x = PPW * w + e, q = x / (NR / 16), pp = x % (NR / 16);
+        const int r = 16 * pp + (lane >> 2), ch = (lane & 3) ^ x3swz16((r >> 2) & 3);
+        const bool second = pp >= J0;
+        const int n = second ? r - 16 * J0 : r, N = second ? 16 * J1 : 16 * J0;
+        const uint16_t *W = NP == 2 ? (second ? p1.Wh2 : p0.Wh2) : (second ? p1.Wx3 : p0.Wx3);
+        pbase[e] = W;
+        voff[e] = (unsigned)(((size_t)q * N * K + (size_t)n * K + 8 * ch) * 2);
+    }
+    const int kr0 = p0.kr, kr1 = p1.kr;
+    auto sl0 = [&](int d) { const int x = d + kr0; return x >= nd ? x - nd : x; };
+    auto sl1 = [&](int d) { const int x = d + kr1; return x >= nd ? x - nd : x; };
+    auto issueW = [&](int d, int buf) {
+#pragma unroll
+        for (int e = 0; e < PPW; ++e) {
+            const int x = PPW * w + e, q = x / (NR / 16), pp = x % (NR / 16);
+            const int sl = pp >= J0 ? sl1(d) : sl0(d);
+            glds16_async_s(reinterpret_cast<const char *>(pbase[e]) + (size_t)sl * 64, voff[e], &lds_w[buf][q][64 * pp]);
+        }
+    };
+    const float *a0 = p0.A + (size_t)row * p0.lda + 8 * g, *a1 = p1.A + (size_t)row * p1.lda + 8 * g;
+    float4 ra[2][2][2];  // [prefetch set][product][half]
+    auto loadA = [&](int d, float4 (&r)[2][2]) {
+        const float *x0 = a0 + 32 * sl0(d), *x1 = a1 + 32 * sl1(d);
+        r[0][0] = *reinterpret_cast<const float4 *>(x0);
+        r[0][1] = *reinterpret_cast<const float4 *>(x0 + 4);
+        r[1][0] = *reinterpret_cast<const float4 *>(x1);  // the same columns when the walks align: an L1 hit
+        r[1][1] = *reinterpret_cast<const float4 *>(x1 + 4);
+    };
+    f32x4 acc[J0 + J1];
+#pragma unroll
+    for (int j = 0; j < J0 + J1; ++j) acc[j] = f32x4{};
+    loadA(0, ra[0]);
+    loadA(1, ra[1]);
+    issueW(0, 0);
+    wait_vmcnt<0>();
+    barrier_lds();
+    const int slot = g ^ x3swz16((l16 >> 2) & 3);
+    auto split = [&](const float4 (&r)[2], uint4 (&fa)[NP]) {
+        if constexpr (NP == 3) {
+            const Split8 sp = split8(r[0], r[1]);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) fa[q] = sp.p[q];
+        } else {
+            const float4 u = r[0], v = r[1];
+            const SplitH4 s0 = splith4(make_float4(ldexpf(u.x, ea), ldexpf(u.y, ea), ldexpf(u.z, ea), ldexpf(u.w, ea)));
+            const SplitH4 s1 = splith4(make_float4(ldexpf(v.x, ea), ldexpf(v.y, ea), ldexpf(v.z, ea), ldexpf(v.w, ea)));
+            fa[0] = make_uint4(s0.p[0].x, s0.p[0].y, s1.p[0].x, s1.p[0].y);
+            fa[1] = make_uint4(s0.p[1].x, s0.p[1].y, s1.p[1].x, s1.p[1].y);
+        }
+    };
+    auto mm = [&](const uint4 (&fa)[NP], const uint4 (&fb)[NP], f32x4 c) {
+        if constexpr (NP == 3) {
+            auto m = [](const uint4 &a, const uint4 &b, const f32x4 &c) {
+                return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                               c, 0, 0, 0);
+            };
+            c = m(fa[2], fb[0], c);
+            c = m(fa[1], fb[1], c);
+            c = m(fa[0], fb[2], c);
+            c = m(fa[1], fb[0], c);
+            c = m(fa[0], fb[1], c);
+            c = m(fa[0], fb[0], c);
+        } else {
+            auto m = [](const uint4 &a, const uint4 &b, const f32x4 &c) {
+                return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8v, a), __builtin_bit_cast(f16x8v, b),
+                                                              c, 0, 0, 0);
+            };
+            c = m(fa[0], fb[1], c);  // h l
+            c = m(fa[1], fb[0], c);  // l h
+            c = m(fa[0], fb[0], c);  // h h
+        }
+        return c;
+    };
+    const bool samek = p0.lda == p1.lda;
+#pragma unroll
+    for (int d = 0; d < nd; ++d) {
+        const int buf = d & 1;
+        float4 (&r)[2][2] = ra[d & 1];
+        uint4 fa0[NP], fa1[NP];
+        split(r[0], fa0);
+        // a use of the second operand's registers on every path: hipcc then waits for them here, with the
+        // first operand's (same age), instead of before refilling them below (which would also drain the DMA)
+        asm volatile("" ::"v"(r[1][0].x), "v"(r[1][0].y), "v"(r[1][0].z), "v"(r[1][0].w), "v"(r[1][1].x),
+                     "v"(r[1][1].y), "v"(r[1][1].z), "v"(r[1][1].w));
+        // one split for both products where their walks read the same packed columns (uniform)
+        if (samek && p0.A + 32 * sl0(d) == p1.A + 32 * sl1(d)) {
+#pragma unroll
+            for (int q = 0; q < NP; ++q) fa1[q] = fa0[q];
+        } else {
+            split(r[1], fa1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (d + 1 < nd) issueW(d + 1, buf ^ 1);
+        if (d + 2 < nd) loadA(d + 2, r);  // this set was just split
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < J0 + J1; ++j) {
+            uint4 fb[NP];
+#pragma unroll
+            for (int q = 0; q < NP; ++q) fb[q] = lds_w[buf][q][(16 * j + l16) * 4 + slot];
+            acc[j] = j < J0 ? mm(fa0, fb, acc[j]) : mm(fa1, fb, acc[j]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // W(d + 1) landed; A(d + 2), issued after it, may fly
+        if (d + 2 < nd) wait_vmcnt<4>();
+        else wait_vmcnt<0>();
+        barrier_lds();
+    }
+    // epilogue: rescale rows by 2^-(e + kDgW) (C/D map: lane (l16, g) holds rows 4 g + reg, column l16), old
+    // dh rows loaded first, the product-1 columns written while they land, then product 0's; each 16 x 16
+    // block goes through the wave's 1 KiB stage (the weight buffers are free after the last barrier) to
+    // float4 row pieces
+    if constexpr (NP == 2) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int sh = -(__shfl(ea, 4 * g + reg, 16) + kDgW);
+#pragma unroll
+            for (int j = 0; j < J0 + J1; ++j) acc[j][reg] = ldexpf(acc[j][reg], sh);
+        }
+    }
+    const int orow = m0 + 16 * w + (lane >> 2), oc4 = 4 * (lane & 3);
+    const int crow = min(orow, M - 1);
+    float4 old0[J0];
+    if (p0.accumulate) {
+#pragma unroll
+        for (int j = 0; j < J0; ++j)
+            old0[j] = *reinterpret_cast<const float4 *>(p0.C + (size_t)crow * p0.ldc + 16 * j + oc4);
+    }
+    float *stage = reinterpret_cast<float *>(&lds_w[0][0][0]) + w * 256;
+    auto put = [&](int j, const DgradProblem &p, int col0, const float4 *old) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) stage[(4 * g + reg) * 16 + l16] = acc[j][reg];
+        asm volatile("" ::: "memory");  // the wave's LDS operations run in order; keep hipcc's order too
+        float4 v = *reinterpret_cast<const float4 *>(stage + (lane >> 2) * 16 + oc4);
+        asm volatile("" ::: "memory");
+        if (p.accumulate) {
+            const float4 ov = old ? *old : *reinterpret_cast<const float4 *>(p.C + (size_t)crow * p.ldc + col0 + oc4);
+            v.x = ov.x + v.x; v.y = ov.y + v.y; v.z = ov.z + v.z; v.w = ov.w + v.w;
+        }
+        if (orow < M) *reinterpret_cast<float4 *>(p.C + (size_t)orow * p.ldc + col0 + oc4) = v;
+    };
+#pragma unroll
+    for (int j = 0; j < J1; ++j) put(J0 + j, p1, 16 * j, nullptr);
+#pragma unroll
+    for (int j = 0; j < J0; ++j) put(j, p0, 16 * j, &old0[j]);
+}
+
+template <int J1>
+__global__ void __launch_bounds__(kWdT, 1) gemm_h2_dual_wide_kernel(DgradProblem p0, DgradProblem p1,
+                                                                     const int *__restrict__ rexp, int M) {
+    __shared__ uint4 lds_w[2][3][kWdNR * 4];  // 144 KiB (the fp16x2 body uses two of the three planes)
+    const int m0 = xcd_remap_x3(blockIdx.x, gridDim.x) * 128;
+    if (*p0.wbad | *p1.wbad)
+        dgrad_wide_body<3, 8, J1>(p0, p1, nullptr, M, m0, lds_w);
+    else
+        dgrad_wide_body<2, 8, J1>(p0, p1, rexp, M, m0, lds_w);
+}
+
 // planes[q][r][c] = part q of 2^kDgW W[r][(c + rot) % cols] (fp16x2, q = 0, 1); *bad = 1 if a scaled
 // weight is outside (-2^15, 2^15) or not finite (msat_gemm_h2 then runs its bf16x3 body)
 __global__ void split_f16x2_rot_kernel(const float *__restrict__ W, int rows, int cols, int ldw, int rot,
@@ -1508,6 +1699,18 @@ extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h
         return check_launch("gemm_h2_dual_resident_kernel");
     }
     const int ntm = (M + 127) / 128;
+    // the full-width form: a GRU cell's shapes (N0 = 128, N1 = 128 / 256, K = 384), float4 rows out
+    const char *wide = getenv("MARLSAT_DGRAD_WIDE");  // ablation: 0 = the per-tile kernel
+    if (!(wide && wide[0] == '0') && K == 384 && N0 == 128 && (N1 == 128 || N1 == 256) && p[0].vec_out &&
+        p[1].vec_out) {
+        if (N1 == 256)
+            hipLaunchKernelGGL(gemm_h2_dual_wide_kernel<16>, dim3(ntm), dim3(kWdT), 0, (hipStream_t)stream, p[0], p[1],
+                               rexp, M);
+        else
+            hipLaunchKernelGGL(gemm_h2_dual_wide_kernel<8>, dim3(ntm), dim3(kWdT), 0, (hipStream_t)stream, p[0], p[1],
+                               rexp, M);
+        return check_launch("gemm_h2_dual_wide_kernel");
+    }
     hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(kX3T), 0,
                        (hipStream_t)stream, p[0], p[1], rexp, M, K);
     return check_launch("gemm_h2r16_dual_kernel");

@@ -20,6 +20,9 @@ int msat_probe_obs_expand(void *dst, int32_t E, int32_t A, int32_t D, const int3
  * (amajor = 0) or agent-major [A][E][D] (amajor = 1); threads 256 or 512. */
 int msat_probe_fill_rows(void *dst, int32_t E, int32_t A, int32_t D16, int32_t amajor, int32_t value, int32_t threads,
                          int32_t grid, void *stream);
+/* Read M x K floats of D (leading dimension ld) as the data gradient's register-A column strips (mode 0),
+ * as contiguous rows (1), or as strips with three workgroups per row block (2); out: one float per thread. */
+int msat_probe_strip_read(const float *D, int32_t M, int32_t ld, int32_t K, int32_t mode, float *out, void *stream);
 #ifdef __cplusplus
 }
 #endif

@@ -93,7 +93,58 @@ __global__ void __launch_bounds__(NT) fill_rows_kernel(int4 *__restrict__ dst, i
             for (int i = threadIdx.x; i < D16; i += NT) *reinterpret_cast<v4i *>(dst + row * D16 + i) = v;
         }
 }
+
+// Read-pattern probe for the data gradient's activation stream: the same bytes (M rows x K floats of a
+// row-major buffer with leading dimension ld) read (0) as register-A column strips -- per 128-row workgroup
+// and 32-column step, lane (l16, g) loads two float4 of row l16 + 16 i, columns 32 d + 8 g .. + 7, i < 2 --
+// (1) as contiguous rows (each wave-instruction 1 KiB of one row), (2) as (0) with three workgroups per
+// row block (the per-tile kernel's three column tiles re-reading from L2).
+template <int MODE>
+__global__ void __launch_bounds__(256) strip_read_kernel(const float *__restrict__ D, int M, int ld, int K,
+                                                         float *__restrict__ out) {
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63, l16 = lane & 15, g = lane >> 4;
+    const int blk = MODE == 2 ? blockIdx.x / 3 : blockIdx.x;
+    const int m0 = blk * 128 + w * 32;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (MODE == 1) {
+        for (int r = 0; r < 32; ++r) {
+            const float *row = D + (size_t)min(m0 + r, M - 1) * ld;
+            for (int c = 4 * lane; c < K; c += 256) {
+                const float4 v = *reinterpret_cast<const float4 *>(row + c);
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+        }
+    } else {
+        const float *a0 = D + (size_t)min(m0 + l16, M - 1) * ld + 8 * g;
+        const float *a1 = D + (size_t)min(m0 + 16 + l16, M - 1) * ld + 8 * g;
+        for (int d = 0; d < K / 32; ++d) {
+            const float4 u0 = *reinterpret_cast<const float4 *>(a0 + 32 * d);
+            const float4 u1 = *reinterpret_cast<const float4 *>(a0 + 32 * d + 4);
+            const float4 v0 = *reinterpret_cast<const float4 *>(a1 + 32 * d);
+            const float4 v1 = *reinterpret_cast<const float4 *>(a1 + 32 * d + 4);
+            s.x += u0.x + u1.x + v0.x + v1.x; s.y += u0.y + u1.y + v0.y + v1.y;
+            s.z += u0.z + u1.z + v0.z + v1.z; s.w += u0.w + u1.w + v0.w + v1.w;
+        }
+    }
+    out[(size_t)blockIdx.x * 256 + t] = s.x + s.y + s.z + s.w;
+}
 }  // namespace msat
+
+extern "C" int msat_probe_strip_read(const float *D, int32_t M, int32_t ld, int32_t K, int32_t mode, float *out,
+                                     void *stream) {
+    MSAT_REQUIRE(D && out && M > 0 && K % 32 == 0 && ld >= K && ld % 4 == 0 && mode >= 0 && mode <= 2,
+                 "bad strip_read args");
+    const int nb = (M + 127) / 128;
+    if (mode == 0)
+        hipLaunchKernelGGL(msat::strip_read_kernel<0>, dim3(nb), dim3(256), 0, (hipStream_t)stream, D, M, ld, K, out);
+    else if (mode == 1)
+        hipLaunchKernelGGL(msat::strip_read_kernel<1>, dim3(nb), dim3(256), 0, (hipStream_t)stream, D, M, ld, K, out);
+    else
+        hipLaunchKernelGGL(msat::strip_read_kernel<2>, dim3(3 * nb), dim3(256), 0, (hipStream_t)stream, D, M, ld, K,
+                           out);
+    return msat::check_launch("strip_read_kernel");
+}
+
 
 extern "C" int msat_probe_obs_expand(void *dst, int32_t E, int32_t A, int32_t D, const int32_t *inst,
                                      const uint32_t *vimg, const uint32_t *mimg, int32_t grid, void *stream) {

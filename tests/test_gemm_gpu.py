@@ -372,12 +372,14 @@ def test_dual_launches_match_fp64(M, K1):
 
 @pytest.mark.parametrize("M,K1,wbig", [(1, 128, 0), (255, 256, 0), (257, 128, 0), (70001, 256, 0), (131071, 128, 0),
                                        (4999, 256, 1)])
-def test_dual_resident_matches_per_tile(M, K1, wbig, monkeypatch):
-    """msat_gemm_h2_dual's resident-weight kernel (MARLSAT_DGRAD_RESIDENT=1, gemm_h2_dual_resident_kernel: 64-column
-    weight tiles kept in LDS, 256-row blocks walked per workgroup) against the per-tile kernel (default): the same
-    split, MFMA sequence, k order and rescale per output element, so both outputs agree exactly -- ragged last
-    blocks, both GRU cell shapes (K1 = 128 / 256), dh accumulated onto its old value, and a weight past the
-    fp16x2 range (wbig: the bf16x3 planes, NP = 3 image)."""
+@pytest.mark.parametrize("form", ["MARLSAT_DGRAD_RESIDENT=1", "MARLSAT_DGRAD_WIDE=1"])
+def test_dual_forms_match_per_tile(M, K1, wbig, form, monkeypatch):
+    """msat_gemm_h2_dual's full-width kernel (gemm_h2_dual_wide_kernel, the default for a GRU cell's shapes) and
+    its resident-weight kernel (MARLSAT_DGRAD_RESIDENT=1: 64-column weight tiles kept in LDS, 256-row blocks per
+    workgroup) against the per-tile kernel (MARLSAT_DGRAD_WIDE=0): the same split, MFMA sequence, k order and
+    rescale per output element, so the outputs agree exactly -- ragged last blocks, both GRU cell shapes
+    (K1 = 128 / 256), dh accumulated onto its old value, and a weight past the fp16x2 range (wbig: the bf16x3
+    planes; the full-width kernel then runs both products on them, so its dh is checked against fp64 there)."""
     from marlsat import _lib
 
     H = 128
@@ -404,11 +406,12 @@ def test_dual_resident_matches_per_tile(M, K1, wbig, monkeypatch):
     assert int(planes[1][2]) == wbig
     C0 = torch.randn(M, H, device="cuda", generator=g)
     outs = {}
-    for mode in (None, "1"):
-        if mode is None:
-            monkeypatch.delenv("MARLSAT_DGRAD_RESIDENT", raising=False)
-        else:
-            monkeypatch.setenv("MARLSAT_DGRAD_RESIDENT", mode)
+    var, val = form.split("=")
+    for mode in ("base", "form"):
+        monkeypatch.delenv("MARLSAT_DGRAD_RESIDENT", raising=False)
+        monkeypatch.setenv("MARLSAT_DGRAD_WIDE", "0")
+        if mode == "form":
+            monkeypatch.setenv(var, val)
         dh = C0.clone()
         dx = torch.full((M, K1), float("nan"), device="cuda")
         _lib.check(_lib.lib.msat_gemm_h2_dual(
@@ -417,8 +420,13 @@ def test_dual_resident_matches_per_tile(M, K1, wbig, monkeypatch):
             planes[1][2].data_ptr(), dx.data_ptr(), K1, K1, 0, rexp.data_ptr(), M, 3 * H, s), "dual dgrad")
         torch.cuda.synchronize()
         outs[mode] = (dh, dx)
-    assert torch.equal(outs["1"][0], outs[None][0])
-    assert torch.equal(outs["1"][1], outs[None][1])
+    assert torch.equal(outs["form"][1], outs["base"][1])
+    if wbig and "WIDE" in form:
+        dgh = D[:, H:]
+        _ref_close(outs["form"][0], dgh.double() @ Wh.double().t() + C0.double(),
+                   dgh.double().abs() @ Wh.double().abs().t() + C0.double().abs())
+    else:
+        assert torch.equal(outs["form"][0], outs["base"][0])
     Fr = torch.roll(F.double(), -2 * H, dims=1)
     dgi = D[:, :3 * H]
-    _ref_close(outs[None][1], dgi.double() @ Fr.t(), dgi.double().abs() @ Fr.abs().t())
+    _ref_close(outs["form"][1], dgi.double() @ Fr.t(), dgi.double().abs() @ Fr.abs().t())
