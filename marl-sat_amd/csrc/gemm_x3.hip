@@ -17,7 +17,6 @@
 // are too short to cover an HBM load issued one slab ahead).
 
 #include <algorithm>
-#include <stdlib.h>
 
 #include "common.h"
 #include "split3.h"
@@ -656,411 +655,6 @@ gemm_h2r16_dual_kernel(DgradProblem p0, DgradProblem p1, const int *__restrict__
                              lds_w, p.kr);
 }
 
-// Resident-weight form of the dual data gradient (msat_gemm_h2_dual when K = 384, a GRU cell's 3H at
-// H = 128, and both N are multiples of 64).  The per-tile kernel above re-stages its 128 x K weight tile through LDS for every
-// 128-row block: four weight DMA pieces and a barrier per wave and k step beside 48 MFMAs, and the
-// stamps put 39 % of its wave cycles in issuing those memory operations.  Here one
-// 512-thread workgroup per CU keeps ONE 64-column tile of one product's weight planes in LDS for the
-// whole launch (NP x 64 x K halves: 96 KiB fp16x2, 144 KiB bf16x3 at K = 384) and walks 512-row blocks
-// (8 waves x 64 rows, register-A as above).  The k loop has no barrier and no DMA: per wave and step,
-// eight activation loads (prefetched PF steps ahead, across block boundaries), eight ds_read_b128 of the
-// resident image and 48 MFMAs.  The T = N0 / 64 + N1 / 64 tiles of a row block form a group; a group's
-// workgroups sit on one XCD (blockIdx % 8) and walk the same blocks in the same order, with the second
-// product's walk started kr slabs in as above, so the packed rows come from HBM once and from L2 for
-// the other T - 1 tiles.  The arithmetic per output element (split, MFMA sequence, k order, rescale,
-// accumulate) is the per-tile kernel's: the two forms agree bitwise (tests/test_gemm_gpu.py).
-constexpr int kRsT = 512, kRsRT = 2, kRsRows = 8 * 16 * kRsRT, kRsMaxD = 12;
-constexpr int kRsImg = 3 * kRsMaxD * 4 * 64;  // uint4s of the largest weight image (bf16x3, K = 384)
-
-struct DgradResident {
-    DgradProblem p[2];
-    int T0, T;   // 64-column tiles of product 0, of both
-    int gx, ng;  // groups of T workgroups per XCD in the XCD-aligned part; groups in all
-    int nrb;     // 512-row blocks
-};
-
-template <int NP, int PF, int ND>
-__device__ __forceinline__ void dgrad_resident_body(const DgradProblem &p, const int *__restrict__ rexp, int M,
-                                                    int n0, int grp, int ng, int nb, uint4 *lds) {
-    typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
-    constexpr int RT = kRsRT, nd = ND, K = 32 * ND;
-    static_assert(ND <= kRsMaxD && ND % PF == 0, "resident image / prefetch ring");
-    const int t = threadIdx.x, w = t >> 6, lane = t & 63, l16 = lane & 15, g = lane >> 4;
-    // the weight tile, once: image [q][d][j][lane] = 16 B of plane q, column n0 + 16 j + (lane & 15),
-    // k 32 d + 8 (lane >> 4) .. + 7 -- each ds_read_b128 below reads 1 KiB contiguous (no conflicts)
-    {
-        const uint16_t *Wp = NP == 2 ? p.Wh2 : p.Wx3;
-        constexpr int per = nd * 256;
-        static_assert((NP * per) % kRsT == 0, "whole fill rounds");
-#pragma unroll
-        for (int u = 0; u < NP * per / kRsT; ++u) {  // unrolled: the loads go out together
-            const int c = t + kRsT * u;
-            const int q = c / per, rem = c - q * per, d = rem >> 8, j = (rem >> 6) & 3, ln = rem & 63;
-            const int n = n0 + 16 * j + (ln & 15), k = 32 * d + 8 * (ln >> 4);
-            MSAT_DCHECK(((size_t)q * p.N + n) * K + k + 8, (size_t)NP * p.N * K + 1);
-            lds[c] = *reinterpret_cast<const uint4 *>(Wp + ((size_t)q * p.N + n) * K + k);
-        }
-    }
-    __syncthreads();
-    const int kr = p.kr;
-    auto sl = [&](int d) { const int x = d + kr; return x >= nd ? x - nd : x; };
-    auto rowof = [&](int b, int i) { return (grp + b * ng) * kRsRows + w * 16 * RT + 16 * i; };
-    auto loadA = [&](int b, int d, float4 (&ra)[RT][2]) {
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-            const int r = min(rowof(b, i) + l16, M - 1);
-            const float *a = p.A + (size_t)r * p.lda + 8 * g + 32 * d;
-            ra[i][0] = *reinterpret_cast<const float4 *>(a);
-            ra[i][1] = *reinterpret_cast<const float4 *>(a + 4);
-        }
-    };
-    auto expof = [&](int b, int (&ea)[RT]) {
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-            const int e = rexp[min(rowof(b, i) + l16, M - 1)];
-            ea[i] = e == kExpZero ? 0 : e;
-        }
-    };
-    float4 ras[PF][RT][2];
-#pragma unroll
-    for (int x = 0; x < PF; ++x) loadA(0, sl(x), ras[x]);
-    int ea[RT] = {};
-    if constexpr (NP == 2) expof(0, ea);
-    float *stage = reinterpret_cast<float *>(lds + kRsImg) + w * 256;  // 16 x 16 fp32 per wave (writes 2-way)
-    for (int b = 0; b < nb; ++b) {
-        // the next block's row exponents and this block's old C (accumulate), issued now: both land under the
-        // block's k walk (unconditional loads of clamped rows keep hipcc's vmcnt bookkeeping exact)
-        int ean[RT];
-        if constexpr (NP == 2) expof(min(b + 1, nb - 1), ean);
-        const int r0 = rowof(b, 0);
-        float4 old[RT][4];
-        if (p.accumulate) {
-#pragma unroll
-            for (int i = 0; i < RT; ++i) {
-                const float *oc = p.C + (size_t)min(r0 + 16 * i + (lane >> 2), M - 1) * p.ldc + n0 + 4 * (lane & 3);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) old[i][j] = *reinterpret_cast<const float4 *>(oc + 16 * j);
-            }
-        }
-        f32x4 acc[RT][4];
-#pragma unroll
-        for (int i = 0; i < RT; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
-        auto step = [&](int dd, float4 (&ra)[RT][2]) {
-            const int d = sl(dd);
-            uint4 fa[RT][NP];
-#pragma unroll
-            for (int i = 0; i < RT; ++i) {
-                if constexpr (NP == 3) {
-                    const Split8 sp = split8(ra[i][0], ra[i][1]);
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) fa[i][q] = sp.p[q];
-                } else {
-                    const float4 u = ra[i][0], v = ra[i][1];
-                    const int e = ea[i];
-                    const SplitH4 s0 = splith4(make_float4(ldexpf(u.x, e), ldexpf(u.y, e), ldexpf(u.z, e), ldexpf(u.w, e)));
-                    const SplitH4 s1 = splith4(make_float4(ldexpf(v.x, e), ldexpf(v.y, e), ldexpf(v.z, e), ldexpf(v.w, e)));
-                    fa[i][0] = make_uint4(s0.p[0].x, s0.p[0].y, s1.p[0].x, s1.p[0].y);
-                    fa[i][1] = make_uint4(s0.p[1].x, s0.p[1].y, s1.p[1].x, s1.p[1].y);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);  // keep each step's split, loads and MFMAs in their place
-            // this set was just split: refill it PF steps ahead (into the next block past the last step;
-            // the last block re-reads its own rows there, so every step issues the same loads and hipcc's
-            // vmcnt bookkeeping stays exact across the loop)
-            {
-                const bool in = dd + PF < nd;
-                loadA(in ? b : min(b + 1, nb - 1), sl(in ? dd + PF : dd + PF - nd), ra);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                uint4 fb[NP];
-#pragma unroll
-                for (int q = 0; q < NP; ++q) fb[q] = lds[((q * nd + d) * 4 + j) * 64 + lane];
-#pragma unroll
-                for (int i = 0; i < RT; ++i) {
-                    f32x4 c = acc[i][j];
-                    if constexpr (NP == 3) {
-                        auto m = [](const uint4 &a, const uint4 &bb, const f32x4 &c) {
-                            return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                                           __builtin_bit_cast(bf16x8, bb), c, 0, 0, 0);
-                        };
-                        c = m(fa[i][2], fb[0], c);
-                        c = m(fa[i][1], fb[1], c);
-                        c = m(fa[i][0], fb[2], c);
-                        c = m(fa[i][1], fb[0], c);
-                        c = m(fa[i][0], fb[1], c);
-                        c = m(fa[i][0], fb[0], c);
-                    } else {
-                        auto m = [](const uint4 &a, const uint4 &bb, const f32x4 &c) {
-                            return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8v, a),
-                                                                          __builtin_bit_cast(f16x8v, bb), c, 0, 0, 0);
-                        };
-                        c = m(fa[i][0], fb[1], c);  // h l
-                        c = m(fa[i][1], fb[0], c);  // l h
-                        c = m(fa[i][0], fb[0], c);  // h h
-                    }
-                    acc[i][j] = c;
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        };
-#pragma unroll
-        for (int dd = 0; dd < nd; dd += PF) {
-#pragma unroll
-            for (int x = 0; x < PF; ++x) step(dd + x, ras[x]);
-        }
-        // epilogue: rescale rows by 2^-(e + kDgW) (the C/D map: lane (l16, g) holds rows 4 g + reg, column
-        // l16), then per 16 x 16 block through the wave's stage to float4 rows (+ the old C), stored
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-            if constexpr (NP == 2) {
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) {
-                    const int sh = -(__shfl(ea[i], 4 * g + reg, 16) + kDgW);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j][reg] = ldexpf(acc[i][j][reg], sh);
-                }
-            }
-            const int row = r0 + 16 * i + (lane >> 2);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) stage[(4 * g + reg) * 16 + l16] = acc[i][j][reg];
-                asm volatile("" ::: "memory");  // the wave's own LDS ops run in order; keep hipcc's order too
-                float4 v = *reinterpret_cast<const float4 *>(stage + (lane >> 2) * 16 + 4 * (lane & 3));
-                asm volatile("" ::: "memory");
-                if (p.accumulate) {
-                    const float4 &ov = old[i][j];
-                    v.x = ov.x + v.x; v.y = ov.y + v.y; v.z = ov.z + v.z; v.w = ov.w + v.w;
-                }
-                if (row < M) *reinterpret_cast<float4 *>(p.C + (size_t)row * p.ldc + n0 + 16 * j + 4 * (lane & 3)) = v;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < RT; ++i) ea[i] = ean[i];
-    }
-}
-
-template <int PF>
-__global__ void __launch_bounds__(kRsT, 1) gemm_h2_dual_resident_kernel(DgradResident a, const int *__restrict__ rexp,
-                                                                         int M) {
-    __shared__ uint4 lds[kRsImg + 8 * 64];  // weight image + eight 1 KiB wave stages: 152 KiB
-    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
-    int grp, tile;
-    if (local < a.gx * a.T) {
-        grp = (local / a.T) * 8 + xcd;
-        tile = local % a.T;
-    } else {  // the CUs an XCD has left over: groups spread over XCDs
-        const int e = (local - a.gx * a.T) * 8 + xcd;
-        grp = 8 * a.gx + e / a.T;
-        tile = e % a.T;
-        if (grp >= a.ng) return;
-    }
-    const int nb = grp < a.nrb ? (a.nrb - grp + a.ng - 1) / a.ng : 0;
-    if (nb == 0) return;
-    const bool first = tile < a.T0;
-    const DgradProblem &p = first ? a.p[0] : a.p[1];
-    const int n0 = (first ? tile : tile - a.T0) * 64;
-    if (*p.wbad)
-        dgrad_resident_body<3, 2, kRsMaxD>(p, rexp, M, n0, grp, a.ng, nb, lds);
-    else
-        dgrad_resident_body<2, PF, kRsMaxD>(p, rexp, M, n0, grp, a.ng, nb, lds);
-}
-
-// Full-width form of the dual data gradient (msat_gemm_h2_dual for a GRU cell: N0 = 128, N1 = 128 / 256,
-// K = 384).  One 512-thread workgroup per 128-row block computes BOTH products over ALL N0 + N1 columns: each
-// wave holds 16 rows x 384 columns of accumulators (96 VGPRs), so every packed row is read from HBM once and
-// split once per k step for all columns, where the per-tile kernel reads and splits it once per 128-column
-// tile (three times) and leans on L2 for the re-reads.  Both products' weight slabs stream through LDS per
-// 32-deep step (48 KiB, double-buffered: 96 KiB fp16x2, 144 KiB bf16x3), LDS-DMA as above: per wave and
-// step 6 DMA pieces, 2 activation loads per operand, 48 ds_read_b128 and 72 MFMAs against the per-tile
-// kernel's 4 + 4 + 16 per 48 MFMAs.  The second product's k walk starts kr slabs in (host, as above), so for
-// kr = H / 32 the two products read the same packed columns for the first 3H - H of K: one split serves
-// both.  Per output element the arithmetic is the per-tile kernel's (split, MFMA order, k order, rescale,
-// accumulate): the two forms agree bitwise (tests/test_gemm_gpu.py).
-constexpr int kWdT = 512, kWdNR = 384;  // threads (8 waves x 16 rows); image rows per plane (N0 + N1 max)
-
-template <int NP, int J0, int J1>
-__device__ __forceinline__ void dgrad_wide_body(const DgradProblem &p0, const DgradProblem &p1,
-                                                const int *__restrict__ rexp, int M, int m0,
-                                                uint4 (*lds_w)[3][kWdNR * 4]) {
-    typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
-    constexpr int nd = 12, K = 32 * nd, NR = 16 * (J0 + J1), PPW = NP * NR / 128;
-    static_assert(NR <= kWdNR && (NP * NR) % 128 == 0, "image rows / DMA pieces per wave");
-    const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, g = lane >> 4;
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: the DMA bases stay in SGPRs
-    const int row = min(m0 + 16 * w + l16, M - 1);  // this lane's activation row (register-A)
-    int ea = 0;
-    if constexpr (NP == 2) {
-        const int e = rexp[row];
-        ea = e == kExpZero ? 0 : e;
-    }
-    // weight DMA: piece x -> plane q, image rows 16 pp .. + 15 (product 0 below 16 J0, product 1 above)
-    unsigned voff[PPW];
-    const uint16_t *pbase[PPW];
-#pragma unroll
-    for (int e = 0; e < PPW; ++e) {
-        const int x = PPW * w + e, q = x / (NR / 16), pp = x % (NR / 16);
-        const int r = 16 * pp + (lane >> 2), ch = (lane & 3) ^ x3swz16((r >> 2) & 3);
-        const bool second = pp >= J0;
-        const int n = second ? r - 16 * J0 : r, N = second ? 16 * J1 : 16 * J0;
-        const uint16_t *W = NP == 2 ? (second ? p1.Wh2 : p0.Wh2) : (second ? p1.Wx3 : p0.Wx3);
-        pbase[e] = W;
-        voff[e] = (unsigned)(((size_t)q * N * K + (size_t)n * K + 8 * ch) * 2);
-    }
-    const int kr0 = p0.kr, kr1 = p1.kr;
-    auto sl0 = [&](int d) { const int x = d + kr0; return x >= nd ? x - nd : x; };
-    auto sl1 = [&](int d) { const int x = d + kr1; return x >= nd ? x - nd : x; };
-    auto issueW = [&](int d, int buf) {
-#pragma unroll
-        for (int e = 0; e < PPW; ++e) {
-            const int x = PPW * w + e, q = x / (NR / 16), pp = x % (NR / 16);
-            const int sl = pp >= J0 ? sl1(d) : sl0(d);
-            glds16_async_s(reinterpret_cast<const char *>(pbase[e]) + (size_t)sl * 64, voff[e], &lds_w[buf][q][64 * pp]);
-        }
-    };
-    const float *a0 = p0.A + (size_t)row * p0.lda + 8 * g, *a1 = p1.A + (size_t)row * p1.lda + 8 * g;
-    float4 ra[2][2][2];  // [prefetch set][product][half]
-    auto loadA = [&](int d, float4 (&r)[2][2]) {
-        const float *x0 = a0 + 32 * sl0(d), *x1 = a1 + 32 * sl1(d);
-        r[0][0] = *reinterpret_cast<const float4 *>(x0);
-        r[0][1] = *reinterpret_cast<const float4 *>(x0 + 4);
-        r[1][0] = *reinterpret_cast<const float4 *>(x1);  // the same columns when the walks align: an L1 hit
-        r[1][1] = *reinterpret_cast<const float4 *>(x1 + 4);
-    };
-    f32x4 acc[J0 + J1];
-#pragma unroll
-    for (int j = 0; j < J0 + J1; ++j) acc[j] = f32x4{};
-    loadA(0, ra[0]);
-    loadA(1, ra[1]);
-    issueW(0, 0);
-    wait_vmcnt<0>();
-    barrier_lds();
-    const int slot = g ^ x3swz16((l16 >> 2) & 3);
-    auto split = [&](const float4 (&r)[2], uint4 (&fa)[NP]) {
-        if constexpr (NP == 3) {
-            const Split8 sp = split8(r[0], r[1]);
-#pragma unroll
-            for (int q = 0; q < 3; ++q) fa[q] = sp.p[q];
-        } else {
-            const float4 u = r[0], v = r[1];
-            const SplitH4 s0 = splith4(make_float4(ldexpf(u.x, ea), ldexpf(u.y, ea), ldexpf(u.z, ea), ldexpf(u.w, ea)));
-            const SplitH4 s1 = splith4(make_float4(ldexpf(v.x, ea), ldexpf(v.y, ea), ldexpf(v.z, ea), ldexpf(v.w, ea)));
-            fa[0] = make_uint4(s0.p[0].x, s0.p[0].y, s1.p[0].x, s1.p[0].y);
-            fa[1] = make_uint4(s0.p[1].x, s0.p[1].y, s1.p[1].x, s1.p[1].y);
-        }
-    };
-    auto mm = [&](const uint4 (&fa)[NP], const uint4 (&fb)[NP], f32x4 c) {
-        if constexpr (NP == 3) {
-            auto m = [](const uint4 &a, const uint4 &b, const f32x4 &c) {
-                return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
-                                                               c, 0, 0, 0);
-            };
-            c = m(fa[2], fb[0], c);
-            c = m(fa[1], fb[1], c);
-            c = m(fa[0], fb[2], c);
-            c = m(fa[1], fb[0], c);
-            c = m(fa[0], fb[1], c);
-            c = m(fa[0], fb[0], c);
-        } else {
-            auto m = [](const uint4 &a, const uint4 &b, const f32x4 &c) {
-                return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8v, a), __builtin_bit_cast(f16x8v, b),
-                                                              c, 0, 0, 0);
-            };
-            c = m(fa[0], fb[1], c);  // h l
-            c = m(fa[1], fb[0], c);  // l h
-            c = m(fa[0], fb[0], c);  // h h
-        }
-        return c;
-    };
-    const bool samek = p0.lda == p1.lda;
-#pragma unroll
-    for (int d = 0; d < nd; ++d) {
-        const int buf = d & 1;
-        float4 (&r)[2][2] = ra[d & 1];
-        uint4 fa0[NP], fa1[NP];
-        split(r[0], fa0);
-        // a use of the second operand's registers on every path: hipcc then waits for them here, with the
-        // first operand's (same age), instead of before refilling them below (which would also drain the DMA)
-        asm volatile("" ::"v"(r[1][0].x), "v"(r[1][0].y), "v"(r[1][0].z), "v"(r[1][0].w), "v"(r[1][1].x),
-                     "v"(r[1][1].y), "v"(r[1][1].z), "v"(r[1][1].w));
-        // one split for both products where their walks read the same packed columns (uniform)
-        if (samek && p0.A + 32 * sl0(d) == p1.A + 32 * sl1(d)) {
-#pragma unroll
-            for (int q = 0; q < NP; ++q) fa1[q] = fa0[q];
-        } else {
-            split(r[1], fa1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (d + 1 < nd) issueW(d + 1, buf ^ 1);
-        if (d + 2 < nd) loadA(d + 2, r);  // this set was just split
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < J0 + J1; ++j) {
-            uint4 fb[NP];
-#pragma unroll
-            for (int q = 0; q < NP; ++q) fb[q] = lds_w[buf][q][(16 * j + l16) * 4 + slot];
-            acc[j] = j < J0 ? mm(fa0, fb, acc[j]) : mm(fa1, fb, acc[j]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // W(d + 1) landed; A(d + 2), issued after it, may fly
-        if (d + 2 < nd) wait_vmcnt<4>();
-        else wait_vmcnt<0>();
-        barrier_lds();
-    }
-    // epilogue: rescale rows by 2^-(e + kDgW) (C/D map: lane (l16, g) holds rows 4 g + reg, column l16), old
-    // dh rows loaded first, the product-1 columns written while they land, then product 0's; each 16 x 16
-    // block goes through the wave's 1 KiB stage (the weight buffers are free after the last barrier) to
-    // float4 row pieces
-    if constexpr (NP == 2) {
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const int sh = -(__shfl(ea, 4 * g + reg, 16) + kDgW);
-#pragma unroll
-            for (int j = 0; j < J0 + J1; ++j) acc[j][reg] = ldexpf(acc[j][reg], sh);
-        }
-    }
-    const int orow = m0 + 16 * w + (lane >> 2), oc4 = 4 * (lane & 3);
-    const int crow = min(orow, M - 1);
-    float4 old0[J0];
-    if (p0.accumulate) {
-#pragma unroll
-        for (int j = 0; j < J0; ++j)
-            old0[j] = *reinterpret_cast<const float4 *>(p0.C + (size_t)crow * p0.ldc + 16 * j + oc4);
-    }
-    float *stage = reinterpret_cast<float *>(&lds_w[0][0][0]) + w * 256;
-    auto put = [&](int j, const DgradProblem &p, int col0, const float4 *old) {
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) stage[(4 * g + reg) * 16 + l16] = acc[j][reg];
-        asm volatile("" ::: "memory");  // the wave's LDS operations run in order; keep hipcc's order too
-        float4 v = *reinterpret_cast<const float4 *>(stage + (lane >> 2) * 16 + oc4);
-        asm volatile("" ::: "memory");
-        if (p.accumulate) {
-            const float4 ov = old ? *old : *reinterpret_cast<const float4 *>(p.C + (size_t)crow * p.ldc + col0 + oc4);
-            v.x = ov.x + v.x; v.y = ov.y + v.y; v.z = ov.z + v.z; v.w = ov.w + v.w;
-        }
-        if (orow < M) *reinterpret_cast<float4 *>(p.C + (size_t)orow * p.ldc + col0 + oc4) = v;
-    };
-#pragma unroll
-    for (int j = 0; j < J1; ++j) put(J0 + j, p1, 16 * j, nullptr);
-#pragma unroll
-    for (int j = 0; j < J0; ++j) put(j, p0, 16 * j, &old0[j]);
-}
-
-template <int J1>
-__global__ void __launch_bounds__(kWdT, 1) gemm_h2_dual_wide_kernel(DgradProblem p0, DgradProblem p1,
-                                                                     const int *__restrict__ rexp, int M) {
-    __shared__ uint4 lds_w[2][3][kWdNR * 4];  // 144 KiB (the fp16x2 body uses two of the three planes)
-    const int m0 = xcd_remap_x3(blockIdx.x, gridDim.x) * 128;
-    if (*p0.wbad | *p1.wbad)
-        dgrad_wide_body<3, 8, J1>(p0, p1, nullptr, M, m0, lds_w);
-    else
-        dgrad_wide_body<2, 8, J1>(p0, p1, rexp, M, m0, lds_w);
-}
-
 // planes[q][r][c] = part q of 2^kDgW W[r][(c + rot) % cols] (fp16x2, q = 0, 1); *bad = 1 if a scaled
 // weight is outside (-2^15, 2^15) or not finite (msat_gemm_h2 then runs its bf16x3 body)
 __global__ void split_f16x2_rot_kernel(const float *__restrict__ W, int rows, int cols, int ldw, int rot,
@@ -1615,20 +1209,6 @@ extern "C" int msat_gemm_h2(const float *A, int32_t lda, const int32_t *rexp, co
     return check_launch("gemm_h2r16_kernel");
 }
 
-// compute units of the current device (the resident kernel's grid: 8 XCDs x cpx), read once
-static int dgrad_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v >= 8)
-            n = v;
-        else
-            n = 256;
-    }
-    return n;
-}
-
 // C0 (+)= A0 @ W0^T and C1 (+)= A1 @ W1^T over the same M rows (one row-exponent array), in one launch
 // (gemm_h2r16_dual_kernel).  Conditions of msat_gemm_h2 for each product; no bias.
 extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h2, const void *W0_x3,
@@ -1672,45 +1252,7 @@ extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h
         const long off = (long)(A0 - A1);
         if (lda0 == lda1 && off > 0 && off % 32 == 0 && off / 32 < K / 32) p[1].kr = (int)(off / 32);
     }
-    // the resident-weight form (opt-in, measured slower: DESIGN.md round 4): K = 384, 64-column tiles, float4
-    // rows out, T tiles no more than an XCD's CUs
-    const int cpx = dgrad_cus() / 8;
-    const char *ab = getenv("MARLSAT_DGRAD_RESIDENT");  // 1 (or the prefetch depth 2 / 3 / 4) = resident form
-    if (ab && ab[0] >= '1' && ab[0] <= '4' && K == 32 * kRsMaxD && N0 % 64 == 0 && N1 % 64 == 0 && p[0].vec_out &&
-        p[1].vec_out && N0 / 64 + N1 / 64 <= cpx) {
-        DgradResident r;
-        r.p[0] = p[0];
-        r.p[1] = p[1];
-        r.T0 = N0 / 64;
-        r.T = r.T0 + N1 / 64;
-        r.gx = cpx / r.T;
-        r.ng = 8 * r.gx + 8 * (cpx - r.gx * r.T) / r.T;
-        r.nrb = (M + kRsRows - 1) / kRsRows;
-        const int pf = ab && ab[0] >= '2' && ab[0] <= '4' ? ab[0] - '0' : 3;  // A/B: prefetch depth
-        if (pf == 2)
-            hipLaunchKernelGGL(gemm_h2_dual_resident_kernel<2>, dim3(8 * cpx), dim3(kRsT), 0, (hipStream_t)stream, r,
-                               rexp, M);
-        else if (pf == 4)
-            hipLaunchKernelGGL(gemm_h2_dual_resident_kernel<4>, dim3(8 * cpx), dim3(kRsT), 0, (hipStream_t)stream, r,
-                               rexp, M);
-        else
-            hipLaunchKernelGGL(gemm_h2_dual_resident_kernel<3>, dim3(8 * cpx), dim3(kRsT), 0, (hipStream_t)stream, r,
-                               rexp, M);
-        return check_launch("gemm_h2_dual_resident_kernel");
-    }
     const int ntm = (M + 127) / 128;
-    // the full-width form: a GRU cell's shapes (N0 = 128, N1 = 128 / 256, K = 384), float4 rows out
-    const char *wide = getenv("MARLSAT_DGRAD_WIDE");  // ablation: 0 = the per-tile kernel
-    if (!(wide && wide[0] == '0') && K == 384 && N0 == 128 && (N1 == 128 || N1 == 256) && p[0].vec_out &&
-        p[1].vec_out) {
-        if (N1 == 256)
-            hipLaunchKernelGGL(gemm_h2_dual_wide_kernel<16>, dim3(ntm), dim3(kWdT), 0, (hipStream_t)stream, p[0], p[1],
-                               rexp, M);
-        else
-            hipLaunchKernelGGL(gemm_h2_dual_wide_kernel<8>, dim3(ntm), dim3(kWdT), 0, (hipStream_t)stream, p[0], p[1],
-                               rexp, M);
-        return check_launch("gemm_h2_dual_wide_kernel");
-    }
     hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(kX3T), 0,
                        (hipStream_t)stream, p[0], p[1], rexp, M, K);
     return check_launch("gemm_h2r16_dual_kernel");

@@ -368,65 +368,3 @@ def test_dual_launches_match_fp64(M, K1):
                hx.double().abs().t() @ dgh.double().abs() + W0.double().abs(), rtol=4e-6)
     _ref_close(gW1, torch.roll(xx.double().t() @ dgi.double(), 2 * H, dims=1) + W1.double(),
                torch.roll(xx.double().abs().t() @ dgi.double().abs(), 2 * H, dims=1) + W1.double().abs(), rtol=4e-6)
-
-
-@pytest.mark.parametrize("M,K1,wbig", [(1, 128, 0), (255, 256, 0), (257, 128, 0), (70001, 256, 0), (131071, 128, 0),
-                                       (4999, 256, 1)])
-@pytest.mark.parametrize("form", ["MARLSAT_DGRAD_RESIDENT=1", "MARLSAT_DGRAD_WIDE=1"])
-def test_dual_forms_match_per_tile(M, K1, wbig, form, monkeypatch):
-    """msat_gemm_h2_dual's full-width kernel (gemm_h2_dual_wide_kernel, the default for a GRU cell's shapes) and
-    its resident-weight kernel (MARLSAT_DGRAD_RESIDENT=1: 64-column weight tiles kept in LDS, 256-row blocks per
-    workgroup) against the per-tile kernel (MARLSAT_DGRAD_WIDE=0): the same split, MFMA sequence, k order and
-    rescale per output element, so the outputs agree exactly -- ragged last blocks, both GRU cell shapes
-    (K1 = 128 / 256), dh accumulated onto its old value, and a weight past the fp16x2 range (wbig: the bf16x3
-    planes; the full-width kernel then runs both products on them, so its dh is checked against fp64 there)."""
-    from marlsat import _lib
-
-    H = 128
-    g = torch.Generator(device="cuda").manual_seed(M + K1 + wbig)
-    D = torch.randn(M, 4 * H, device="cuda", generator=g)
-    D *= torch.pow(10.0, torch.empty(M, 1, device="cuda").uniform_(-12, 1, generator=g))
-    D[::7] = 0
-    rexp = row_exp(D)
-    Wh = torch.randn(H, 3 * H, device="cuda", generator=g) * 0.1
-    F = torch.randn(K1, 3 * H, device="cuda", generator=g) * 0.1
-    if wbig:
-        F[5, 9] = 70.0
-    s = _lib.stream_ptr()
-    planes = []
-    for Wm in (Wh, F):
-        n, k = Wm.shape
-        p2 = torch.empty(2 * n * k + 8, dtype=torch.int16, device="cuda")
-        p3 = torch.empty(3 * n * k + 8, dtype=torch.int16, device="cuda")
-        bad = torch.empty(1, dtype=torch.int32, device="cuda")
-        rot = 0 if Wm is Wh else 2 * H
-        _lib.check(_lib.lib.msat_split_f16x2_rot(Wm.data_ptr(), n, k, k, rot, p2.data_ptr(), bad.data_ptr(), s), "s2")
-        _lib.check(_lib.lib.msat_split_bf16x3_rot(Wm.data_ptr(), n, k, k, rot, p3.data_ptr(), s), "s3")
-        planes.append((p2, p3, bad))
-    assert int(planes[1][2]) == wbig
-    C0 = torch.randn(M, H, device="cuda", generator=g)
-    outs = {}
-    var, val = form.split("=")
-    for mode in ("base", "form"):
-        monkeypatch.delenv("MARLSAT_DGRAD_RESIDENT", raising=False)
-        monkeypatch.setenv("MARLSAT_DGRAD_WIDE", "0")
-        if mode == "form":
-            monkeypatch.setenv(var, val)
-        dh = C0.clone()
-        dx = torch.full((M, K1), float("nan"), device="cuda")
-        _lib.check(_lib.lib.msat_gemm_h2_dual(
-            D.data_ptr() + 4 * H, 4 * H, planes[0][0].data_ptr(), planes[0][1].data_ptr(), planes[0][2].data_ptr(),
-            dh.data_ptr(), H, H, 1, D.data_ptr(), 4 * H, planes[1][0].data_ptr(), planes[1][1].data_ptr(),
-            planes[1][2].data_ptr(), dx.data_ptr(), K1, K1, 0, rexp.data_ptr(), M, 3 * H, s), "dual dgrad")
-        torch.cuda.synchronize()
-        outs[mode] = (dh, dx)
-    assert torch.equal(outs["form"][1], outs["base"][1])
-    if wbig and "WIDE" in form:
-        dgh = D[:, H:]
-        _ref_close(outs["form"][0], dgh.double() @ Wh.double().t() + C0.double(),
-                   dgh.double().abs() @ Wh.double().abs().t() + C0.double().abs())
-    else:
-        assert torch.equal(outs["form"][0], outs["base"][0])
-    Fr = torch.roll(F.double(), -2 * H, dims=1)
-    dgi = D[:, :3 * H]
-    _ref_close(outs["form"][1], dgi.double() @ Fr.t(), dgi.double().abs() @ Fr.abs().t())
