@@ -164,9 +164,12 @@ def load_pmc_traffic(workload: str):
 
 
 def load_gru_pmc_ratio():
-    """PMC HBM bytes / algorithmic bytes of the GRU forward (profiles/r03k_pmc_gru.json: FETCH_SIZE x 2 +
+    """PMC HBM bytes / algorithmic bytes of the GRU forward (the newest profiles/*pmc_gru.json: FETCH_SIZE x 2 +
     WRITE_SIZE per launch on the clause and var training shapes, profiles/pmc_gru_traffic.sh)."""
-    f = os.path.join(ROOT, "profiles", "r03k_pmc_gru.json")
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gru.json")))
+    if not files:
+        return None, None
+    f = files[-1]
     try:
         d = json.load(open(f))
         r = [v["pmc_over_algorithmic"] for v in d.values()]
