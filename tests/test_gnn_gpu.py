@@ -3,7 +3,9 @@ torch-CPU oracle of the reference network (oracle/net.py), float64 on the same
 fp32 parameters.  Tolerances: forward outputs 1e-5 normwise (|err| <= 1e-5 * max|ref| per
 tensor: the phi-folded encoder re-associates fp32 products, so near-zero elements carry
 ~1e-6 absolute error in either association); gradients 1e-4 relative to the gradient
-tensor's max magnitude (fp32 accumulation over L GRU steps and thousands of rows)."""
+tensor's max magnitude (fp32 accumulation over L GRU steps and thousands of rows); and on every
+element, forward and gradients, |err| <= 1e-5 |ref| + k x the error of the same oracle run in
+float32 on the CPU (k = FWD_FACTOR / GRAD_FACTOR, the depth tests' bar)."""
 import numpy as np
 import pytest
 import torch
@@ -83,12 +85,17 @@ def test_forward_backward_match_oracle(V, C, vpa, H, L, S, mode, fuse, path, mon
     _set_path(monkeypatch, path, c_precision)
     monkeypatch.setattr(GNNActorCritic, "fuse_phi", fuse)
     net, b, P, batch, av, am, A, M = _setup(V, C, vpa, H, L, S, mode)
+    args = (batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"])
+    onet.RELU_LOG = log = []
+    try:
+        ref_logits = onet.actor_logits(P, L, *args, av, am, mode)
+        ref_value = onet.critic(P, L, *args)
+    finally:
+        onet.RELU_LOG = None
     logits, value, state = net.forward(b, save=True)
-    ref_logits = onet.actor_logits(P, L, batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"], av,
-                                   am, mode)
-    ref_value = onet.critic(P, L, batch["svf"], batch["x"], batch["cf"], batch["A_pos"], batch["A_neg"])
-    _close_norm(logits.cpu().numpy(), ref_logits.detach().numpy(), 1e-5, "logits")
-    _close_norm(value.cpu().numpy(), ref_value.detach().numpy(), 1e-5, "value")
+    rl, rv = ref_logits.detach().numpy(), ref_value.detach().numpy()
+    _close_norm(logits.cpu().numpy(), rl, 1e-5, "logits")
+    _close_norm(value.cpu().numpy(), rv, 1e-5, "value")
     # random cotangents
     g = torch.Generator().manual_seed(3)
     wl = torch.randn(ref_logits.shape, generator=g, dtype=torch.float64)
@@ -96,7 +103,13 @@ def test_forward_backward_match_oracle(V, C, vpa, H, L, S, mode, fuse, path, mon
     wv = torch.randn(ref_value.shape, generator=g, dtype=torch.float64)
     obj = (torch.where(torch.isfinite(ref_logits), ref_logits, torch.zeros_like(ref_logits)) * wl).sum() + \
         (ref_value * wv).sum()
+    kink, _ = onet.kink_bound(obj, P, log)
     obj.backward()
+    # the elementwise bar of the depth tests as well: |err| <= 1e-5 |ref| + factor x the fp32 CPU oracle's error
+    y_l, y_v, y_g = _fp32_yardstick(P, L, args, av, am, mode, wl, wv)
+    report = []
+    _close_yard(logits.cpu().numpy(), rl, y_l, FWD_FACTOR, "logits", report)
+    _close_yard(value.cpu().numpy(), rv, y_v, FWD_FACTOR, "value", report)
     net.grads.zero_()
     net.backward(b, state, wl.float().cuda().contiguous(), wv.float().cuda().contiguous())
     got = net.to_flax(grads=True)
@@ -104,6 +117,10 @@ def test_forward_backward_match_oracle(V, C, vpa, H, L, S, mode, fuse, path, mon
         ref = p.grad.numpy() if p.grad is not None else np.zeros(p.shape)
         scale = max(np.abs(ref).max(), 1e-12)
         _close(got[name], ref, 0.0, 1e-4 * scale, f"grad {name}")
+        _close_yard(got[name], ref, y_g[name], GRAD_FACTOR, f"grad {name}", report, kink[name])
+    report.sort(key=lambda t: -t[1])
+    print(f"small {path} fuse={fuse} V={V} H={H} L={L} mode={mode}: err / fp32-oracle err, worst",
+          [(w, round(r, 2)) for w, r in report[:4]])
 
 
 DEPTH_CASES = [  # the reference's depth (MAPPO_CONFIG.yaml:23-24: H = 128, L = 16)

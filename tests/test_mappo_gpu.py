@@ -102,18 +102,25 @@ def test_train_cycle_matches_oracle_replay(mode):
             params, state = onet.adam_update(params, grads, state, lr)
     got = np.stack([metrics["epoch_value_losses"].reshape(-1), metrics["epoch_actor_losses"].reshape(-1),
                     metrics["epoch_entropies"].reshape(-1)], 1)
-    np.testing.assert_allclose(got, np.array(losses), rtol=2e-4, atol=1e-5)
+    lerr = np.abs(got - np.array(losses)) / (np.abs(np.array(losses)) + 1e-5)
+    print(f"replay mode {mode}: loss error / (|loss| + 1e-5) max {lerr.max():.3g}")
+    # measured on MI355X (profiles/r04i_parity.log): loss error <= 2.0e-5 relative, update norm <= 2.5e-4
+    np.testing.assert_allclose(got, np.array(losses), rtol=5e-5, atol=1e-5)
     # Adam divides by sqrt(v), so an element whose gradient is near fp32 noise at some step moves by a
     # noise-signed ~lr: single elements are ill-conditioned, the tensor-level update is not.  The loss
     # trajectory above already pins every intermediate parameter set; here each tensor's total update
-    # must match the oracle's to 5 % in norm and no element may move beyond the Adam step budget.
+    # must match the oracle's to 0.1 % in norm and no element may move beyond the Adam step budget.
     final = net.to_flax()
+    ratios = []
     for kk, vv in params.items():
         ref, start = vv.numpy(), p0[kk].astype(np.float64)
         upd = np.linalg.norm(ref - start)
         diff = np.linalg.norm(final[kk] - ref)
-        assert diff <= 0.05 * upd + 1e-7, (kk, diff, upd)
+        ratios.append(diff / max(upd, 1e-30))
+        assert diff <= 1e-3 * upd + 1e-7, (kk, diff, upd)
         assert np.abs(final[kk] - ref).max() <= 2.0 * lr_sum + 1e-6, kk
+    print(f"replay mode {mode}: |update - oracle update| / |oracle update| worst {max(ratios):.3g}, median "
+          f"{float(np.median(ratios)):.3g}")
     # cycle metrics (learner:661-719) from the recorded transitions + the oracle critic on the final params
     done = tr["done"].astype(bool)
     solved = tr["solved"].astype(bool) & done
