@@ -436,9 +436,10 @@ def compact_leg(full: dict, side: Optional[str]) -> dict:
                      "traffic": _sig(r["traffic"]) if r["traffic"] else None,
                      "kernel": r["kernel"].split(" ")[0], "kernel_ms": _sig(r["kernel_ms"]),
                      "mfma_frac": _sig(r["mfma"]["frac"], 3),
-                     "rank_ms": [_sig(v) for v in r["per_rank_kernel_ms"]]},
+                     # the dominant kernel's launch ms, min and max over ranks (every rank's in the side file)
+                     "rank_ms": [_sig(min(r["per_rank_kernel_ms"])), _sig(max(r["per_rank_kernel_ms"]))]},
         "params_check": {k: v for k, v in (full.get("params_check") or {}).items() if k != "checksum"},
-        "detail": side,
+        "detail": os.path.basename(side) if side else side,  # under gpurun_out/
     }
 
 
@@ -606,7 +607,7 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
 
 
 def env_side_legs(args, rank, world, dist) -> list:
-    """BASELINE configs 3 and 5 beside the headline env leg (``--env-legs``, 'workload:envs_per_gpu,...'):
+    """BASELINE configs 2, 3 and 5 beside the headline env leg (``--env-legs``, 'workload:envs_per_gpu,...'):
     the same timed loop, compact records (whole-job env-steps/s, mean launch ms, HBM fraction)."""
     out = []
     for spec in filter(None, args.env_legs.split(",")):
@@ -703,8 +704,8 @@ def main():
     ap.add_argument("--mappo-micro-gb", type=float, default=240.0, help="activation budget per PPO micro-batch")
     ap.add_argument("--mappo-cycles", type=int, default=2,
                     help="timed train cycles per MAPPO leg (after one warm-up cycle); value = 1 / their median")
-    ap.add_argument("--env-legs", default="uf100-430:4096,mixed:1024,mixed:8192",
-                    help="env side legs 'workload:envs_per_gpu,...' ('' skips): BASELINE config 3 and config 5 "
+    ap.add_argument("--env-legs", default="uf50-218:1024,uf100-430:4096,mixed:1024,mixed:8192",
+                    help="env side legs 'workload:envs_per_gpu,...' ('' skips): BASELINE configs 2 and 3 and config 5 "
                          "(1024 envs per GPU = its 8-GPU share of 8192, and all 8192 on one GPU)")
     args = ap.parse_args()
 

@@ -97,7 +97,8 @@ def test_side_legs_fit_the_driver_tail():
             "params_check": {"finite": True, "identical": True, "checksum": [123.4567890123, 1234567890123456789]}}
     leg = bench.compact_leg(full, "gpurun_out/bench_mappo_uf200-860_n8_rank0.json")
     env = [{"workload": w, "envs_per_gpu": b, "value": bench._sig(1.234567e8), "kernel_ms": bench._sig(0.0267123),
-            "frac": bench._sig(0.612345, 3)} for w, b in (("uf100-430", 4096), ("mixed", 1024), ("mixed", 8192))]
+            "frac": bench._sig(0.612345, 3)} for w, b in (("uf50-218", 1024), ("uf100-430", 4096), ("mixed", 1024),
+                                                          ("mixed", 8192))]
     tail = json.dumps({"env_other_legs": env, "mappo_other_legs": [leg], "mappo": leg})
     assert len(tail) < 1600, len(tail)
     assert leg["roofline"]["kernel"] == "gru_ln_fused_fwd_h2s_kernel" and leg["config"].endswith(" dp8")
