@@ -23,6 +23,11 @@ int msat_probe_fill_rows(void *dst, int32_t E, int32_t A, int32_t D16, int32_t a
 /* Read M x K floats of D (leading dimension ld) as the data gradient's register-A column strips (mode 0),
  * as contiguous rows (1), or as strips with three workgroups per row block (2); out: one float per thread. */
 int msat_probe_strip_read(const float *D, int32_t M, int32_t ld, int32_t K, int32_t mode, float *out, void *stream);
+/* Texture-path probe: `grid` x 256 threads read an L2-resident window of `window` bytes, `iters` wave-
+ * instructions of 1 KiB per wave, as plain loads (mode 0 lane-linear, 2 register-A pattern: 16 rows `stride`
+ * bytes apart, 64 B each) or LDS-DMA pieces (1 lane-linear, 3 weight-piece pattern: 16 rows, 64 B each). */
+int msat_probe_l2_read(const void *buf, int32_t window, int32_t mode, int32_t iters, int32_t grid, int32_t stride,
+                       float *out, void *stream);
 #ifdef __cplusplus
 }
 #endif

@@ -128,7 +128,70 @@ __global__ void __launch_bounds__(256) strip_read_kernel(const float *__restrict
     }
     out[(size_t)blockIdx.x * 256 + t] = s.x + s.y + s.z + s.w;
 }
+
+// Texture-path probe: L2-resident reads at full occupancy (three 256-thread workgroups per CU, as the data
+// gradient runs), 1 KiB per wave-instruction, in four forms -- plain loads into registers (0: lane-linear,
+// 2: the register-A pattern, 16 rows x 64 B at a 2 KiB row stride) and LDS-DMA pieces (1: lane-linear,
+// 3: the weight-piece pattern, 16 rows x 64 B at a 768 B stride) -- so the TA / TD counters of each can be
+// read against its byte rate.
+template <int MODE>
+__global__ void __launch_bounds__(256, 3) l2_read_kernel(const char *__restrict__ buf, int window, int iters,
+                                                         int stride, float *__restrict__ out) {
+    __shared__ uint4 ring[4][8][64];  // per wave: eight 1 KiB pieces
+    const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), l16 = lane & 15, g = lane >> 4;
+    const int wid = blockIdx.x * 4 + w;
+    unsigned lo;
+    if (MODE == 0 || MODE == 1) lo = 16u * lane;
+    else if (MODE == 2) lo = (unsigned)stride * l16 + 32u * g;
+    else if (MODE == 4) lo = (unsigned)stride * (lane >> 3) + 16u * (lane & 7);  // 8 rows x 128 B
+    else lo = (unsigned)stride * (lane >> 2) + 16u * (lane & 3);                // 16 rows x 64 B
+    const unsigned span = (MODE == 0 || MODE == 1) ? 1024u : 16u * (unsigned)stride;
+    const unsigned nwin = (unsigned)window > span ? (unsigned)window - span : 0u;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int it = 0; it < iters; it += 8) {
+        if constexpr (MODE == 0 || MODE == 2 || MODE == 4 || MODE == 5) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const unsigned off = ((unsigned)(wid * 8 + it + u) * 4096u) % (nwin + 1u);
+                v[u] = *reinterpret_cast<const float4 *>(buf + off + lo);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const unsigned off = ((unsigned)(wid * 8 + it + u) * 4096u) % (nwin + 1u);
+                glds16_async_s(buf + off, lo, &ring[w][u][0]);
+            }
+            wait_vmcnt<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const uint4 q = ring[w][it & 7][lane];
+            acc.x += __uint_as_float(q.x);
+        }
+    }
+    out[(size_t)blockIdx.x * 256 + t] = acc.x + acc.y + acc.z + acc.w;
+}
 }  // namespace msat
+
+extern "C" int msat_probe_l2_read(const void *buf, int32_t window, int32_t mode, int32_t iters, int32_t grid,
+                                  int32_t stride, float *out, void *stream) {
+    MSAT_REQUIRE(buf && out && window >= 65536 && iters > 0 && iters % 8 == 0 && grid > 0 && mode >= 0 && mode <= 5 &&
+                     stride >= 128 && stride % 16 == 0 && 16 * stride < window,
+                 "bad l2_read args");
+    const char *b = static_cast<const char *>(buf);
+    hipStream_t s = (hipStream_t)stream;
+    if (mode == 0) hipLaunchKernelGGL(msat::l2_read_kernel<0>, dim3(grid), dim3(256), 0, s, b, window, iters, stride, out);
+    else if (mode == 1) hipLaunchKernelGGL(msat::l2_read_kernel<1>, dim3(grid), dim3(256), 0, s, b, window, iters, stride, out);
+    else if (mode == 2) hipLaunchKernelGGL(msat::l2_read_kernel<2>, dim3(grid), dim3(256), 0, s, b, window, iters, stride, out);
+    else if (mode == 3) hipLaunchKernelGGL(msat::l2_read_kernel<3>, dim3(grid), dim3(256), 0, s, b, window, iters, stride, out);
+    else if (mode == 4) hipLaunchKernelGGL(msat::l2_read_kernel<4>, dim3(grid), dim3(256), 0, s, b, window, iters, stride, out);
+    else hipLaunchKernelGGL(msat::l2_read_kernel<5>, dim3(grid), dim3(256), 0, s, b, window, iters, stride, out);
+    return msat::check_launch("l2_read_kernel");
+}
+
 
 extern "C" int msat_probe_strip_read(const float *D, int32_t M, int32_t ld, int32_t K, int32_t mode, float *out,
                                      void *stream) {

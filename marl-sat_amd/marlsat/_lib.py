@@ -194,7 +194,8 @@ def probe_lib():
                            ("msat_probe_obs_expand", [P, c_int32, c_int32, c_int32, P, P, P, c_int32, P]),
                            ("msat_probe_fill_rows", [P, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                                      P]),
-                           ("msat_probe_strip_read", [P, c_int32, c_int32, c_int32, c_int32, P, P])):
+                           ("msat_probe_strip_read", [P, c_int32, c_int32, c_int32, c_int32, P, P]),
+                           ("msat_probe_l2_read", [P, c_int32, c_int32, c_int32, c_int32, c_int32, P, P])):
             fn = getattr(d, name)
             fn.restype, fn.argtypes = c_int32, args
         _probe = d
