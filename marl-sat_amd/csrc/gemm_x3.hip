@@ -397,7 +397,7 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
 // bf16x3 body on the bf16x3 planes instead (same grid and LDS).
 constexpr int kDgW = 10;  // weight scale 2^10: |W| < 32 fits
 
-template <int RT, int NP>
+template <int RT, int NP, int NWV = 4>
 __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int lda, const int *__restrict__ rexp,
                                               const uint16_t *__restrict__ Wp, float *__restrict__ C, int ldc,
                                               const float *__restrict__ bias, int M, int N, int K, int accumulate,
@@ -416,12 +416,13 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
             ea[i] = e == kExpZero ? 0 : e;
         }
     }
-    // weight DMA: 8 NP wave-instructions (1 KiB = 16 rows x 4 chunks) per double slab, 2 NP per wave
-    constexpr int PW = 2 * NP;
+    // weight DMA: 8 NP wave-instructions (1 KiB = 16 rows x 4 chunks) per double slab, 2 NP per wave at
+    // NWV = 4 (NWV waves: ceil(8 NP / NWV), the last waves' surplus slots idle)
+    constexpr int PW = (8 * NP + NWV - 1) / NWV;
     unsigned voff[PW];
 #pragma unroll
     for (int e = 0; e < PW; ++e) {
-        const int x = PW * w + e, q = x >> 3, p = x & 7, row = 16 * p + (lane >> 2);
+        const int x = min(PW * w + e, 8 * NP - 1), q = x >> 3, p = x & 7, row = 16 * p + (lane >> 2);
         const int ch = (lane & 3) ^ x3swz16((row >> 2) & 3);
         voff[e] = (unsigned)(((size_t)q * N * K + (size_t)min(n0 + row, N - 1) * K + 8 * ch) * 2);
     }
@@ -430,7 +431,7 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
 #pragma unroll
         for (int e = 0; e < PW; ++e) {
             const int x = PW * w + e;
-            glds16_async_s(base, voff[e], &lds_w[buf][x >> 3][64 * (x & 7)]);
+            if (8 * NP % NWV == 0 || x < 8 * NP) glds16_async_s(base, voff[e], &lds_w[buf][x >> 3][64 * (x & 7)]);
         }
     };
     f32x4 acc[RT][8];
@@ -637,22 +638,25 @@ struct DgradProblem {
     int kr;  // first double slab of the k walk (aligns the two products' reads of the shared rows)
 };
 
-template <int RT>
-__global__ void __launch_bounds__(kX3T, RT == 2 ? 3 : 2)
+template <int RT, int NWV = 4>
+__global__ void __launch_bounds__(64 * NWV, NWV == 4 ? (RT == 2 ? 3 : 2) : 1)
 gemm_h2r16_dual_kernel(DgradProblem p0, DgradProblem p1, const int *__restrict__ rexp, int M, int K) {
-    __shared__ uint4 lds_w[2][3][kX3M * 4];
+    // the weight buffers, and the epilogue's per-wave stage (8 KiB per wave) in the same memory
+    constexpr int LDSU = (NWV * 8192 > 2 * 3 * kX3M * 4 * 16 ? NWV * 8192 : 2 * 3 * kX3M * 4 * 16) / 16;
+    __shared__ uint4 lds_raw[LDSU];
+    uint4 (*lds_w)[3][kX3M * 4] = reinterpret_cast<uint4 (*)[3][kX3M * 4]>(lds_raw);
     const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
     const int T = p0.ntn + p1.ntn, sub = id % T;
-    const int m0 = (id / T) * 64 * RT;
+    const int m0 = (id / T) * 16 * NWV * RT;
     const bool first = sub < p0.ntn;
     const DgradProblem &p = first ? p0 : p1;
     const int n0 = (first ? sub : sub - p0.ntn) * kX3M;
     if (*p.wbad)
-        gemm_r16_body<RT, 3>(p.A, p.lda, nullptr, p.Wx3, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0,
-                             p.vec_out, lds_w, p.kr);
+        gemm_r16_body<RT, 3, NWV>(p.A, p.lda, nullptr, p.Wx3, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0,
+                                  p.vec_out, lds_w, p.kr);
     else
-        gemm_r16_body<RT, 2>(p.A, p.lda, rexp, p.Wh2, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0, p.vec_out,
-                             lds_w, p.kr);
+        gemm_r16_body<RT, 2, NWV>(p.A, p.lda, rexp, p.Wh2, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0,
+                                  p.vec_out, lds_w, p.kr);
 }
 
 // planes[q][r][c] = part q of 2^kDgW W[r][(c + rot) % cols] (fp16x2, q = 0, 1); *bad = 1 if a scaled
@@ -1252,8 +1256,11 @@ extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h
         const long off = (long)(A0 - A1);
         if (lda0 == lda1 && off > 0 && off % 32 == 0 && off / 32 < K / 32) p[1].kr = (int)(off / 32);
     }
-    const int ntm = (M + 127) / 128;
-    hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(kX3T), 0,
+    // 384-row workgroups of 12 waves (one per CU, three per SIMD as before): each weight slab fetched into
+    // LDS serves 384 rows instead of 128, a third of the weight DMA pieces per output; bitwise the same
+    // result as 128-row workgroups, 1-2 % faster (profiles/r04w_ab_dgrad_waves.log)
+    const int ntm = (M + 383) / 384;
+    hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2, 12>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(768), 0,
                        (hipStream_t)stream, p[0], p[1], rexp, M, K);
     return check_launch("gemm_h2r16_dual_kernel");
 }
