@@ -122,15 +122,39 @@ def host_cpu() -> dict:
         "OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS") else "affinity")
     cap = int(os.environ.get("MARLSAT_CPU_BASELINE_CORES") or os.environ.get("OMP_NUM_THREADS") or affinity)
     return {"cpu_model": model, "affinity_cores": affinity, "cores": max(1, min(affinity, cap)),
-            "cap_source": cap_src}
+            "cap_source": cap_src, "cgroup_cpus": cgroup_cpus()}
 
 
-def cpu_baseline(V, C, vpa, pool, budget_s=12.0, nenv=16):
-    """Reference algorithm restated in NumPy (oracle), one single-thread process per host core."""
+def cgroup_cpus():
+    """The CPU time this process's cgroup may use, in CPUs (cgroup v2 cpu.max quota / period; v1
+    cfs_quota / cfs_period), or None when unlimited or unreadable: a process pool larger than this
+    shares that much CPU, whatever the affinity mask shows."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(V, C, vpa, pool, budget_s=12.0, nenv=16, cores=None):
+    """Reference algorithm restated in NumPy (oracle), one single-thread process per host core
+    (``cores`` processes; default: the box's CPU share, host_cpu())."""
     import multiprocessing as mp
 
     host = host_cpu()
-    cores = host["cores"]
+    if cores is None:
+        cores = host["cores"]
+    else:
+        host = dict(host, cores=cores, cap_source="all affinity cores")
     ctx = mp.get_context("fork")  # forked before any GPU initialisation
     with ctx.Pool(cores) as p:
         res = p.map(_cpu_worker, [(V, C, vpa, nenv, budget_s, w, pool) for w in range(cores)])
@@ -419,14 +443,15 @@ def _sig(x, n=4):
 def compact_leg(full: dict, side: Optional[str]) -> dict:
     """The MAPPO leg as it goes into the JSON line: ~0.6 KB, so the env side legs and both MAPPO legs fit the
     driver's 2,000-character tail (which also holds the run's stderr).  value = 1 / the median of the timed
-    cycles' s_per_update.  The full record (per-kernel table, both roofline views) is in the side file."""
+    cycles' s_per_update (with --mappo-cycles 3, the default, a true median of three).  The full record (per-kernel table, both roofline views) is in the side file."""
     c, r = full["config"], full["roofline"]
     ph = full["phase_ms"]
+    cyc = full.get("s_per_update_cycles", [full["s_per_update"]])
     return {
         "value": _sig(full["value"]),
-        "s_per_update": [_sig(v) for v in full.get("s_per_update_cycles", [full["s_per_update"]])],
-        "s_median": _sig(full["s_per_update"]), "samples_per_s": _sig(full["samples_per_s"]),
-        "adam_steps_per_s": _sig(full["adam_steps_per_s"]),
+        # min / median / max over the timed cycles (each cycle's time, in order, and Adam steps/s: side file)
+        "s_min_med_max": [_sig(min(cyc)), _sig(full["s_per_update"]), _sig(max(cyc))],
+        "samples_per_s": _sig(full["samples_per_s"]),
         "phase_ms": [round(ph[k]) for k in ("rollout", "gae", "ppo_update", "metrics")],
         "config": f"{c['workload']} A{c['num_agents']} m{c['max_vars_per_agent']} B{c['envs_per_gpu']}/gpu "
                   f"T{c['NUM_STEPS']} E{c['UPDATE_EPOCHS']} mb{c['MINIBATCH_SIZE']} H{c['GNN_HIDDEN_DIM']} "
@@ -486,9 +511,53 @@ def write_side_file(name: str, obj) -> Optional[str]:
 MIXED = ("uf50-218", "uf100-430", "uf200-860")  # BASELINE config 5 size classes (1024 envs per GPU of 8192)
 
 
-def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optional[int] = None):
+def clock_summary(vals) -> Optional[dict]:
+    """Median / p10 / p90 of per-workgroup clocks (MHz) from the env kernel's stamps."""
+    import torch
+
+    if vals is None or vals.numel() == 0:
+        return None
+    q = torch.quantile(vals, torch.tensor([0.1, 0.5, 0.9], dtype=vals.dtype)).tolist()
+    return {"median": round(q[1], 1), "p10": round(q[0], 1), "p90": round(q[2], 1), "workgroups": int(vals.numel())}
+
+
+def stamp_phases(log) -> Optional[dict]:
+    """Where an env launch's time goes, from the kernel's stamps (msat_step_out.clock_stamps, 100 MHz real
+    time): per launch, the span from the first workgroup's start to the last one's end, and over all
+    workgroups the median time from the launch's first start to each workgroup's start (dispatch) and the
+    median duration of each phase (wave 0's view), in microseconds; medians over the stamped launches."""
+    import statistics
+
+    if not log:
+        return None
+    names = ("assign_loaded", "clause_scan", "tables_staged", "images_built", "obs_stored")
+    span, disp, wg, ph = [], [], [], {n: [] for n in names}
+    for t in log:
+        t = t[t[:, 1] > 0]
+        if t.numel() == 0:
+            continue
+        st, en = t[:, 2], t[:, 7]
+        s0 = float(st.min())
+        span.append((float(en.max()) - s0) / 100.0)
+        disp.append(float((st - s0).median()) / 100.0)
+        wg.append(float((en - st).median()) / 100.0)
+        marks = [t[:, 2]] + [t[:, 3 + i] for i in range(4)] + [t[:, 7]]
+        for i, n in enumerate(names):
+            a, b = marks[i], marks[i + 1]
+            ok = (a > 0) & (b > 0)
+            if bool(ok.any()):
+                ph[n].append(float((b[ok] - a[ok]).median()) / 100.0)
+    med = lambda v: round(statistics.median(v), 3) if v else None
+    return {"launch_span_us": med(span), "dispatch_median_us": med(disp), "workgroup_median_us": med(wg),
+            "phase_median_us": {n: med(v) for n, v in ph.items()}, "launches": len(span)}
+
+
+def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optional[int] = None,
+            preroll_s: Optional[float] = None):
     """Time K fused env steps (+ auto-reset) over the local shard; returns the measurement dict.
-    workload / envs override --workload / --envs (the side legs)."""
+    workload / envs override --workload / --envs (the side legs).  Before the W warm-up steps, preroll_s
+    seconds of untimed back-to-back launches; after the timed region, --clock-launches launches with the
+    kernel's clock stamps on (msat_step_out.clock_stamps), and one stamped launch first of all (cold)."""
     import torch
 
     from marlsat import SATEnv
@@ -540,6 +609,46 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
     for st in states:
         st.step.copy_(torch.randint(0, 512, (st.num_envs,), generator=gen, device="cuda", dtype=torch.int32))
     counter = 1
+    # the same launches with the kernel's clock stamps on (a second out record carrying the stamp buffers)
+    nclk = args.clock_launches
+    cbufs = [torch.zeros((b, 8), dtype=torch.int64, device="cuda") for b in sizes]
+    couts = [dict(o, clock_stamps=c) for o, c in zip(outs, cbufs)]
+    if mixed:
+        cg = menv.stepper(states, obs, couts, autoreset=True, seed=seed)
+        cstep = lambda i, c: cg([a[i % ring] for a in acts], c)
+    else:
+        cs1 = classes[0].stepper(states[0], obs[0], couts[0], autoreset=True, seed=seed)
+        cstep = lambda i, c: cs1(acts[0][i % ring], c)
+
+    stamp_log = []  # per stamped launch: the (B, 8) stamp rows (msat_step_out.clock_stamps)
+
+    def stamped(n, counter):
+        vals = []
+        for i in range(n):
+            for c in cbufs:
+                c.zero_()
+            cstep(i, counter + i)
+            torch.cuda.synchronize()
+            t = torch.cat(cbufs).double()
+            stamp_log.append(t.cpu())
+            ok = t[:, 1] > 0
+            vals.append((t[ok, 0] / t[ok, 1] * 100.0).cpu())  # s_memrealtime ticks at 100 MHz
+        return torch.cat(vals) if vals else None
+
+    clk_cold = None
+    if nclk:
+        clk_cold = clock_summary(stamped(1, counter))  # the process's first env launch
+        counter += 1
+    # time-based pre-roll (untimed): DVFS settles under sustained load, a 5-launch warm-up is ~0.5 ms
+    preroll_s = args.preroll_s if preroll_s is None else preroll_s
+    n_pre, t_pre = 0, time.perf_counter()
+    while time.perf_counter() - t_pre < preroll_s:
+        for _ in range(32):
+            step(n_pre, counter)
+            counter += 1
+            n_pre += 1
+        torch.cuda.synchronize()
+    preroll = {"s": round(time.perf_counter() - t_pre, 3), "launches": n_pre}
     for i in range(args.warmup):
         step(i, counter)
         counter += 1
@@ -590,6 +699,15 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
     # restarted, so it ends below K; the others advanced by exactly K
     resets = int(sum(int((st.step < K).sum()) for st in states))
     assert all(bool(((st.step < K) | (st.step == sb + K)).all()) for st, sb in zip(states, step_before))
+    # the clock the kernel ran at, right after the timed region (stamped launches; not timed)
+    stamp_log.clear()  # keep the hot launches only
+    clk_hot = clock_summary(stamped(nclk, counter)) if nclk else None
+    counter += nclk
+    phases = stamp_phases(stamp_log)
+    if dist is not None and clk_hot is not None:  # the slowest rank's clock (MIN over ranks)
+        t = torch.tensor([clk_hot["median"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        clk_hot["median_min_over_ranks"] = float(t[0])
     per_class = []
     launch_bytes = 0
     for name, e, b in zip(names, classes, sizes):
@@ -601,7 +719,8 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
                           "num_agents": e.num_agents, "vars_per_agent": WORKLOADS[name][2], "envs_per_gpu": b,
                           "algorithmic_bytes_per_env_step": pe})
     return {"workload": workload, "names": names, "sizes": sizes, "elapsed": elapsed, "kern_ms": kern_ms,
-            "rank_ms": rank_ms, "K": K,
+            "rank_ms": rank_ms, "K": K, "sclk": clk_hot, "sclk_cold": clk_cold, "preroll": preroll,
+            "stamp_phases": phases,
             "kernel": kernel,
             "launch_bytes": launch_bytes, "per_class": per_class, "done_frac": done_frac, "resets": resets}
 
@@ -609,14 +728,18 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
 def env_side_legs(args, rank, world, dist) -> list:
     """BASELINE configs 2, 3 and 5 beside the headline env leg (``--env-legs``, 'workload:envs_per_gpu,...'):
     the same timed loop, compact records (whole-job env-steps/s, mean launch ms, HBM fraction)."""
-    out = []
+    out, stamps = [], {}
     for spec in filter(None, args.env_legs.split(",")):
         wl, envs = spec.split(":")
-        r = env_leg(args, rank, world, dist, wl, int(envs))
+        r = env_leg(args, rank, world, dist, wl, int(envs), preroll_s=min(args.preroll_s, 0.25))
         B = sum(r["sizes"])
         gbs = r["launch_bytes"] / (r["kern_ms"] * 1e-3) / 1e9
         out.append({"workload": wl, "envs_per_gpu": B, "value": _sig(B * r["K"] * world / r["elapsed"]),
-                    "kernel_ms": _sig(r["kern_ms"]), "frac": _sig(gbs / HBM_PEAK_GBS, 3)})
+                    "kernel_ms": _sig(r["kern_ms"]), "frac": _sig(gbs / HBM_PEAK_GBS, 3),
+                    "sclk_mhz": r["sclk"]["median"] if r["sclk"] else None})
+        stamps[f"{wl}:{B}"] = {"kernel_ms": r["kern_ms"], "sclk": r["sclk"], "phases": r["stamp_phases"]}
+    if rank == 0 and stamps:
+        write_side_file(f"env_stamps_n{world}", stamps)
     return out
 
 
@@ -630,16 +753,28 @@ def run_cpu_baselines(args) -> dict:
 
     names = MIXED if args.workload == "mixed" else (args.workload,)
     rates = []
-    for name in names:
-        V, C, vpa, _, size_id = WORKLOADS[name]
-        pnp = generate_problem_pool(V, C, min(256, args.pool), size_id=size_id)
-        rates.append(cpu_baseline(V, C, vpa, pnp, budget_s=args.cpu_budget / len(names)))
-    cpu = rates[0]
-    if len(rates) > 1:  # time to step one env of each class in the workload's proportions
-        tot = args.envs or 1024
-        sz = [tot // 3 + (1 if i < tot % 3 else 0) for i in range(3)]
-        cpu = dict(rates[0], value=sum(sz) / sum(b / r["value"] for b, r in zip(sz, rates)),
-                   sample=" | ".join(r["sample"] for r in rates))
+    host = host_cpu()
+
+    def leg(cores):
+        rates = []
+        for name in names:
+            V, C, vpa, _, size_id = WORKLOADS[name]
+            pnp = generate_problem_pool(V, C, min(256, args.pool), size_id=size_id)
+            rates.append(cpu_baseline(V, C, vpa, pnp, budget_s=args.cpu_budget / len(names), cores=cores))
+        cpu = rates[0]
+        if len(rates) > 1:  # time to step one env of each class in the workload's proportions
+            tot = args.envs or 1024
+            sz = [tot // 3 + (1 if i < tot % 3 else 0) for i in range(3)]
+            cpu = dict(rates[0], value=sum(sz) / sum(b / r["value"] for b, r in zip(sz, rates)),
+                       sample=" | ".join(r["sample"] for r in rates))
+        return cpu
+
+    # one worker per host core of the box (the affinity mask); beside it the run capped
+    # at the box's CPU share (OMP_NUM_THREADS), when that is smaller
+    cpu = leg(host["affinity_cores"] if args.cpu_all_cores else None)
+    if args.cpu_all_cores and host["cores"] < host["affinity_cores"]:
+        capped = leg(None)
+        cpu["capped"] = {"value": capped["value"], "cores": capped["cores"], "cap_source": host["cap_source"]}
     out = {"env": cpu, "mappo": None}
     legs = [s for s in args.mappo.split(",") if s]
     if legs:
@@ -702,8 +837,19 @@ def main():
                          "'mappo' (BASELINE config 3, the metric's 4096 envs), the others are 'mappo_other_legs' "
                          "(config 4: uf200-860, 25 agents, 4096 envs per GPU)")
     ap.add_argument("--mappo-micro-gb", type=float, default=240.0, help="activation budget per PPO micro-batch")
-    ap.add_argument("--mappo-cycles", type=int, default=2,
-                    help="timed train cycles per MAPPO leg (after one warm-up cycle); value = 1 / their median")
+    ap.add_argument("--mappo-cycles", type=int, default=3,
+                    help="timed train cycles per MAPPO leg (after one warm-up cycle); value = 1 / their median "
+                         "(min / median / max reported)")
+    ap.add_argument("--preroll-s", type=float, default=1.0,
+                    help="seconds of untimed back-to-back env launches before the --warmup steps of the headline env "
+                         "leg (the side legs run 0.25 s), so the timed region starts at the clock a long rollout "
+                         "runs at; reported in the line")
+    ap.add_argument("--clock-launches", type=int, default=8,
+                    help="env launches with the kernel's clock stamps on, right after the timed region (0: none): "
+                         "sclk_mhz in the line")
+    ap.add_argument("--cpu-all-cores", type=int, default=1,
+                    help="1: the env CPU baseline runs one worker per affinity core (BASELINE.md section 2), with the "
+                         "capped run (OMP_NUM_THREADS) beside it; 0: capped only")
     ap.add_argument("--env-legs", default="uf50-218:1024,uf100-430:4096,mixed:1024,mixed:8192",
                     help="env side legs 'workload:envs_per_gpu,...' ('' skips): BASELINE configs 2 and 3 and config 5 "
                          "(1024 envs per GPU = its 8-GPU share of 8192, and all 8192 on one GPU)")
@@ -803,6 +949,11 @@ def main():
             "done_fraction_last_step": r["done_frac"],
             "auto_resets_in_timed_region": r["resets"],
             "steady_state": "episode-step counters staggered uniformly over [0, 512) before warm-up",
+            # the shader clock the env kernel ran at (per-workgroup s_memtime / s_memrealtime deltas of stamped
+            # launches right after the timed region; cold = the process's first env launch), and the untimed
+            # time-based pre-roll ahead of the --warmup steps
+            "sclk_mhz": r["sclk"]["median"] if r["sclk"] else None,
+            "sclk": r["sclk"], "sclk_cold": r["sclk_cold"], "preroll": r["preroll"], "stamp_phases": r["stamp_phases"],
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,

@@ -109,6 +109,13 @@ typedef struct msat_step_out {
     uint8_t *solved;        /* (B,)  infos["solved"]                                 */
     int32_t *num_unsat;     /* (B,)  infos["num_unsatisfied"]  (nullable)            */
     int32_t *episode_step;  /* (B,)  infos["episode_step"]     (nullable)            */
+    /* Diagnostics, not reference state (nullable; NULL in every product call): per env 8 words from
+     * its workgroup's wave 0 -- [0] shader-clock counter delta (s_memtime) and [1] 100 MHz real-time
+     * counter delta over the workgroup's run (clock MHz = 100 * [0] / [1]); [2] real time at its
+     * start, [3..6] at the end of four phases (assignment in LDS, clause scan, agent tables staged,
+     * obs bit images built; 0 where a phase does not run), [7] at its end after its stores drained.
+     * bench.py reads it for the clock and the phase breakdown of its env steps. */
+    uint64_t *clock_stamps; /* (B,8) */
 } msat_step_out;
 
 const char *msat_last_error(void);

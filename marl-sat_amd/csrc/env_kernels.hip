@@ -281,13 +281,48 @@ __device__ __forceinline__ int xcd_major(int blk, int n, bool off) {
 // occupancy, 114-188 us vs 112 us at uf200 x 4096: the 8 resident workgroups per CU already overlap.)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Diagnostic stamps (msat_step_out.clock_stamps, NULL in product calls: a wave-uniform branch at each
+// point).  Per env, 8 words written by lane 0 of wave 0 (vector stores):
+//   [0] shader-clock counter delta over the workgroup's run (s_memtime), [1] the 100 MHz real-time counter
+//   delta (s_memrealtime): clock MHz = 100 [0] / [1];
+//   [2] real time at the workgroup's start, [3..6] at four phase ends (3: assignment bits + flips in LDS,
+//   i.e. the first global loads landed; 4: clause scan done; 5: agent tables staged; 6: obs bit images
+//   built), [7] at the end, after wave 0's stores have drained (vmcnt(0)).
+// Same CU, same wave: the ratio is the clock that CU ran at while it stepped this env, and the phase times
+// are wave 0's view of the env's dependent chain.
+struct ClockStamp {
+    uint64_t *buf = nullptr;
+    uint64_t t0 = 0, r0 = 0;
+    __device__ __forceinline__ ClockStamp(uint64_t *stamps, int b) {
+        if (stamps != nullptr) {
+            t0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
+            buf = stamps + 8 * (size_t)b;
+        }
+    }
+    __device__ __forceinline__ void mark(int i) const {
+        if (buf == nullptr) return;
+        const uint64_t r = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) buf[2 + i] = i == 0 ? r0 : r;
+    }
+    __device__ __forceinline__ void finish() const {
+        if (buf == nullptr) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x < 4) {
+            const int i = threadIdx.x;
+            buf[i == 3 ? 7 : i] = i == 0 ? t1 - t0 : i == 1 ? r1 - r0 : i == 2 ? r0 : r1;
+        }
+    }
+};
+
 // One environment (index b of its batch) advanced / reset / observed by one workgroup.
 template <int MODE, typename ObsT, int T>
 __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &pool, const msat_env_state &st,
                                         const int32_t *__restrict__ actions, const uint8_t *__restrict__ reset_mask,
                                         const int32_t *__restrict__ new_pidx, const uint8_t *__restrict__ new_assign,
                                         uint64_t seed, uint64_t ctr, const msat_step_out &out, ObsT *__restrict__ obs,
-                                        int b, uint32_t *smem) {
+                                        int b, uint32_t *smem, const ClockStamp &cs) {
     const EnvLds l = carve(smem, p);
     const int tid = threadIdx.x;
     if (MODE == kModeReset && reset_mask != nullptr && reset_mask[b] == 0) return;
@@ -330,6 +365,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         // ---- assignment + the agents' flips (env:230-250) --------------------
         load_x_bits<T>(p, l, xg);
         lds_barrier();
+        cs.mark(1);
         if (MODE == kModeObs) {
             // get_obs only: no flips, no state update
         } else if (p.action_mode == 0) {
@@ -366,6 +402,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         else
             eval_clauses<T, false, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
         lds_barrier();
+        cs.mark(2);
         if (MODE != kModeObs && tid == 0) {
             const int u_new = l.red[0];
             const bool solved = (u_new == 0);
@@ -460,10 +497,12 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         for (int t = tid; t < 2 * obs_image_words(p); t += T) l.fm[t] = 0u;  // fm, fx contiguous
     }
     lds_barrier();
+    cs.mark(3);
     ObsT *o = obs + (size_t)b * p.A * p.D;
     if ((p.ablate & 3) == 0) {
         build_obs_images<T>(p, l);
         lds_barrier();
+        cs.mark(4);
         write_obs<T, ObsT>(p, l, o);
     } else {
         constexpr int VEC = ObsVec<ObsT>::N;
@@ -480,7 +519,9 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
            ObsT *__restrict__ obs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int b = xcd_major(blockIdx.x, p.B, p.ablate & 4);
-    env_run<MODE, ObsT, T>(p, pool, st, actions, reset_mask, new_pidx, new_assign, seed, ctr, out, obs, b, smem);
+    const ClockStamp cs(out.clock_stamps, b);
+    env_run<MODE, ObsT, T>(p, pool, st, actions, reset_mask, new_pidx, new_assign, seed, ctr, out, obs, b, smem, cs);
+    cs.finish();
 }
 
 // Ragged batches (BASELINE config 5): several size classes, each its own (V, C, A) batch with its own
@@ -517,8 +558,10 @@ env_group_kernel(EnvGroups gs, uint64_t seed, uint64_t ctr) {
     for (int k = 1; k < MSAT_MAX_GROUPS; ++k)
         if (k < gs.G && gb >= gs.g[k].begin) g = k;
     const EnvGroup &e = gs.g[g];
+    const ClockStamp cs(e.out.clock_stamps, gb - e.begin);
     env_run<MODE, ObsT, T>(e.p, e.pool, e.st, e.actions, nullptr, nullptr, nullptr, seed ^ group_seed(e.gid), ctr, e.out,
-                        reinterpret_cast<ObsT *>(e.obs), gb - e.begin, smem);
+                        reinterpret_cast<ObsT *>(e.obs), gb - e.begin, smem, cs);
+    cs.finish();
 }
 
 // ---------------------------------------------------------------- cold path --

@@ -62,6 +62,7 @@ class StepOutC(ctypes.Structure):
         ("solved", c_void_p),
         ("num_unsat", c_void_p),
         ("episode_step", c_void_p),
+        ("clock_stamps", c_void_p),  # diagnostics (bench.py's clock), NULL otherwise
     ]
 
 

@@ -81,7 +81,8 @@ class MixedSATEnv:
         descs, cpools, cst, cobs = self._arrays([s.pool for s in states], sizes, states, obs)
         couts = (_lib.StepOutC * G)(*[
             _lib.StepOutC(o["reward"].data_ptr(), o["done"].data_ptr(), o["solved"].data_ptr(),
-                          o["num_unsatisfied"].data_ptr(), o["episode_step"].data_ptr()) for o in outs])
+                          o["num_unsatisfied"].data_ptr(), o["episode_step"].data_ptr(),
+                          _lib.ptr(o.get("clock_stamps"))) for o in outs])
         cact = (ctypes.c_void_p * G)()
         fn = _lib.lib.msat_env_step_grouped
         s = _lib.stream_ptr(self.device)

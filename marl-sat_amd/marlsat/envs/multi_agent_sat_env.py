@@ -386,8 +386,10 @@ class SATEnv:
         B = state.num_envs
         desc = self._desc(B, state.pool)
         cst = state._c()
+        # out["clock_stamps"] (optional, (B, 2) int64): the kernel's diagnostic clock stamps (bench.py)
         so = _lib.StepOutC(out["reward"].data_ptr(), out["done"].data_ptr(), out["solved"].data_ptr(),
-                           out["num_unsatisfied"].data_ptr(), out["episode_step"].data_ptr())
+                           out["num_unsatisfied"].data_ptr(), out["episode_step"].data_ptr(),
+                           _lib.ptr(out.get("clock_stamps")))
         fn = _lib.lib.msat_env_step
         cpool = state.pool.c(self)
         obs_p, s = obs.data_ptr(), _lib.stream_ptr(self.device)

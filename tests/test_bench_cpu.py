@@ -84,7 +84,7 @@ def test_side_legs_fit_the_driver_tail():
 
     kern = "gru_ln_fused_fwd_h2s_kernel (fp16x2, + x3r fixup launch)"
     full = {"metric": "MAPPO updates/sec", "value": 1 / 27.6123456, "unit": "updates/s", "s_per_update": 27.6123456,
-            "s_per_update_cycles": [27.6123456, 27.7123456],
+            "s_per_update_cycles": [27.6123456, 27.7123456, 27.5123456],
             "samples_per_s": 296.712345, "adam_steps_per_s": 0.579123,
             "phase_ms": {"rollout": 1618.1123, "gae": 122.7123, "ppo_update": 25631.7123, "metrics": 244.5123},
             "config": {"workload": "uf200-860", "num_agents": 25, "max_vars_per_agent": 8, "envs_per_gpu": 4096,
@@ -97,9 +97,9 @@ def test_side_legs_fit_the_driver_tail():
             "params_check": {"finite": True, "identical": True, "checksum": [123.4567890123, 1234567890123456789]}}
     leg = bench.compact_leg(full, "gpurun_out/bench_mappo_uf200-860_n8_rank0.json")
     env = [{"workload": w, "envs_per_gpu": b, "value": bench._sig(1.234567e8), "kernel_ms": bench._sig(0.0267123),
-            "frac": bench._sig(0.612345, 3)} for w, b in (("uf50-218", 1024), ("uf100-430", 4096), ("mixed", 1024),
+            "frac": bench._sig(0.612345, 3), "sclk_mhz": 2103.4} for w, b in (("uf50-218", 1024), ("uf100-430", 4096), ("mixed", 1024),
                                                           ("mixed", 8192))]
     tail = json.dumps({"env_other_legs": env, "mappo_other_legs": [leg], "mappo": leg})
     assert len(tail) < 1600, len(tail)
     assert leg["roofline"]["kernel"] == "gru_ln_fused_fwd_h2s_kernel" and leg["config"].endswith(" dp8")
-    assert leg["s_per_update"] == [27.61, 27.71] and leg["s_median"] == 27.61
+    assert leg["s_min_med_max"] == [27.51, 27.61, 27.71]

@@ -10,6 +10,7 @@ import torch
 from conftest import GOLDEN
 from oracle.rng import reset_draws
 from oracle.sat_env import OracleSATEnv
+from marlsat.random import Key
 
 pytestmark = pytest.mark.gpu
 
@@ -482,3 +483,41 @@ def test_config5_full_size_8192_properties_and_sampled_parity():
             np.testing.assert_array_equal(_np(st.variable_assignments)[sm], ost.variable_assignments)
             n_done[g] += int(outs[g]["done"].sum())
     assert all(n > 0 for n in n_done)
+
+
+@pytest.mark.parametrize("V,C,vpa,B", [(50, 218, 10, 64), (200, 860, 8, 16)])
+def test_clock_stamps_are_inert_and_plausible(V, C, vpa, B):
+    """The diagnostic stamps (msat_step_out.clock_stamps, bench.py's clock and phase breakdown) change no
+    output: the same auto-reset steps with and without them are bitwise equal; the stamps give a clock in a
+    plausible range and phase times in order (start <= each phase end <= end)."""
+    env, _ = _mk(V, C, vpa, max_steps=4)
+    pool = _pool(V, C, 6)
+    rng = np.random.default_rng(5)
+    pidx = rng.integers(0, 6, B).astype(np.int32)
+    x = rng.integers(0, 2, (B, V)).astype(np.uint8)
+    dpool = env.make_pool(pool)
+    runs = []
+    for stamp in (False, True):
+        obs, st = env.reset_from_pool(dpool, B, problem_idx=pidx, assignments=x)
+        out = env._step_out(B)
+        if stamp:
+            out["clock_stamps"] = torch.zeros((B, 8), dtype=torch.int64, device="cuda")
+        rec = []
+        for t in range(6):
+            a = torch.from_numpy(np.random.default_rng(10 + t).integers(0, env.max_vars_per_agent + 1,
+                                                                       (B, env.num_agents)).astype(np.int32)).cuda()
+            o, _ = env.step_raw(st, a, autoreset=True, key=Key(7, t + 1), out=out)
+            rec.append([_np(o).copy()] + [_np(out[k]).copy() for k in ("reward", "done", "num_unsatisfied")])
+        runs.append((rec, _np(st.variable_assignments).copy(), out.get("clock_stamps")))
+    for a, b in zip(runs[0][0], runs[1][0]):
+        for u, v in zip(a, b):
+            np.testing.assert_array_equal(u, v)
+    np.testing.assert_array_equal(runs[0][1], runs[1][1])
+    s = _np(runs[1][2]).astype(np.int64)
+    assert (s[:, 1] > 0).all()
+    mhz = 100.0 * s[:, 0] / s[:, 1]
+    assert (mhz > 300).all() and (mhz < 3000).all(), mhz
+    start, end = s[:, 2], s[:, 7]
+    for i in range(3, 7):
+        assert ((s[:, i] >= start) & (s[:, i] <= end)).all(), i
+    assert (np.diff(s[:, 3:7], axis=1) >= 0).all()
