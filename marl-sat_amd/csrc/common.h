@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <limits.h>
 
 #include "marlsat.h"
 #include "marlsat_net.h"  // every extern "C" definition is checked against its declaration
@@ -60,6 +61,19 @@ static inline int check_launch(const char *what) {
 static inline int check_launch(const char *what) { return check_launch_plain(what); }
 #define MSAT_DEBUG_BUILD 0
 #endif
+
+// Debug builds: the number of elements of size `elem` from p to the end of p's device allocation (for a
+// torch tensor: the end of its caching-allocator segment, so an index past the tensor but inside the segment
+// is not caught -- an index past the segment is).  The bounds the kernels' MSAT_DCHECKs compare against.
+// Product builds: 0 without a driver call (the checks compile to nothing).
+// (A pointer the runtime does not know -- NULL, host memory -- gets no bound: LLONG_MAX.)
+static inline long long dbg_extent(const void *p, size_t elem) {
+    if (!MSAT_DEBUG_BUILD) return 0;
+    hipDeviceptr_t base = nullptr;
+    size_t bytes = 0;
+    if (p == nullptr || hipMemGetAddressRange(&base, &bytes, (hipDeviceptr_t)p) != hipSuccess) return LLONG_MAX;
+    return (long long)(((const char *)base + bytes - (const char *)p) / (long long)elem);
+}
 
 #define MSAT_REQUIRE(cond, ...)                      \
     do {                                             \

@@ -40,6 +40,9 @@ struct EnvParams {
     float r_clause, r_sat, gamma;
     int ablate;  // diagnostics only (MARLSAT_ABLATE): bits 0-1: 0 full, 1 constant obs, 2 no obs write;
                  // bit 2: disable the XCD-major env order
+    // debug builds (MSAT_DCHECK): elements from each caller buffer's pointer to the end of its allocation
+    // (dbg_extent); 0 in product builds
+    long long dbg_obs, dbg_assign, dbg_sat, dbg_ntrue, dbg_actions;
 };
 
 enum : int { kModeReset = 0, kModeStep = 1, kModeStepAutoReset = 2, kModeObs = 3 };
@@ -334,6 +337,15 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
 
     bool do_reset = (MODE == kModeReset);
     int pidx = st.problem_idx[b];
+    if (MSAT_DEBUG_BUILD && tid == 0) {  // this env's rows of every caller buffer, and its pool row
+        if (MODE != kModeReset) MSAT_DCHECK(pidx, p.N);
+        MSAT_DCHECK((long long)(b + 1) * p.V - 1, p.dbg_assign);
+        MSAT_DCHECK((long long)(b + 1) * p.C - 1, p.dbg_sat);
+        if (ntrue_g) MSAT_DCHECK((long long)(b + 1) * p.C - 1, p.dbg_ntrue);
+        if (obs) MSAT_DCHECK((long long)(b + 1) * p.A * p.D - 1, p.dbg_obs);
+        if (MODE == kModeStep || MODE == kModeStepAutoReset)
+            MSAT_DCHECK((long long)(b + 1) * p.A * (p.action_mode == 0 ? 1 : p.M) - 1, p.dbg_actions);
+    }
     uint64_t pw[kPfClause];
     uint32_t prel[kPfRel], pnbr[kPfNbr];
     int step0 = 0, u_old = 0;
@@ -449,6 +461,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
             const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 0u);
             pidx = (int)(((uint64_t)r.x * (uint64_t)p.N) >> 32);
         }
+        if (MSAT_DEBUG_BUILD && tid == 0) MSAT_DCHECK(pidx, p.N);  // the reset's pool row
         if (new_assign != nullptr) {
             load_x_bits<T>(p, l, new_assign + (size_t)b * p.V);
         } else {
@@ -820,7 +833,19 @@ static int make_params(const msat_env_desc *d, EnvParams *p) {
     p->gamma = d->gamma;
     const char *ab = getenv("MARLSAT_ABLATE");
     p->ablate = ab ? atoi(ab) : 0;
+    p->dbg_obs = p->dbg_assign = p->dbg_sat = p->dbg_ntrue = p->dbg_actions = 0;
     return MSAT_OK;
+}
+
+// debug builds: the extents of the launch's caller buffers (EnvParams::dbg_*)
+static void set_dbg_extents(EnvParams *p, const msat_env_state *st, const int32_t *actions, const void *obs,
+                            int obs_dtype) {
+    if (!MSAT_DEBUG_BUILD) return;
+    p->dbg_obs = dbg_extent(obs, obs_dtype == MSAT_OBS_I32 ? 4 : 1);
+    p->dbg_assign = dbg_extent(st->assign, 1);
+    p->dbg_sat = dbg_extent(st->clause_sat, 1);
+    p->dbg_ntrue = dbg_extent(st->clause_ntrue, 1);
+    p->dbg_actions = dbg_extent(actions, 4);
 }
 
 static int check_state(const msat_env_state *st) {
@@ -862,12 +887,14 @@ static int launch_env(const EnvParams &p, const msat_env_desc *d, const msat_poo
     if (out) o = *out;
     if (p.B == 0) return MSAT_OK;
     const int T = env_threads(p);
+    EnvParams pd = p;  // + the buffer extents in debug builds
+    set_dbg_extents(&pd, st, actions, obs, d->obs_dtype);
 #define MSAT_ENV_LAUNCH(TT)                                                                                        \
     if (d->obs_dtype == MSAT_OBS_I32)                                                                              \
-        hipLaunchKernelGGL((env_kernel<MODE, int32_t, TT>), dim3(p.B), dim3(TT), lds, s, p, *pool, *st, actions,    \
+        hipLaunchKernelGGL((env_kernel<MODE, int32_t, TT>), dim3(p.B), dim3(TT), lds, s, pd, *pool, *st, actions,   \
                            mask, npidx, nassign, seed, ctr, o, (int32_t *)obs);                                    \
     else                                                                                                           \
-        hipLaunchKernelGGL((env_kernel<MODE, int8_t, TT>), dim3(p.B), dim3(TT), lds, s, p, *pool, *st, actions,     \
+        hipLaunchKernelGGL((env_kernel<MODE, int8_t, TT>), dim3(p.B), dim3(TT), lds, s, pd, *pool, *st, actions,    \
                            mask, npidx, nassign, seed, ctr, o, (int8_t *)obs);
     if (T == 64) {
         MSAT_ENV_LAUNCH(64)
@@ -921,6 +948,7 @@ static int launch_groups(int G, const msat_env_desc *descs, const msat_pool *poo
             e.out = outs[g];
         }
         e.obs = obs[g];
+        set_dbg_extents(&e.p, &e.st, e.actions, e.obs, descs[g].obs_dtype);
         total += e.p.B;
         lds = std::max(lds, env_lds_words(e.p) * 4);
         gs.ablate = e.p.ablate;

@@ -17,6 +17,17 @@ namespace msat {
 
 constexpr int kRowThreads = 256;  // 4 waves -> 4 rows per block iteration
 
+// Debug builds (MSAT_DCHECK): elements from each buffer's pointer to the end of its allocation (dbg_extent):
+// the sources, the destinations and the index array (slots / inc) and ptr; zeros in product builds.
+struct GatherDbg {
+    long long src_pos, src_neg, dst_pos, dst_neg, idx, ptr;
+};
+static GatherDbg gather_dbg(const void *sp, const void *sn, const void *dp, const void *dn, const void *idx,
+                            const void *ptr) {
+    return GatherDbg{dbg_extent(sp, 4), dbg_extent(sn, 4), dbg_extent(dp, 4), dbg_extent(dn, 4), dbg_extent(idx, 4),
+                     dbg_extent(ptr, 4)};
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // ------------------------------------------------------------------ gathers --
@@ -29,7 +40,7 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __ex
 __global__ void __launch_bounds__(kRowThreads)
 clause_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ src_neg, int lds_,
                      const int *__restrict__ slots, float *__restrict__ dst, int ldd, int Nc, int H, int merged,
-                     int accumulate) {
+                     int accumulate, GatherDbg dbg) {
     const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
     const int W = merged ? H : 2 * H;
     // two clause rows per wave, one per 32-lane half: twice the independent slot -> row load chains in
@@ -38,6 +49,7 @@ clause_gather_kernel(const float *__restrict__ src_pos, const float *__restrict_
     for (int c0 = 2 * (blockIdx.x * 4 + (threadIdx.x >> 6)); c0 < Nc; c0 += gridDim.x * 8) {
         const int c = c0 + half;
         if (c >= Nc) continue;
+        MSAT_DCHECK(3 * (long long)c + 2, dbg.idx);
         const int s0 = slots[3 * (size_t)c], s1 = slots[3 * (size_t)c + 1], s2 = slots[3 * (size_t)c + 2];
         for (int j = l32 * 4; j < W; j += 128) {
             const int want = j < H ? 0 : 1;  // split: first half positive literals, second negative
@@ -53,13 +65,17 @@ clause_gather_kernel(const float *__restrict__ src_pos, const float *__restrict_
                 ok[u] = S >= 0 && (merged || (S & 1) == want);
                 const float *src = (S & 1) ? src_neg : src_pos;
                 x[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (ok[u]) x[u] = *reinterpret_cast<const float4 *>(src + (size_t)(S >> 1) * lds_ + col);
+                if (ok[u]) {
+                    MSAT_DCHECK((long long)(S >> 1) * lds_ + col + 3, (S & 1) ? dbg.src_neg : dbg.src_pos);
+                    x[u] = *reinterpret_cast<const float4 *>(src + (size_t)(S >> 1) * lds_ + col);
+                }
             }
 #pragma unroll
             for (int u = 0; u < 3; ++u)
                 if (ok[u]) {
                     acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
                 }
+            MSAT_DCHECK((long long)c * ldd + j + 3, dbg.dst_pos);
             float4 *d = reinterpret_cast<float4 *>(dst + (size_t)c * ldd + j);
             if (accumulate) {
                 const float4 o = *d;
@@ -77,18 +93,20 @@ clause_gather_kernel(const float *__restrict__ src_pos, const float *__restrict_
 __global__ void __launch_bounds__(kRowThreads)
 var_gather_hw_kernel(const float *__restrict__ src_pos, const float *__restrict__ src_neg, int lds_,
                      const int *__restrict__ ptr, const int *__restrict__ inc, float *__restrict__ dst_pos,
-                     float *__restrict__ dst_neg, int ldd, int Nv, int H, int accumulate) {
+                     float *__restrict__ dst_neg, int ldd, int Nv, int H, int accumulate, GatherDbg dbg) {
     __shared__ int s_idx[4][64];  // per wave: each half's current chunk of 32 entries
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
     for (int v0 = 2 * (blockIdx.x * 4 + wv); v0 < Nv; v0 += gridDim.x * 8) {  // wave-uniform trip count
         const int v = v0 + half;
         const bool ok = v < Nv;
+        if (ok) MSAT_DCHECK(v + 1, dbg.ptr);
         const int e0 = ok ? ptr[v] : 0, ne = ok ? ptr[v + 1] - e0 : 0;
         const int nmax = max(__builtin_amdgcn_readlane(ne, 0), __builtin_amdgcn_readlane(ne, 32));
         for (int col = l32 * 4; col < H; col += 128) {
             float4 ap = make_float4(0.f, 0.f, 0.f, 0.f), an = ap;
             for (int cb = 0; cb < nmax; cb += 32) {
                 const int n = min(32, ne - cb);  // this half's entries in the chunk (<= 0: none)
+                if (l32 < n) MSAT_DCHECK((long long)e0 + cb + l32, dbg.idx);
                 s_idx[wv][lane] = l32 < n ? inc[e0 + cb + l32] : 0;
                 const int nm = min(32, nmax - cb);
                 for (int k = 0; k < nm; k += 8) {
@@ -100,6 +118,8 @@ var_gather_hw_kernel(const float *__restrict__ src_pos, const float *__restrict_
                         const int sl = s_idx[wv][32 * half + (kk < 32 ? kk : 31)];
                         sg[u] = kk < n ? (sl & 1) : -1;  // -1: no entry
                         const float *src = (sl & 1) ? src_neg : src_pos;
+                        if (sg[u] >= 0)
+                            MSAT_DCHECK((long long)(sl >> 1) * lds_ + col + 3, (sl & 1) ? dbg.src_neg : dbg.src_pos);
                         x[u] = sg[u] >= 0 ? *reinterpret_cast<const float4 *>(src + (size_t)(sl >> 1) * lds_ + col)
                                           : make_float4(0.f, 0.f, 0.f, 0.f);
                     }
@@ -114,6 +134,8 @@ var_gather_hw_kernel(const float *__restrict__ src_pos, const float *__restrict_
                 }
             }
             if (ok) {
+                MSAT_DCHECK((long long)v * ldd + col + 3, dbg.dst_pos);
+                MSAT_DCHECK((long long)v * ldd + col + 3, dbg.dst_neg);
                 float4 *dp = reinterpret_cast<float4 *>(dst_pos + (size_t)v * ldd + col);
                 float4 *dn = reinterpret_cast<float4 *>(dst_neg + (size_t)v * ldd + col);
                 if (accumulate) {
@@ -134,11 +156,13 @@ var_gather_hw_kernel(const float *__restrict__ src_pos, const float *__restrict_
 __global__ void __launch_bounds__(kRowThreads)
 var_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ src_neg, int lds_,
                   const int *__restrict__ ptr, const int *__restrict__ inc, float *__restrict__ dst_pos,
-                  float *__restrict__ dst_neg, int ldd, int Nv, int H, int accumulate) {
+                  float *__restrict__ dst_neg, int ldd, int Nv, int H, int accumulate, GatherDbg dbg) {
     __shared__ int s_idx[4][64];  // per wave: one chunk of the var row's entry list
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int v = blockIdx.x * 4 + (threadIdx.x >> 6); v < Nv; v += gridDim.x * 4) {
+        MSAT_DCHECK(v + 1, dbg.ptr);
         const int e0 = ptr[v], e1 = ptr[v + 1];
+        if (e1 > e0) MSAT_DCHECK((long long)e1 - 1, dbg.idx);
         for (int j = lane * 4; j < 2 * H; j += 256) {
             const int want = j < H ? 0 : 1;
             const int col = j < H ? j : j - H;
@@ -148,6 +172,7 @@ var_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ s
                 for (int e = e0; e < e1; ++e) {
                     const int s = inc[e];
                     if ((s & 1) != want) continue;
+                    MSAT_DCHECK((long long)(s >> 1) * lds_ + col + 3, want ? dbg.src_neg : dbg.src_pos);
                     const float4 x = *reinterpret_cast<const float4 *>(src + (size_t)(s >> 1) * lds_ + col);
                     acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
                 }
@@ -175,6 +200,7 @@ var_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ s
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int s = s_idx[wv][k[u]];
+                        if (ok[u]) MSAT_DCHECK((long long)(s >> 1) * lds_ + col + 3, want ? dbg.src_neg : dbg.src_pos);
                         x[u] = ok[u] ? *reinterpret_cast<const float4 *>(src + (size_t)(s >> 1) * lds_ + col)
                                      : make_float4(0.f, 0.f, 0.f, 0.f);
                     }
@@ -185,6 +211,7 @@ var_gather_kernel(const float *__restrict__ src_pos, const float *__restrict__ s
                         }
                 }
             }
+            MSAT_DCHECK((long long)v * ldd + col + 3, want ? dbg.dst_neg : dbg.dst_pos);
             float4 *d = reinterpret_cast<float4 *>((want ? dst_neg : dst_pos) + (size_t)v * ldd + col);
             if (accumulate) {
                 const float4 o = *d;
@@ -549,6 +576,7 @@ struct PartialSeg4 {
     float4 *dst[4];
     int N4[4], accumulate[4], ends[4];
     int nseg, nrows, ld4;
+    long long esrc[4], edst[4];  // debug builds: float4s to the end of each buffer's allocation
 };
 __global__ void __launch_bounds__(256)
 partial_reduce4_multi_kernel(PartialSeg4 p) {
@@ -562,6 +590,7 @@ partial_reduce4_multi_kernel(PartialSeg4 p) {
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c < N4)
         for (int r = ty; r < p.nrows; r += 16) {
+            MSAT_DCHECK((long long)r * p.ld4 + c, p.esrc[i]);
             const float4 v = part[(size_t)r * p.ld4 + c];
             a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
         }
@@ -574,6 +603,7 @@ partial_reduce4_multi_kernel(PartialSeg4 p) {
             t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
         }
         float4 *dst = p.dst[i];
+        MSAT_DCHECK(c, p.edst[i]);
         if (p.accumulate[i]) {
             const float4 o = dst[c];
             t.x = o.x + t.x; t.y = o.y + t.y; t.z = o.z + t.z; t.w = o.w + t.w;
@@ -597,7 +627,8 @@ colsum_partial_kernel(const float *__restrict__ G, int ldg, int M, int N, int ro
 // rows strided over the row lanes, combined through LDS in a fixed order -> deterministic).
 // part[split][:] = column sums of G rows [split*rows_per, +rows_per).
 __global__ void __launch_bounds__(256)
-colsum4_kernel(const float4 *__restrict__ G, int ldg4, int M, int N4, int rows_per, float4 *__restrict__ part) {
+colsum4_kernel(const float4 *__restrict__ G, int ldg4, int M, int N4, int rows_per, float4 *__restrict__ part,
+               long long eg, long long ep) {  // eg / ep: debug builds' extents of G and part, in float4s
     __shared__ float4 red[16][16];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int c = blockIdx.x * 16 + tx;
@@ -605,6 +636,7 @@ colsum4_kernel(const float4 *__restrict__ G, int ldg4, int M, int N4, int rows_p
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c < N4)
         for (int r = r0 + ty; r < r1; r += 16) {
+            MSAT_DCHECK((long long)r * ldg4 + c, eg);
             const float4 v = G[(size_t)r * ldg4 + c];
             a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
         }
@@ -616,6 +648,7 @@ colsum4_kernel(const float4 *__restrict__ G, int ldg4, int M, int N4, int rows_p
             const float4 v = red[k][tx];
             t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
         }
+        MSAT_DCHECK((long long)blockIdx.y * N4 + c, ep);
         part[(size_t)blockIdx.y * N4 + c] = t;
     }
 }
@@ -623,13 +656,14 @@ colsum4_kernel(const float4 *__restrict__ G, int ldg4, int M, int N4, int rows_p
 // dst[c] (+)= sum over the nrows rows of part (row stride ld4 float4s).
 __global__ void __launch_bounds__(256)
 partial_reduce4_kernel(const float4 *__restrict__ part, int nrows, int N4, int ld4, float4 *__restrict__ dst,
-                       int accumulate) {
+                       int accumulate, long long ep, long long ed) {  // ep / ed: debug extents, float4s
     __shared__ float4 red[16][16];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int c = blockIdx.x * 16 + tx;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c < N4)
         for (int r = ty; r < nrows; r += 16) {
+            MSAT_DCHECK((long long)r * ld4 + c, ep);
             const float4 v = part[(size_t)r * ld4 + c];
             a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
         }
@@ -641,6 +675,7 @@ partial_reduce4_kernel(const float4 *__restrict__ part, int nrows, int N4, int l
             const float4 v = red[k][tx];
             t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
         }
+        MSAT_DCHECK(c, ed);
         if (accumulate) {
             const float4 o = dst[c];
             t.x = o.x + t.x; t.y = o.y + t.y; t.z = o.z + t.z; t.w = o.w + t.w;
@@ -664,6 +699,11 @@ __global__ void relu_bwd_kernel(float *__restrict__ dy, const float *__restrict_
 // ---------------------------------------------------------- batch assembly --
 // Block per sample: instantiate the instance's graph templates at the sample's row
 // bases and compute its node features from the sample's assignment.
+// Debug builds: element extents of every buffer the kernel indexes (dbg_extent), checked at each access.
+struct AsmDbg {
+    long long x, svf, pool, t_vgid, t_cgid, t_slots, t_ptr, t_inc, vfeat, cfeat, cdeg, slots, ptr, inc, g_vbase, g_nv,
+        g_cbase, g_nc;
+};
 __global__ void __launch_bounds__(256)
 assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__restrict__ inst,
                             const uint8_t *__restrict__ x, const float *__restrict__ svf,
@@ -675,7 +715,7 @@ assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__rest
                             const int *__restrict__ gc, float *__restrict__ vfeat, float *__restrict__ cfeat,
                             float *__restrict__ cdeg, int *__restrict__ slots, int *__restrict__ ptr, int *__restrict__ inc,
                             int *__restrict__ g_vbase, int *__restrict__ g_nv, int *__restrict__ g_cbase,
-                            int *__restrict__ g_nc, int Nv, int nnz) {
+                            int *__restrict__ g_nc, int Nv, int nnz, AsmDbg dbg) {
     const int s = blockIdx.x;
     const int n = inst[s];
     const int vr0 = sb[3 * s], cr0 = sb[3 * s + 1], e0 = sb[3 * s + 2];
@@ -684,11 +724,21 @@ assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__rest
     const int nvr = gvn[G], ncr = gcn[G];
     const int ne = t_ptr[tp0 + nvr];
     const uint8_t *xs = x + (size_t)s * V;
+    if (threadIdx.x == 0) {
+        MSAT_DCHECK((long long)(s + 1) * V - 1, dbg.x);
+        MSAT_DCHECK((long long)tp0 + nvr, dbg.t_ptr);
+    }
     for (int t = threadIdx.x; t < nvr; t += blockDim.x) {
+        MSAT_DCHECK((long long)tv0 + t, dbg.t_vgid);
         const int gid = t_vgid[tv0 + t];
+        MSAT_DCHECK(gid, V);
+        MSAT_DCHECK((long long)(vr0 + t) * 8 + 7, dbg.vfeat);
+        MSAT_DCHECK(((long long)n * V + gid) * 3 + 2, dbg.svf);
         float *f = vfeat + (size_t)(vr0 + t) * 8;
         const float *sv = svf + ((size_t)n * V + gid) * 3;
         const int pb = t_ptr[tp0 + t], pe = t_ptr[tp0 + t + 1];
+        if (pe > pb) MSAT_DCHECK((long long)te0 + pe - 1, dbg.t_inc);
+        MSAT_DCHECK((long long)vr0 + t, dbg.ptr);
         int nneg = 0;
         for (int e = pb; e < pe; ++e) nneg += t_inc[te0 + e] & 1;
         f[0] = (float)(xs[gid] & 1u);
@@ -702,11 +752,20 @@ assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__rest
         ptr[vr0 + t] = e0 + pb;
     }
     for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+        MSAT_DCHECK((long long)te0 + e, dbg.t_inc);
+        MSAT_DCHECK((long long)e0 + e, dbg.inc);
         const int ent = t_inc[te0 + e];
         inc[e0 + e] = ((cr0 + (ent >> 1)) << 1) | (ent & 1);
     }
     for (int t = threadIdx.x; t < ncr; t += blockDim.x) {
+        MSAT_DCHECK((long long)tc0 + t, dbg.t_cgid);
+        MSAT_DCHECK((long long)(tc0 + t) * 3 + 2, dbg.t_slots);
+        MSAT_DCHECK((long long)(cr0 + t) * 3 + 2, dbg.slots);
+        MSAT_DCHECK((long long)(cr0 + t) * 3 + 2, dbg.cfeat);
+        if (cdeg) MSAT_DCHECK((long long)(cr0 + t) * 4 + 3, dbg.cdeg);
         const int gcid = t_cgid[tc0 + t];
+        MSAT_DCHECK(gcid, C);
+        MSAT_DCHECK((long long)n * C + gcid, dbg.pool);
         int npos = 0, nneg = 0;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -735,12 +794,19 @@ assemble_graph_batch_kernel(int S, int G, int A, int V, int C, const int *__rest
         f[2] = 1.0f;
     }
     for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        MSAT_DCHECK((long long)s * G + g, dbg.g_vbase);
+        MSAT_DCHECK((long long)s * G + g, dbg.g_nv);
+        MSAT_DCHECK((long long)s * G + g, dbg.g_cbase);
+        MSAT_DCHECK((long long)s * G + g, dbg.g_nc);
         g_vbase[s * G + g] = vr0 + gvn[g];
         g_nv[s * G + g] = gvn[g + 1] - gvn[g];
         g_cbase[s * G + g] = cr0 + gcn[g];
         g_nc[s * G + g] = gcn[g + 1] - gcn[g];
     }
-    if (s == 0 && threadIdx.x == 0) ptr[Nv] = nnz;
+    if (s == 0 && threadIdx.x == 0) {
+        MSAT_DCHECK(Nv, dbg.ptr);
+        ptr[Nv] = nnz;
+    }
 }
 
 }  // namespace msat
@@ -776,11 +842,13 @@ static int colsum_det(const float *G, int ldg, int M, int N, float *out, int acc
     if (N % 4 == 0 && ldg % 4 == 0 && a16(G) && a16(out) && a16(ws)) {
         const int sp = colsum4_splits(M, N), rows_per = (M + sp - 1) / sp, N4 = N / 4;
         hipLaunchKernelGGL(colsum4_kernel, dim3((N4 + 15) / 16, sp), dim3(256), 0, s,
-                           reinterpret_cast<const float4 *>(G), ldg / 4, M, N4, rows_per, reinterpret_cast<float4 *>(ws));
+                           reinterpret_cast<const float4 *>(G), ldg / 4, M, N4, rows_per, reinterpret_cast<float4 *>(ws),
+                           dbg_extent(G, 16), dbg_extent(ws, 16));
         int rc = check_launch("colsum4_kernel");
         if (rc) return rc;
         hipLaunchKernelGGL(partial_reduce4_kernel, dim3((N4 + 15) / 16), dim3(256), 0, s,
-                           reinterpret_cast<const float4 *>(ws), sp, N4, N4, reinterpret_cast<float4 *>(out), accumulate);
+                           reinterpret_cast<const float4 *>(ws), sp, N4, N4, reinterpret_cast<float4 *>(out), accumulate,
+                           dbg_extent(ws, 16), dbg_extent(out, 16));
         return check_launch("partial_reduce4_kernel");
     }
     const int sp = colsum_splits(M, N);
@@ -812,7 +880,7 @@ extern "C" int msat_clause_gather2(const float *src_pos, const float *src_neg, i
                  "bad clause_gather args");
     hipLaunchKernelGGL(clause_gather_kernel, dim3(grid_rows(num_clause_rows)), dim3(kRowThreads), 0,
                        (hipStream_t)stream, src_pos, src_neg, ld_src, slots, dst, ld_dst, num_clause_rows, H,
-                       merged ? 1 : 0, accumulate);
+                       merged ? 1 : 0, accumulate, gather_dbg(src_pos, src_neg, dst, dst, slots, nullptr));
     return check_launch("clause_gather_kernel");
 }
 
@@ -836,11 +904,12 @@ extern "C" int msat_var_gather2(const float *src_pos, const float *src_neg, int3
     if (H % 128 == 0) {
         hipLaunchKernelGGL(var_gather_hw_kernel, dim3(grid_rows(num_var_rows)), dim3(kRowThreads), 0,
                            (hipStream_t)stream, src_pos, src_neg, ld_src, ptr, inc, dst_pos, dst_neg, ld_dst,
-                           num_var_rows, H, accumulate);
+                           num_var_rows, H, accumulate, gather_dbg(src_pos, src_neg, dst_pos, dst_neg, inc, ptr));
         return check_launch("var_gather_hw_kernel");
     }
     hipLaunchKernelGGL(var_gather_kernel, dim3(grid_rows(num_var_rows)), dim3(kRowThreads), 0, (hipStream_t)stream,
-                       src_pos, src_neg, ld_src, ptr, inc, dst_pos, dst_neg, ld_dst, num_var_rows, H, accumulate);
+                       src_pos, src_neg, ld_src, ptr, inc, dst_pos, dst_neg, ld_dst, num_var_rows, H, accumulate,
+                       gather_dbg(src_pos, src_neg, dst_pos, dst_neg, inc, ptr));
     return check_launch("var_gather_kernel");
 }
 
@@ -963,7 +1032,8 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
     MSAT_REQUIRE(a16(partial) && a16(dln_scale) && (!bias || (a16(dbi) && a16(dbh_n))) && (!nfeat || a16(dfeat)),
                  "gru_ln_bwd_g4: partial / gradient outputs must be 16-byte aligned");
     hipLaunchKernelGGL(colsum4_kernel, dim3((W4 + 15) / 16, sp), dim3(256), 0, s,
-                       reinterpret_cast<const float4 *>(partial), W4, nb, W4, kPartRows, reinterpret_cast<float4 *>(ws));
+                       reinterpret_cast<const float4 *>(partial), W4, nb, W4, kPartRows, reinterpret_cast<float4 *>(ws),
+                       dbg_extent(partial, 16), dbg_extent(ws, 16));
     rc = check_launch("colsum4_kernel");
     if (rc) return rc;
     // stage 2: the segments [dln (2H) | dbi (3H) | dbh_n (H) | dfeat (3 nfeat H, the input matrix's feature rows,
@@ -979,6 +1049,8 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
         ps.N4[i] = n4;
         ps.accumulate[i] = acc;
         ps.ends[i] = (i ? ps.ends[i - 1] : 0) + (n4 + 15) / 16;
+        ps.esrc[i] = dbg_extent(ps.src[i], 16);
+        ps.edst[i] = dbg_extent(dst, 16);
     };
     add_seg(0, 2 * H / 4, dln_scale, accumulate_ln);
     if (bias) {
@@ -1035,10 +1107,15 @@ extern "C" int msat_assemble_graph_batch(
                  "NULL pointer");
     MSAT_REQUIRE(G >= 1 && G <= A + 1, "G must be 1 (critic only) or A+1");
     if (!S) return MSAT_OK;
+    const AsmDbg dbg{dbg_extent(x, 1),       dbg_extent(svf, 4),     dbg_extent(pool, 8),    dbg_extent(t_vgid, 4),
+                     dbg_extent(t_cgid, 4),  dbg_extent(t_slots, 4), dbg_extent(t_ptr, 4),   dbg_extent(t_inc, 4),
+                     dbg_extent(vfeat, 4),   dbg_extent(cfeat, 4),   dbg_extent(cdeg, 4),    dbg_extent(slots, 4),
+                     dbg_extent(ptr, 4),     dbg_extent(inc, 4),     dbg_extent(g_vbase, 4), dbg_extent(g_nv, 4),
+                     dbg_extent(g_cbase, 4), dbg_extent(g_nc, 4)};
     hipLaunchKernelGGL(assemble_graph_batch_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, S, G, A, V, C, inst, x,
                        svf, reinterpret_cast<const uint64_t *>(pool), sample_bases, t_vgid, t_cgid, t_slots, t_ptr,
                        t_inc, voff, coff, eoff, poff, gv, gc, vfeat, cfeat, cdeg, slots, ptr, inc, g_vbase, g_nv, g_cbase,
-                       g_nc, Nv, nnz);
+                       g_nc, Nv, nnz, dbg);
     return check_launch("assemble_graph_batch_kernel");
 }
 

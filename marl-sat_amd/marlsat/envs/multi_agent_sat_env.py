@@ -371,7 +371,8 @@ class SATEnv:
         x = None if assignments is None else torch.as_tensor(assignments, device=self.device).to(torch.uint8).contiguous()
         k = as_key(key)
         so = _lib.StepOutC(out["reward"].data_ptr(), out["done"].data_ptr(), out["solved"].data_ptr(),
-                           out["num_unsatisfied"].data_ptr(), out["episode_step"].data_ptr())
+                           out["num_unsatisfied"].data_ptr(), out["episode_step"].data_ptr(),
+                           _lib.ptr(out.get("clock_stamps")))
         _lib.check(_lib.lib.msat_env_step(self._desc(B, state.pool), state.pool.c(self), state._c(),
                                           a.data_ptr(), 1 if autoreset else 0, _lib.ptr(pidx), _lib.ptr(x), k.seed,
                                           k.counter, so, _lib.ptr(obs), _lib.stream_ptr(self.device)),

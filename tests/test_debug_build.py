@@ -83,11 +83,23 @@ def test_debug_library_checks_the_gru_backward():
         outs[name] = {k: v.clone() for k, v in out.items()}
     for k in outs["product"]:
         assert torch.equal(outs["product"][k], outs["debug"][k]), k
-    # an allocation smaller than msat_gru_ln_bwd_partial_floats: refused before the launch
-    small = torch.empty(cap // 2, device="cuda")
-    args, _, keep = _bwd_args(torch, R, H, nfeat, feat, small)
-    assert dbg.msat_gru_ln_bwd_g4fe(*args, s) == -1
-    assert b"partial buffer smaller" in dbg.msat_last_error()
+    # an allocation smaller than msat_gru_ln_bwd_partial_floats: refused before the launch.  Allocated by
+    # hipMalloc itself, so its extent is its own (a torch tensor may be carved from a larger cached segment)
+    hip = ctypes.CDLL("libamdhip64.so")
+    raw = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(raw), ctypes.c_size_t(4 * (cap // 2))) == 0
+
+    class Small:  # the one attribute _bwd_args reads of the partial buffer
+        def data_ptr(self):
+            return raw.value
+
+    try:
+        args, _, keep = _bwd_args(torch, R, H, nfeat, feat, Small())
+        assert dbg.msat_gru_ln_bwd_g4fe(*args, s) == -1
+        assert b"partial buffer smaller" in dbg.msat_last_error()
+    finally:
+        torch.cuda.synchronize()
+        hip.hipFree(raw)
     # an unwritten feature row (NaN, as MARLSAT_DEBUG=1 assembly poisons them): the device check names its row
     bad = feat.clone()
     bad[12345, 1] = float("nan")
@@ -100,3 +112,45 @@ def test_debug_library_checks_the_gru_backward():
     assert dbg.msat_gru_ln_bwd_g4fe(*args, s) == 0, dbg.msat_last_error()
     torch.cuda.synchronize()
     assert np.array_equal(out["dfeat"].cpu().numpy(), outs["product"]["dfeat"].cpu().numpy())
+
+
+TRAIN_SCRIPT = r"""
+import sys, torch
+sys.path[:0] = [{root!r}, {root!r} + '/marl-sat_amd']
+from marlsat import _lib
+assert _lib.LIB_PATH.endswith('libmarlsat_debug.so'), _lib.LIB_PATH
+from marlsat import SATEnv
+from marlsat.learners.gnn import GNNActorCritic
+from marlsat.learners.mappo_gnn_sat_learner import MAPPOLearner
+from marlsat.random import PRNGKey
+from marlsat.utils.generate_cnf_dataset import generate_problem_pool
+cfg = dict(NUM_ENVS=4, NUM_STEPS=2, NUM_UPDATES=10, UPDATE_EPOCHS=1, MINIBATCH_SIZE=4, LEARNING_RATE=3e-3,
+           GAMMA=0.99, GAE_LAMBDA=0.95, CLIP_EPS=0.2, ENT_COEF=0.01, VF_COEF=0.5, VF_CLIP=0.2, ANNEAL_LR=True,
+           LR_START_FACTOR=1.0, LR_END_FLOOR=1e-5, GNN_HIDDEN_DIM=128, GNN_NUM_MESSAGE_PASSING_STEPS=2, action_mode=0)
+env = SATEnv(50, 218, max_steps=2, vars_per_agent=10)
+pool = env.make_pool(generate_problem_pool(50, 218, 4, size_id=12, skip_isolated=True))
+net = GNNActorCritic(128, 2, env.num_agents, env.max_vars_per_agent, 0, 50, device="cuda", seed=4)
+learner = MAPPOLearner(cfg, env, net, pool)
+rs = learner.init_runner_state(PRNGKey(1))
+rs, metrics = learner.train_cycle(rs, 0, torch.Generator().manual_seed(7))
+assert torch.isfinite(net.params).all()
+print("debug train cycle ok", _lib.LIB_PATH)
+"""
+
+
+@pytest.mark.gpu
+def test_debug_library_runs_a_train_cycle():
+    """A small train cycle (uf50, H = 128, L = 2: env steps, batch assembly with NaN-poisoned feature rows,
+    gathers, GRU forward / backward, reductions, GEMMs, Adam) on libmarlsat_debug.so with MARLSAT_DEBUG=1 (every
+    launch synchronised and its device bounds checks read back; host-side planned-vs-actual totals), in a child
+    process so that the library it loads is the debug one."""
+    import sys
+
+    path = os.path.join(LIBDIR, "libmarlsat_debug.so")
+    if not os.path.exists(path):
+        pytest.skip("libmarlsat_debug.so not built")
+    env = dict(os.environ, MARLSAT_LIB=path, MARLSAT_DEBUG="1")
+    r = subprocess.run([sys.executable, "-c", TRAIN_SCRIPT.format(root=ROOT)], capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "debug train cycle ok" in r.stdout and "libmarlsat_debug.so" in r.stdout

@@ -317,11 +317,15 @@ def test_gemm_x3_fp32_accuracy(M, N, K, lda):
         _ref_close(C, ref, absprod)
 
 
-@pytest.mark.parametrize("M,K1", [(1, 128), (4999, 128), (70001, 256)])
-def test_dual_launches_match_fp64(M, K1):
+@pytest.mark.parametrize("M,K1,wbig", [(1, 128, None), (4999, 128, None), (70001, 256, None), (385, 256, "Wh"),
+                                       (385, 128, "F"), (4999, 256, "both")])
+def test_dual_launches_match_fp64(M, K1, wbig):
     """A GRU cell's two data gradients (msat_gemm_h2_dual) and two weight gradients (msat_gemm_wgrad_h2_dual)
     from one packed buffer D = [dan | dar | daz | dan r] (ld 4H): dh (+)= D[:, H:] @ Wh^T, dx = D[:, :3H] @ F^T,
-    dWh (+)= h^T D[:, H:], dF (+)= x^T D[:, :3H] rotated by 2H -- each against fp64 at the fp32 bound."""
+    dWh (+)= h^T D[:, H:], dF (+)= x^T D[:, :3H] rotated by 2H -- each against fp64 at the fp32 bound.
+    wbig: one weight of Wh / F / both at 48 (2^10 * 48 is past fp16's range): the weight split flags it and the
+    dual data gradient runs its bf16x3 body (the 12-wave, three-plane form of the 384-row workgroups) for that
+    product; M = 385 leaves a one-row last block."""
     from marlsat import _lib
 
     H = 128
@@ -331,6 +335,10 @@ def test_dual_launches_match_fp64(M, K1):
     rexp = row_exp(D)
     Wh = torch.randn(H, 3 * H, device="cuda", generator=g) * 0.1   # dh rows N0 = H, K = 3H
     F = torch.randn(K1, 3 * H, device="cuda", generator=g) * 0.1   # dx rows N1 = K1
+    if wbig in ("Wh", "both"):
+        Wh[3, 7] = 48.0
+    if wbig in ("F", "both"):
+        F[K1 - 1, 5] = -48.0
     s = _lib.stream_ptr()
     planes = []
     for Wm in (Wh, F):
@@ -342,6 +350,8 @@ def test_dual_launches_match_fp64(M, K1):
         _lib.check(_lib.lib.msat_split_f16x2_rot(Wm.data_ptr(), n, k, k, rot, p2.data_ptr(), bad.data_ptr(), s), "s2")
         _lib.check(_lib.lib.msat_split_bf16x3_rot(Wm.data_ptr(), n, k, k, rot, p3.data_ptr(), s), "s3")
         planes.append((p2, p3, bad))
+        # the split flags exactly the overflowing weight matrices
+        assert int(bad.item()) == (1 if wbig == "both" or (wbig == "Wh") == (Wm is Wh) and wbig else 0), wbig
     C0 = torch.randn(M, H, device="cuda", generator=g)
     dh = C0.clone()
     dx = torch.empty(M, K1, device="cuda")
