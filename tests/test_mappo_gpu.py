@@ -149,7 +149,9 @@ def _yard_close(dev, ref, yard, factor, what, rtol=1e-5, extra=None):
     atol = factor * (np.abs(yard[fin] - ref[fin]).max() if fin.any() else 0.0)
     err = np.abs(dev[fin] - ref[fin])
     bound = rtol * np.abs(ref[fin]) + atol + (0.0 if extra is None else np.asarray(extra, np.float64)[fin])
-    assert (err <= bound).all(), f"{what}: max err {err.max():.3g}, worst ratio {(err / bound).max():.3g}"
+    worst = float((err / np.maximum(bound, 1e-300)).max()) if err.size else 0.0
+    assert (err <= bound).all(), f"{what}: max err {err.max():.3g}, worst ratio {worst:.3g}"
+    return worst
 
 
 # (V, C, vars_per_agent, H, L, mode, (T, B, MB, E))
@@ -159,6 +161,9 @@ TRAIN_CYCLE_CASES = [
     # BASELINE config 4's network: uf200-860, 25 agents of m = 8, two samples, two Adam steps (the fp64
     # oracle runs 25 dense masked 200 x 860 encoders per sample and step; L = 8 keeps it to seconds)
     (200, 860, 8, 128, 8, 0, (1, 2, 1, 1)),
+    # the headline MAPPO leg's network (BASELINE config 3): uf100-430, 10 agents of m = 10, H = 128, L = 16,
+    # two Adam steps
+    (100, 430, 10, 128, 16, 0, (2, 4, 4, 1)),
 ]
 
 
@@ -271,14 +276,34 @@ def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode, shape
         lever = np.maximum(np.abs(v64 - tg), np.abs(vc - tg))
         prop = float(np.mean(lever * tol_v + 0.5 * tol_v ** 2))
         ref_l = np.asarray(out["f64"][0])
-        bound_l = 1e-5 * np.abs(ref_l) + 1e-8 + np.array([prop, 0.0, 0.0])
-        assert (np.abs(dev_losses[s] - ref_l) <= bound_l).all(), \
+        strict = 1e-5 * np.abs(ref_l) + 1e-8
+        bound_l = strict + np.array([prop, 0.0, 0.0])
+        err_l = np.abs(dev_losses[s] - ref_l)
+        assert (err_l <= bound_l).all(), \
             f"Adam step {s}: (value_loss, loss_actor, entropy) {dev_losses[s]} vs {ref_l}, bound {bound_l}"
+        # the allowance is fp32's own noise, not the device's: wherever the device's value loss needs it (misses
+        # the strict 1e-5 bar), the fp32 CPU oracle's value loss -- the reference's arithmetic class, in either
+        # row order -- misses that bar as well
+        e32_l = max(abs(out["f32"][0][0] - ref_l[0]), abs(out["f32r"][0][0] - ref_l[0]))
+        used = bool(err_l[0] > strict[0])
+        if used:
+            assert e32_l > strict[0], (f"Adam step {s}: the device value loss needs the propagated allowance "
+                                       f"(err {err_l[0]:.3g} > {strict[0]:.3g}) but the fp32 oracle's is within "
+                                       f"1e-5 ({e32_l:.3g})")
         g_dev = layout(rec["grads"])
+        gw, gk = 0.0, ""
         for k in P_s:
             g64, g32, g32r = out["f64"][1][k], out["f32"][1][k], out["f32r"][1][k]
             yard = np.where(np.abs(g32r - g64) > np.abs(g32 - g64), g32r, g32)  # elementwise, then max in _yard_close
-            _yard_close(g_dev[k], g64, yard, 4.0, f"step {s} grad {k}", extra=kink[k])
+            r = _yard_close(g_dev[k], g64, yard, 4.0, f"step {s} grad {k}", extra=kink[k])
+            if r >= gw:
+                gw, gk = r, k
+        # margins (printed; profiles/r05*_parity_margins.log): each loss's error over its strict 1e-5 bar and
+        # over the bar applied; the worst gradient tensor's error over its bar (1.0 = at the bar)
+        print(f"margins V{V} C{C} A{A} H{H} L{L} mode{mode} step {s}: loss err/strict "
+              f"{np.array2string(err_l / strict, precision=3)} err/bound {np.array2string(err_l / bound_l, precision=3)} "
+              f"value allowance used {used} (fp32 oracle value-loss err/strict {e32_l / strict[0]:.3g}); "
+              f"grad worst ratio {gw:.3g} ({gk})")
         # optax.adam in float64 on the device's own gradient, from the device's own parameters
         gflat = rec["grads"].double().cpu()
         if m_st["m"] is None:
