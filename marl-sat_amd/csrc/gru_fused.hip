@@ -267,8 +267,23 @@ gru_ln_fused_fwd_kernel(GruFwdArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Fast gate nonlinearities for the register-A epilogues: v_exp + v_rcp (<= 2 ulp each), no IEEE division.
 __device__ __forceinline__ float fsig_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
-__device__ __forceinline__ float ftanh_fast(float x) {  // 2 sigma(2x) - 1, saturates cleanly at +-1
-    return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f;
+// tanh to ~1.3 ulp relative everywhere.  2 sigma(2x) - 1 alone cancels for small |x| (absolute error ~1e-7
+// where tanh is ~x): in the L = 16 encoder that absolute error, divided by a LayerNorm row's small standard
+// deviation step after step, moved one uf100 critic value by 1e-5 (5e-4 relative) where the fp32 oracle
+// stays at 1e-7 (profiles/r05/r05d_*, r05e_*).  |x| < 0.625: odd minimax polynomial x + x u P(u), u = x^2
+// (degree 4 in u, fitted on the relative error, max 1.3 ulp); above: 2 sigma(2|x|) - 1 >= 0.55 (no
+// cancellation) with the sign of x.  Both branches evaluated, one selected (no divergence).
+constexpr float kTh1 = -0.33333277702331543f, kTh2 = 0.13331381976604462f, kTh3 = -0.05373896285891533f,
+                kTh4 = 0.020646216347813606f, kTh5 = -0.005720897577702999f, kThCut = 0.625f;
+__device__ __forceinline__ float ftanh_fast(float x) {
+    const float u = x * x;
+    float p = fmaf(u, kTh5, kTh4);
+    p = fmaf(u, p, kTh3);
+    p = fmaf(u, p, kTh2);
+    p = fmaf(u, p, kTh1);
+    const float small = fmaf(x, u * p, x);
+    const float big = 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * fabsf(x))) - 1.0f;
+    return fabsf(x) < kThCut ? small : copysignf(big, x);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -356,16 +371,9 @@ __device__ __forceinline__ f32x4g h2mma(const uint4 &a, const uint4 &b, const f3
 // 64-row "ping-pong" tiles at two workgroups per CU (5-7 % slower), 16-wave tiles (5-9 % slower),
 // deeper fragment lookahead (+-0.5 %), a split stagger of SIMD partners (0..+0.5 %).
 constexpr int kDmaLate = 8;  // waves 4..7 issue the step's DMA before this block (SIMD-partner stagger)
-//
-// PERSIST (gru_ln_fused_fwd_h2p_kernel): one workgroup per CU walks tiles; `pre` says the caller's previous
-// tile already issued this tile's first weight step and activation steps 0..2 (from its epilogue), and
-// next >= 0 asks this tile to do the same for tile `next` as soon as its epilogue has read h out of the
-// slots: the prologue's HBM round trip then overlaps this tile's gate / LayerNorm / store work instead of
-// following it (one workgroup fills the CU, so nothing else hides it).  The stage of the output flush
-// moves to weight buffer 1 (half rows, 34 KiB) because buffer 0 receives the next tile's step-0 weights.
-// Returns whether that prefetch was issued.
-template <bool PERSIST>
-__device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int next = -1, bool pre = false) {
+// (A persistent form -- one workgroup per CU walking tiles, each prefetching the next tile's prologue from its
+// epilogue -- measured 1-7 % slower in round 4; its source is profiles/archive_r04/gru_persistent.patch.)
+__device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
     constexpr int NW = 8;                // waves (16 rows each)
     constexpr int H = 128, IMG = H * 4;  // uint4 per (plane, gate) image: 128 units x 4 chunks = 8 KiB
     constexpr int NI = 6;                // (plane, gate) images per step
@@ -374,19 +382,15 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
     __shared__ uint4 Bs[2 * NI * IMG];   // 48 KiB per buffer
     constexpr int ASL = TR * 8;          // uint4 per activation slot (128 B per row)
     __shared__ uint4 As[4 * ASL];        // four activation slots: step s in slot s & 3
-    int t = threadIdx.x;
-    // persistent: the thread index is laundered per tile, so the per-lane addressing derived from it is
-    // recomputed inside the tile loop instead of being hoisted out of it and held (spilled) across tiles
-    if constexpr (PERSIST) asm volatile("" : "+v"(t));
+    const int t = threadIdx.x;
     const int lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int row0 = tile * TR, wr = 16 * w;
     int *const flag = a.flags + tile;
-    // weights out of fp16 range: the bf16x3 launch does every tile (the persistent kernel checks this once,
-    // before its tile loop: a load here would make the compiler's wait for it drain the previous tile's stores)
-    if (!PERSIST && (a.wbad[0] | a.wbad[1])) {
+    // weights out of fp16 range: the bf16x3 launch does every tile
+    if (a.wbad[0] | a.wbad[1]) {
         if (t == 0) *flag = 1;
-        return false;
+        return;
     }
     // step order: the input steps 0 .. nin - 1 first, then the hidden steps (h's four 32-column quarters),
     // whose activation slots still hold all of h at the epilogue (no refetch of h)
@@ -448,8 +452,7 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
     }
     // full tiles whose step lies inside one segment: a wave-uniform base and per-lane 32-bit offsets
     // (precomputed per source leading dimension); the last tile and a step straddling segments take the
-    // per-lane form below
-    // (r0: the tile's first row -- this tile's, or the next tile's for the persistent prefetch)
+    // per-lane form below (r0: the tile's first row)
     auto issueA = [&](int st, int r0) {
         const int k = st * 32;
         const bool full = r0 + TR <= a.R;
@@ -493,18 +496,8 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
         if (ns > 2) issueA(2, r0);
         issueW(0, 0);
     };
-    if (!PERSIST || !pre) {
-        prologue(row0);
-        wait_vmcnt<0>();
-    } else if (a.g4) {
-        // prefetched by the previous tile, whose epilogue then issued 136 stores (a full tile: 128 tape + 8 out)
-        // after it.  vmcnt counts in issue order and saturates at 63 in flight, so vmcnt(63) has the prefetch
-        // landed while the youngest stores keep draining under this tile's first step (its end-of-step wait
-        // retires them)
-        wait_vmcnt<63>();
-    } else {
-        wait_vmcnt<8>();  // the 8 output stores of the previous (full) tile's flush stay in flight
-    }
+    prologue(row0);
+    wait_vmcnt<0>();
     barrier_lds();
     lsplit(0, fas[0]);
     // one 32-k step; two static copies (input, hidden): the weight buffer's parity is a runtime offset and
@@ -586,15 +579,14 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
         if (t == 0) *flag = bad;
         if (bad) {
             wait_vmcnt<0>();  // no LDS-DMA may land after the workgroup's LDS is released
-            return false;
+            return;
         }
     }
 
     // ---- epilogue.  C/D map: unit u = 16 j + l16, row wr + 4 g + reg.
-    // stage: [16 rows][132] per wave in weight buffer 0; persistent: [16 rows][68] (half rows, flushed in two
-    // rounds) in weight buffer 1, below the range-check flags at its tail
-    constexpr int SW = PERSIST ? 68 : 132;
-    float *stage = reinterpret_cast<float *>(Bs) + (PERSIST ? NI * IMG * 4 : 0) + w * 16 * SW;
+    // stage: [16 rows][132] per wave in weight buffer 0
+    constexpr int SW = 132;
+    float *stage = reinterpret_cast<float *>(Bs) + w * 16 * SW;
     const bool tape = a.g4 != nullptr;
     // h of each accumulator's (row, unit) from the hidden steps' slots: quarter q (units 32 q ..) is step
     // nin + q in slot (nin + q) & 3, [row][8 chunks], chunk c of row r at c ^ ((r >> 1) & 5).  All four
@@ -615,69 +607,33 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
     constexpr float sc = 1.0f / (float)(1 << kH2Shift);  // exact power of two
     // packed fp32 (v_pk_mul / v_pk_add on row pairs): no MFMAs run here, so the packed forms halve the
     // epilogue's vector issue instead of competing with matrix work
-    // LayerNorm scale / bias, loaded with the gate biases.  Persistent: parked in a per-wave LDS copy
-    // ([128 scale | 128 bias], weight buffer 1 past the stage) instead of 16 registers across the epilogue
+    // LayerNorm scale / bias, loaded with the gate biases
     float lsc[8], lbs[8];
-    float *const lnp = reinterpret_cast<float *>(Bs) + NI * IMG * 4 + NW * 16 * SW + w * 2 * H;
-    static_assert(!PERSIST || (NI * IMG * 4 + NW * 16 * SW + NW * 2 * H) * 4 <= (2 * NI * IMG * 16 - 32),
-                  "stage + LayerNorm copies fit weight buffer 1 below the range-check flags");
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int u = 16 * j + l16;
-        float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
-        float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
-        // persistent: the compiler counts only its own loads, so a wait for these placed after the prefetch
-        // (it sinks their consumers there) would also wait for the whole prefetch; passing them through an
-        // empty asm makes it wait for them here, ahead of the prefetch
-        if constexpr (PERSIST) asm volatile("" : "+v"(br), "+v"(bz), "+v"(bni), "+v"(bnh));
+        const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
+        const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
         lsc[j] = a.ln_scale[u];
         lbs[j] = a.ln_bias[u];
-        if (PERSIST && g == 0) {
-            lnp[u] = lsc[j];
-            lnp[H + u] = lbs[j];
-        }
         const f32x4g s4 = {sc, sc, sc, sc};
         acc[0][j] = acc[0][j] * s4 + f32x4g{br, br, br, br};
         acc[1][j] = acc[1][j] * s4 + f32x4g{bz, bz, bz, bz};
         acc[2][j] = acc[2][j] * s4 + f32x4g{bni, bni, bni, bni};
         acc[3][j] = acc[3][j] * s4 + f32x4g{bnh, bnh, bnh, bnh};
     }
-    bool prefetched = false;
-    if constexpr (PERSIST) {
-        if (next >= 0) {
-            // the slots' rows are this wave's own (its activation DMA and its reads cover rows wr .. wr + 15), so
-            // once its h reads have returned it may refill them; weight buffer 0 was last read before the k
-            // loop's final barrier.  Issued after the epilogue's last global LOADS (the biases and LayerNorm
-            // parameters above, already consumed): vmcnt counts in issue order, so a load issued after the
-            // prefetch would make its consumer wait for the whole prefetch round trip.
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            prologue(next * TR);
-            prefetched = true;
-        }
-    }
     // float4 rows of the wave's [16][128] stage -> dst (row stride ld), rows < R only.  The stage is
     // wave-private and a wave's LDS operations complete in issue order, so waiting for its own stage
     // writes (lgkmcnt) is the only ordering needed: no workgroup barrier, whose release fence would
     // also drain the wave's global stores.
-    // (persistent: the half rows of columns c0 .. c0 + 63: 4 rows of 16 float4 per instruction)
-    auto flush = [&](float *dst, int ld, int c0 = 0) {
+    auto flush = [&](float *dst, int ld) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (PERSIST) {
 #pragma unroll
-            for (int it = 0; it < 4; ++it) {
-                const int rr = 4 * it + (lane >> 4), c4 = lane & 15;
-                const float4 v = *reinterpret_cast<const float4 *>(stage + rr * SW + 4 * c4);
-                const int row = row0 + wr + rr;
-                if (row < a.R) *reinterpret_cast<float4 *>(dst + (size_t)row * ld + c0 + 4 * c4) = v;
-            }
-        } else {
-#pragma unroll
-            for (int it = 0; it < 8; ++it) {
-                const int rr = 2 * it + (lane >> 5), c4 = lane & 31;
-                const float4 v = *reinterpret_cast<const float4 *>(stage + rr * SW + 4 * c4);
-                const int row = row0 + wr + rr;
-                if (row < a.R) *reinterpret_cast<float4 *>(dst + (size_t)row * ld + 4 * c4) = v;
-            }
+        for (int it = 0; it < 8; ++it) {
+            const int rr = 2 * it + (lane >> 5), c4 = lane & 31;
+            const float4 v = *reinterpret_cast<const float4 *>(stage + rr * SW + 4 * c4);
+            const int row = row0 + wr + rr;
+            if (row < a.R) *reinterpret_cast<float4 *>(dst + (size_t)row * ld + 4 * c4) = v;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
@@ -703,6 +659,19 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
     auto exp2v = [](f2 x) { return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; };
     auto rcpv = [](f2 x) { return f2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; };
     const f2 one = {1.f, 1.f}, ml2e = {-kL2E, -kL2E}, m2l2e = {-2.f * kL2E, -2.f * kL2E}, two = {2.f, 2.f};
+    // ftanh_fast on a row pair (packed FMAs for the polynomial branch)
+    auto tanhv = [&](f2 x) {
+        const f2 u = x * x;
+        auto fm = [](f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); };
+        f2 p = fm(u, f2{kTh5, kTh5}, f2{kTh4, kTh4});
+        p = fm(u, p, f2{kTh3, kTh3});
+        p = fm(u, p, f2{kTh2, kTh2});
+        p = fm(u, p, f2{kTh1, kTh1});
+        const f2 small = fm(x, u * p, x);
+        const f2 ax = {fabsf(x.x), fabsf(x.y)};
+        const f2 big = two * rcpv(one + exp2v(ax * m2l2e)) - one;
+        return f2{ax.x < kThCut ? small.x : copysignf(big.x, x.x), ax.y < kThCut ? small.y : copysignf(big.y, x.y)};
+    };
     f2 s1v[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, s2v[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -712,7 +681,7 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
             const f2 gi = {acc[2][j][2 * p], acc[2][j][2 * p + 1]}, gh = {acc[3][j][2 * p], acc[3][j][2 * p + 1]};
             const f2 h = {hv[j][2 * p], hv[j][2 * p + 1]};
             const f2 rg = rcpv(one + exp2v(rp * ml2e)), zg = rcpv(one + exp2v(zp * ml2e));
-            const f2 ng = two * rcpv(one + exp2v((gi + rg * gh) * m2l2e)) - one;  // tanh = 2 sigma(2x) - 1
+            const f2 ng = tanhv(gi + rg * gh);
             const f2 hn = (one - zg) * ng + zg * h;
             acc[0][j][2 * p] = hn.x;
             acc[0][j][2 * p + 1] = hn.y;
@@ -750,53 +719,23 @@ __device__ __forceinline__ bool gru_h2s_tile(const GruX3rArgs &a, int tile, int 
         const float var = fmaxf(t2 / (float)H - mean[r] * mean[r], 0.0f);
         rs[r] = rsqrtf(var + 1e-6f);
     }
-    // the stage holds JH column tiles (64 columns) per flush round persistent, all 8 otherwise
-    constexpr int JH = PERSIST ? 4 : 8;
 #pragma unroll
-    for (int j0 = 0; j0 < 8; j0 += JH) {
+    for (int j = 0; j < 8; ++j) {
+        const int u = 16 * j + l16;
+        const float scl = lsc[j], lb = lbs[j];
 #pragma unroll
-        for (int j = j0; j < j0 + JH; ++j) {
-            const int u = 16 * j + l16;
-            const float scl = PERSIST ? lnp[u] : lsc[j], lb = PERSIST ? lnp[H + u] : lbs[j];
-#pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const f2 hn = {acc[0][j][2 * p], acc[0][j][2 * p + 1]};
-                const f2 y = (hn - f2{mean[2 * p], mean[2 * p + 1]}) * (f2{rs[2 * p], rs[2 * p + 1]} * f2{scl, scl}) +
-                             f2{lb, lb};
-                stage[(4 * g + 2 * p) * SW + u - 16 * j0] = y.x;
-                stage[(4 * g + 2 * p + 1) * SW + u - 16 * j0] = y.y;
-            }
+        for (int p = 0; p < 2; ++p) {
+            const f2 hn = {acc[0][j][2 * p], acc[0][j][2 * p + 1]};
+            const f2 y = (hn - f2{mean[2 * p], mean[2 * p + 1]}) * (f2{rs[2 * p], rs[2 * p + 1]} * f2{scl, scl}) +
+                         f2{lb, lb};
+            stage[(4 * g + 2 * p) * SW + u] = y.x;
+            stage[(4 * g + 2 * p + 1) * SW + u] = y.y;
         }
-        flush(a.out, a.ldo, 16 * j0);
     }
-    return prefetched;
+    flush(a.out, a.ldo);
 }
 
-__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2s_kernel(GruX3rArgs a) {
-    gru_h2s_tile<false>(a, blockIdx.x);
-}
-
-// Persistent form: one workgroup per CU (gridDim.x <= tiles) walks tiles tile0, tile0 + gridDim.x, ...
-// (the same XCD's tiles: workgroup b sits on XCD b % 8), each prefetching the next one's prologue.
-// The argument block is re-read from the kernarg segment per tile (the segment pointer is laundered), so its
-// ~40 SGPRs of pointers are not held across the tile loop.
-__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2p_kernel(GruX3rArgs a, int ntiles, int prefetch) {
-    if (a.wbad[0] | a.wbad[1]) {  // weights out of fp16 range: the bf16x3 launch does every tile
-        for (int tile = blockIdx.x + threadIdx.x * gridDim.x; tile < ntiles; tile += blockDim.x * gridDim.x)
-            a.flags[tile] = 1;
-        return;
-    }
-    bool pre = false;
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int next = prefetch && tile + (int)gridDim.x < ntiles ? tile + (int)gridDim.x : -1;
-        typedef __attribute__((address_space(4))) const GruX3rArgs KArgs;
-        KArgs *ka = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(ka));
-        pre = gru_h2s_tile<true>(*(const GruX3rArgs *)ka, tile, next, pre);
-    }
-    (void)a;
-}
-
+__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2s_kernel(GruX3rArgs a) { gru_h2s_tile(a, blockIdx.x); }
 
 // bf16x3 register-A kernel (the fp16x2 kernel above is fp16x2-only: instantiated for bf16x3 it computed
 // wrong results; this is the round-1 kernel).  Activations loaded two steps ahead into registers, weight
@@ -1079,20 +1018,6 @@ __global__ void split_f16x2_t_kernel(const float *__restrict__ W, int K, int N, 
 
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// compute units of the current device (the persistent kernels' grid), read once
-static int device_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-            n = v;
-        else
-            n = 256;
-    }
-    return n;
-}
-
 }  // namespace msat
 
 using namespace msat;
@@ -1260,15 +1185,8 @@ extern "C" int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w
     a.flags = tile_flags;
     a.wbad = wbad;
     const int tiles = (R + 127) / 128;
-    const char *pe = getenv("MARLSAT_GRU_PERSIST");  // A/B switch (round 4)
-    if (pe && (pe[0] == '1' || pe[0] == '2')) {  // 2: the persistent walk without the prefetch (ablation)
-        hipLaunchKernelGGL(gru_ln_fused_fwd_h2p_kernel, dim3(std::min(tiles, device_cus())), dim3(512), 0,
-                           (hipStream_t)stream, a, tiles, pe[0] == '1' ? 1 : 0);
-        rc = check_launch("gru_ln_fused_fwd_h2p_kernel");
-    } else {
-        hipLaunchKernelGGL(gru_ln_fused_fwd_h2s_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
-        rc = check_launch("gru_ln_fused_fwd_h2s_kernel");
-    }
+    hipLaunchKernelGGL(gru_ln_fused_fwd_h2s_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
+    rc = check_launch("gru_ln_fused_fwd_h2s_kernel");
     if (rc) return rc;
     a.wiT = reinterpret_cast<const uint16_t *>(wiT_x3);
     a.whT = reinterpret_cast<const uint16_t *>(whT_x3);

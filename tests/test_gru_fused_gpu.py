@@ -116,17 +116,14 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
 def _fwd_cases():
     """(layout, H, R): the fp32 kernel at H 64 / 128 / 256, the register-A bf16x3 and fp16x2 kernels at
     H 128; the 70,000-row case at the production width H = 128 only."""
-    widths = {"plain": (64, 128, 256), "x3r": (128,), "h2r": (128,), "h2p": (128,)}
+    widths = {"plain": (64, 128, 256), "x3r": (128,), "h2r": (128,)}
     return [(lay, H, R) for lay, hs in widths.items() for H in hs for R in (0, 1, 77, 1000, 70000)
             if R != 70000 or H == 128]
 
 
 @pytest.mark.parametrize("layout,H,R", _fwd_cases())
 @pytest.mark.parametrize("kind", ["var", "clause", "var8", "clause4"])
-def test_fused_forward_matches_reference(R, H, kind, layout, monkeypatch):
-    if layout == "h2p":  # the persistent fp16x2 kernel (one workgroup per CU walking tiles)
-        monkeypatch.setenv("MARLSAT_GRU_PERSIST", "1")
-        layout = "h2r"
+def test_fused_forward_matches_reference(R, H, kind, layout):
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=R + H)
     g4 = torch.full((R, 4 * H), float("nan"), device="cuda")
     out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout)
@@ -148,16 +145,13 @@ def test_fused_forward_matches_reference(R, H, kind, layout, monkeypatch):
     assert bool((terr <= 2e-6 * ab + 1e-30).all()), float((terr / (ab + 1e-30)).max())
 
 
-@pytest.mark.parametrize("persist", ["0", "1"])
 @pytest.mark.parametrize("R,bad_tiles", [(1000, (1, 6)), (70000, (0, 300, 546))])
 @pytest.mark.parametrize("kind", ["var8", "clause4"])
-def test_h2r_out_of_range_tiles_take_the_bf16x3_path(kind, R, bad_tiles, persist, monkeypatch):
+def test_h2r_out_of_range_tiles_take_the_bf16x3_path(kind, R, bad_tiles):
     """fp16x2 range check: activations with |a| >= 2^15 in a row flag exactly its 128-row tile, which the
     fixup launch recomputes in bf16x3 (bitwise the x3r kernel's rows there), the other tiles keep the
-    fp16x2 result; weights with |W| >= 32 flag the split and every tile is bf16x3.  70,000 rows: more
-    tiles than CUs, so the persistent form (MARLSAT_GRU_PERSIST=1) meets a flagged tile first in a
-    workgroup's walk (tile 0), after a prefetched one (tile 300) and as the last, partial tile (546)."""
-    monkeypatch.setenv("MARLSAT_GRU_PERSIST", persist)
+    fp16x2 result; weights with |W| >= 32 flag the split and every tile is bf16x3.  70,000 rows: the first
+    tile, one in the middle and the last, partial tile (546)."""
     H = 128
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=3)
     for i, t in enumerate(bad_tiles):

@@ -226,8 +226,13 @@ def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode, shape
     p_start = layout(learner.trace[0]["params"])
     lp64, v64 = rollout_terms(to_t(p_start, torch.float64))
     lp32, v32 = rollout_terms(to_t(p_start, torch.float32))
-    _yard_close(flat(tr["log_prob"]), lp64, lp32, 2.0, "rollout log_prob")
-    _yard_close(flat(tr["value"]), v64, v32, 2.0, "rollout value")
+    vdev = flat(tr["value"]).astype(np.float64)
+    print(f"rollout V{V} C{C} A{A} H{H} L{L} mode{mode}: per-sample value |dev - f64| "
+          f"{np.array2string(np.abs(vdev - v64), precision=2)}, |f32 - f64| "
+          f"{np.array2string(np.abs(v32 - v64), precision=2)}, |value| {np.array2string(np.abs(v64), precision=3)}")
+    rl = _yard_close(flat(tr["log_prob"]), lp64, lp32, 2.0, "rollout log_prob")
+    rv = _yard_close(vdev, v64, v32, 2.0, "rollout value")
+    print(f"margins V{V} C{C} A{A} H{H} L{L} mode{mode} rollout: log_prob worst ratio {rl:.3g}, value worst ratio {rv:.3g}")
     adv, tgt = om.gae(tr["reward"], tr["value"], tr["done"].astype(bool), learner.last_val.cpu().numpy(),
                       cfg["GAMMA"], cfg["GAE_LAMBDA"])
     np.testing.assert_allclose(learner.targets.cpu().numpy(), tgt, rtol=1e-5, atol=1e-7)
