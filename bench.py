@@ -528,19 +528,28 @@ def stamp_phases(log) -> Optional[dict]:
     median duration of each phase (wave 0's view), in microseconds; medians over the stamped launches."""
     import statistics
 
+    import torch
+
     if not log:
         return None
     names = ("assign_loaded", "clause_scan", "tables_staged", "images_built", "obs_stored")
-    span, disp, wg, ph = [], [], [], {n: [] for n in names}
-    for t in log:
-        t = t[t[:, 1] > 0]
+    span, disp, dmax, wg, wg90, wgmax, wgreset, ph = [], [], [], [], [], [], [], {n: [] for n in names}
+    for t, done in log:
+        ok = t[:, 1] > 0
+        t, done = t[ok], done[ok]
         if t.numel() == 0:
             continue
         st, en = t[:, 2], t[:, 7]
         s0 = float(st.min())
+        dur = en - st
         span.append((float(en.max()) - s0) / 100.0)
         disp.append(float((st - s0).median()) / 100.0)
-        wg.append(float((en - st).median()) / 100.0)
+        dmax.append(float((st - s0).max()) / 100.0)
+        wg.append(float(dur.median()) / 100.0)
+        wg90.append(float(torch.quantile(dur, 0.9)) / 100.0)
+        wgmax.append(float(dur.max()) / 100.0)
+        if bool(done.any()):  # workgroups whose env finished its episode this step (and auto-reset)
+            wgreset.append(float(dur[done].median()) / 100.0)
         marks = [t[:, 2]] + [t[:, 3 + i] for i in range(4)] + [t[:, 7]]
         for i, n in enumerate(names):
             a, b = marks[i], marks[i + 1]
@@ -548,7 +557,9 @@ def stamp_phases(log) -> Optional[dict]:
             if bool(ok.any()):
                 ph[n].append(float((b[ok] - a[ok]).median()) / 100.0)
     med = lambda v: round(statistics.median(v), 3) if v else None
-    return {"launch_span_us": med(span), "dispatch_median_us": med(disp), "workgroup_median_us": med(wg),
+    return {"launch_span_us": med(span), "dispatch_median_us": med(disp), "dispatch_max_us": med(dmax),
+            "workgroup_median_us": med(wg), "workgroup_p90_us": med(wg90), "workgroup_max_us": med(wgmax),
+            "reset_workgroup_median_us": med(wgreset),
             "phase_median_us": {n: med(v) for n, v in ph.items()}, "launches": len(span)}
 
 
@@ -630,7 +641,7 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
             cstep(i, counter + i)
             torch.cuda.synchronize()
             t = torch.cat(cbufs).double()
-            stamp_log.append(t.cpu())
+            stamp_log.append((t.cpu(), torch.cat([o["done"] for o in outs]).cpu().bool()))
             ok = t[:, 1] > 0
             vals.append((t[ok, 0] / t[ok, 1] * 100.0).cpu())  # s_memrealtime ticks at 100 MHz
         return torch.cat(vals) if vals else None

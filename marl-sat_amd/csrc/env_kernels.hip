@@ -87,15 +87,22 @@ __device__ __forceinline__ EnvLds carve(uint32_t *smem, const EnvParams &p) {
 
 __device__ __forceinline__ uint32_t bit(const uint32_t *w, int i) { return (w[i >> 5] >> (i & 31)) & 1u; }
 
-// Assignment bytes -> LDS bit words, one ballot per 64 vars.
+// Assignment bytes -> LDS bit words, one ballot per 64 vars.  x0: this lane's byte of the first pass
+// (var threadIdx.x, loaded early by the caller; any value where threadIdx.x >= V).
 template <int T>
-__device__ __forceinline__ void load_x_bits(const EnvParams &p, const EnvLds &l, const uint8_t *__restrict__ xg) {
+__device__ __forceinline__ void load_x_bits(const EnvParams &p, const EnvLds &l, const uint8_t *__restrict__ xg,
+                                            uint32_t x0) {
     const int lane = threadIdx.x & 63;
     for (int v0 = threadIdx.x & ~63; v0 < p.WV * 32; v0 += T) {
         const int v = v0 + lane;
-        const uint64_t m = __ballot(v < p.V && (xg[v] & 1u));
+        const uint32_t xv = v0 == (int)(threadIdx.x & ~63) ? x0 : (v < p.V ? xg[v] : 0u);
+        const uint64_t m = __ballot(v < p.V && (xv & 1u));
         if (lane < 2) l.x[(v0 >> 5) + lane] = (uint32_t)(m >> (32 * lane));
     }
+}
+template <int T>
+__device__ __forceinline__ void load_x_bits(const EnvParams &p, const EnvLds &l, const uint8_t *__restrict__ xg) {
+    load_x_bits<T>(p, l, xg, (int)threadIdx.x < p.V ? xg[threadIdx.x] : 0u);
 }
 
 // Prefetch depth (per lane) of the step path: pool-row words (covers C <= kPfClause*T
@@ -336,6 +343,17 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
     if (tid < 16) l.red[tid] = 0;
 
     bool do_reset = (MODE == kModeReset);
+    // the per-lane loads that do not depend on problem_idx, issued together with it (one round trip): this
+    // lane's action and its assignment byte of the first ballot pass (clamped indices, no branches);
+    // problem_idx last, so that waiting for it retires the group.  (step / unsat are wave-uniform values the
+    // compiler moves to scalar registers as soon as they are loaded, which would wait for them: they go
+    // with the second round trip.)
+    int step0 = 0, u_old = 0, a0 = 0;
+    uint32_t x0 = 0;
+    if (MODE != kModeReset) {
+        if (MODE != kModeObs && p.action_mode == 0) a0 = actions[(size_t)b * p.A + min(tid, p.A - 1)];
+        x0 = xg[min(tid, p.V - 1)];
+    }
     int pidx = st.problem_idx[b];
     if (MSAT_DEBUG_BUILD && tid == 0) {  // this env's rows of every caller buffer, and its pool row
         if (MODE != kModeReset) MSAT_DCHECK(pidx, p.N);
@@ -346,36 +364,43 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         if (MODE == kModeStep || MODE == kModeStepAutoReset)
             MSAT_DCHECK((long long)(b + 1) * p.A * (p.action_mode == 0 ? 1 : p.M) - 1, p.dbg_actions);
     }
-    uint64_t pw[kPfClause];
-    uint32_t prel[kPfRel], pnbr[kPfNbr];
-    int step0 = 0, u_old = 0;
-    if (MODE != kModeReset) {
-        // ---- prefetch the instance's pool row and agent tables ----------------
-        const uint64_t *prow = reinterpret_cast<const uint64_t *>(pool.lits) + (size_t)pidx * p.C;
-        const uint32_t *rel_g = pool.rel + (size_t)pidx * p.A * p.WC;
-        const uint32_t *nbr_g = pool.nbr + (size_t)pidx * p.A * p.WV;
+    // the prefetch of an instance's pool row and agent tables into this lane's registers
+    auto prefetch = [&](int n, uint64_t (&w)[kPfClause], uint32_t (&rl)[kPfRel], uint32_t (&nb)[kPfNbr]) {
+        const uint64_t *prow = reinterpret_cast<const uint64_t *>(pool.lits) + (size_t)n * p.C;
+        const uint32_t *rel_g = pool.rel + (size_t)n * p.A * p.WC;
+        const uint32_t *nbr_g = pool.nbr + (size_t)n * p.A * p.WV;
 #pragma unroll
         for (int j = 0; j < kPfClause; ++j) {
             const int c = tid + j * T;
-            pw[j] = c < p.C ? prow[c] : 0ull;
+            w[j] = c < p.C ? prow[c] : 0ull;
         }
 #pragma unroll
         for (int j = 0; j < kPfRel; ++j) {
             const int t = tid + j * T;
-            prel[j] = t < p.A * p.WC ? rel_g[t] : 0u;
+            rl[j] = t < p.A * p.WC ? rel_g[t] : 0u;
         }
 #pragma unroll
         for (int j = 0; j < kPfNbr; ++j) {
             const int t = tid + j * T;
-            pnbr[j] = t < p.A * p.WV ? nbr_g[t] : 0u;
+            nb[j] = t < p.A * p.WV ? nbr_g[t] : 0u;
         }
-        // step-0 / unsat-0 and this lane's first action, loaded with the prefetch
+    };
+    // the instance a reset draws (env:158-162 via the rollout's reset, learner:426-436): the caller's index, or
+    // Philox word block 0 of (seed, ctr, env)
+    auto reset_instance = [&]() -> int {
+        if (new_pidx != nullptr) return new_pidx[b];
+        const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 0u);
+        return (int)(((uint64_t)r.x * (uint64_t)p.N) >> 32);
+    };
+    uint64_t pw[kPfClause];
+    uint32_t prel[kPfRel], pnbr[kPfNbr];
+    if (MODE != kModeReset) {
+        // ---- then the loads that do: the instance's pool row and agent tables (second round trip) --------
+        prefetch(pidx, pw, prel, pnbr);
         step0 = st.step[b];
         u_old = st.num_unsat[b];
-        int a0 = 0;
-        if (MODE != kModeObs && p.action_mode == 0 && tid < p.A) a0 = actions[(size_t)b * p.A + tid];
         // ---- assignment + the agents' flips (env:230-250) --------------------
-        load_x_bits<T>(p, l, xg);
+        load_x_bits<T>(p, l, xg, x0);
         lds_barrier();
         cs.mark(1);
         if (MODE == kModeObs) {
@@ -455,12 +480,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
 
     if (do_reset) {
         // ---- reset (env:158-181): new problem, new assignment ---------------
-        if (new_pidx != nullptr) {
-            pidx = new_pidx[b];
-        } else {
-            const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 0u);
-            pidx = (int)(((uint64_t)r.x * (uint64_t)p.N) >> 32);
-        }
+        pidx = reset_instance();
         if (MSAT_DEBUG_BUILD && tid == 0) MSAT_DCHECK(pidx, p.N);  // the reset's pool row
         if (new_assign != nullptr) {
             load_x_bits<T>(p, l, new_assign + (size_t)b * p.V);
