@@ -55,6 +55,14 @@ int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h2, const vo
                       float *C0, int32_t ldc0, int32_t N0, int32_t acc0, const float *A1, int32_t lda1,
                       const void *W1_h2, const void *W1_x3, const int32_t *wbad1, float *C1, int32_t ldc1, int32_t N1,
                       int32_t acc1, const int32_t *rexp, int32_t M, int32_t K, void *stream);
+/* The same with A0 / A1 the packed rows as fp16x2 planes (msat_gru_ln_bwd_g4fe with flags bit 3): lda in
+ * fp16 elements (% 8), the lo plane plo elements after the hi plane (% 8); the rows are taken as split.
+ * Bitwise the result of msat_gemm_h2_dual on the fp32 rows (the planes are the split it would make). */
+int msat_gemm_h2_dual_planes(const void *A0, int32_t lda0, const void *W0_h2, const void *W0_x3,
+                             const int32_t *wbad0, float *C0, int32_t ldc0, int32_t N0, int32_t acc0, const void *A1,
+                             int32_t lda1, const void *W1_h2, const void *W1_x3, const int32_t *wbad1, float *C1,
+                             int32_t ldc1, int32_t N1, int32_t acc1, int32_t plo, const int32_t *rexp, int32_t M,
+                             int32_t K, void *stream);
 int msat_gemm_h2(const float *A, int32_t lda, const int32_t *rexp, const void *Wplanes_h2, const void *Wplanes_x3,
                  const int32_t *wbad, float *C, int32_t ldc, const float *bias, int32_t M, int32_t N, int32_t K,
                  int32_t accumulate, void *stream);
@@ -78,6 +86,14 @@ int msat_gemm_wgrad_h2_dual(const float *A0, int32_t lda0, const float *G0, int3
                             int32_t K0, int32_t N0, int32_t rot0, const float *A1, int32_t lda1, const float *G1,
                             int32_t ldg1, float *W1, int32_t ldw1, int32_t K1, int32_t N1, int32_t rot1,
                             const int32_t *rexp, int32_t M, int32_t accumulate, void *workspace, void *stream);
+/* The same with G0 / G1 the packed rows as fp16x2 planes (msat_gru_ln_bwd_g4fe, flags bit 3): ldg in fp16
+ * elements (% 8), the lo plane plo elements after the hi plane (% 8, >= N), N % 8 == 0.  G is staged by
+ * LDS-DMA with no split; the split-wide scale moves to A (a 2^(ge - e_r)). */
+int msat_gemm_wgrad_h2_dual_planes(const float *A0, int32_t lda0, const void *G0, int32_t ldg0, float *W0,
+                                   int32_t ldw0, int32_t K0, int32_t N0, int32_t rot0, const float *A1, int32_t lda1,
+                                   const void *G1, int32_t ldg1, float *W1, int32_t ldw1, int32_t K1, int32_t N1,
+                                   int32_t rot1, int32_t plo, const int32_t *rexp, int32_t M, int32_t accumulate,
+                                   void *workspace, void *stream);
 int msat_gemm_wgrad_rot(const float *A, int32_t lda, const float *G, int32_t ldg, float *W, int32_t ldw,
                         int32_t M, int32_t K, int32_t N, int32_t rot, int32_t accumulate, void *workspace,
                         void *stream);
@@ -196,7 +212,10 @@ int msat_gru_ln_bwd_g4f(const float *dy, int32_t ldy, const float *g4, int32_t l
                         int32_t ldf, int32_t nfeat, float *dfeat, float *partial, int32_t R, int32_t H,
                         int32_t accumulate_ln, void *stream);
 /* msat_gru_ln_bwd_g4f (packed rows) + rexp[r] = the fp16x2 scale exponent of row r's largest |dG|
- * (max |dG| 2^e in [2^14, 2^15); 0x3fff for an all-zero row) for msat_gemm_wgrad_h2 / msat_gemm_h2. */
+ * (max |dG| 2^e in [2^14, 2^15); 0x3fff for an all-zero row) for msat_gemm_wgrad_h2 / msat_gemm_h2.
+ * Flags bit 3 (with the bias outputs and nfeat 2 or 6): the packed row is stored as fp16x2 planes at that
+ * exponent instead of fp32 -- the row's 4H floats at dGi + r lddi hold [hi (4H fp16) | lo (4H fp16)] with
+ * hi = fp16(x 2^e), lo = fp16(x 2^e - hi) (e = 0 for an all-zero row), for the *_planes products. */
 int msat_gru_ln_bwd_g4fe(const float *dy, int32_t ldy, const float *g4, int32_t ldg, const float *hprev, int32_t ldp,
                          const float *ln_scale, float *dGi, int32_t lddi, float *dGh, int32_t lddh, float *dhprev,
                          int32_t lddp, float *dln_scale, float *dln_bias, float *dbi, float *dbh_n, const float *feat,

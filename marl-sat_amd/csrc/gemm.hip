@@ -422,6 +422,10 @@ int msat_wgrad_dual_splits(int M, int K0, int K1);
 int msat_wgrad_h2_dual_launch(const float *A0, int lda0, const float *G0, int ldg0, float *part0, int K0, int N0, int rot0,
                               const float *A1, int lda1, const float *G1, int ldg1, float *part1, int K1, int N1,
                               int rot1, const int *rexp, int M, int splits, int *flags, hipStream_t s);
+int msat_wgrad_h2_dual_pl_launch(const float *A0, int lda0, const void *G0, int ldg0, float *part0, int K0, int N0,
+                                 int rot0, const float *A1, int lda1, const void *G1, int ldg1, float *part1, int K1,
+                                 int N1, int rot1, int plo, const int *rexp, int M, int splits, int *flags,
+                                 hipStream_t s);
 int msat_wgrad_h2w_launch(const float *A, int lda, const float *G, int ldg, const int *rexp, float *part, int M, int K,
                           int N, int rot, int splits, int *flags, hipStream_t s);
 int msat_wgrad_x3_launch(const float *A, int lda, const float *G, int ldg, float *part, int M, int K, int N, int splits,
@@ -633,30 +637,41 @@ extern "C" size_t msat_gemm_wgrad_dual_workspace_bytes(int32_t M, int32_t K0, in
 // W0 (+)= A0^T G0 and W1 (+)= A1^T G1 (each with its column rotation) over the same M rows of G's buffer,
 // whose row exponents are rexp, in one fp16x2 launch (+ fixup) and two fixed-order reduces: a GRU cell's
 // hidden and input weight gradients from its packed backward rows.  Conditions of msat_gemm_wgrad_h2.
-extern "C" int msat_gemm_wgrad_h2_dual(const float *A0, int32_t lda0, const float *G0, int32_t ldg0, float *W0,
-                                       int32_t ldw0, int32_t K0, int32_t N0, int32_t rot0, const float *A1,
-                                       int32_t lda1, const float *G1, int32_t ldg1, float *W1, int32_t ldw1,
-                                       int32_t K1, int32_t N1, int32_t rot1, const int32_t *rexp, int32_t M,
-                                       int32_t accumulate, void *workspace, void *stream) {
+// pl: G0 / G1 are fp16x2 planes (ldg in fp16 elements, lo plane plo elements after hi), else fp32 rows
+static int wgrad_h2_dual_impl(const float *A0, int32_t lda0, const void *G0, int32_t ldg0, float *W0, int32_t ldw0,
+                              int32_t K0, int32_t N0, int32_t rot0, const float *A1, int32_t lda1, const void *G1,
+                              int32_t ldg1, float *W1, int32_t ldw1, int32_t K1, int32_t N1, int32_t rot1, int pl,
+                              int32_t plo, const int32_t *rexp, int32_t M, int32_t accumulate, void *workspace,
+                              void *stream) {
     MSAT_REQUIRE(A0 && G0 && W0 && A1 && G1 && W1 && rexp && workspace, "NULL operand");
     const int Ks[2] = {K0, K1}, Ns[2] = {N0, N1}, rots[2] = {rot0, rot1}, ldas[2] = {lda0, lda1},
               ldgs[2] = {ldg0, ldg1}, ldws[2] = {ldw0, ldw1};
-    const float *As[2] = {A0, A1}, *Gs[2] = {G0, G1};
+    const float *As[2] = {A0, A1};
+    const void *Gs[2] = {G0, G1};
     for (int i = 0; i < 2; ++i) {
         MSAT_REQUIRE(M >= 0 && Ks[i] > kSkinnyK && Ns[i] >= 1 && Ns[i] <= 384 && ldas[i] >= Ks[i] && ldgs[i] >= Ns[i] &&
                          ldws[i] >= Ns[i],
                      "gemm_wgrad_h2_dual: bad dims (K > 8, N <= 384)");
         MSAT_REQUIRE(rots[i] >= 0 && rots[i] < Ns[i] && rots[i] % 4 == 0, "gemm_wgrad_h2_dual: bad rot");
-        MSAT_REQUIRE(msat_wgrad_x3_ok(As[i], ldas[i], Gs[i], ldgs[i], Ks[i], Ns[i]),
-                     "gemm_wgrad_h2_dual: K %% 4, N %% 4, ld %% 4 and 16-byte aligned operands required");
+        if (pl)  // whole 16-byte chunks of both planes (the DMA pieces)
+            MSAT_REQUIRE(Ks[i] % 4 == 0 && Ns[i] % 8 == 0 && ldas[i] % 4 == 0 && ldgs[i] % 8 == 0 && plo % 8 == 0 &&
+                             plo >= Ns[i] && (reinterpret_cast<uintptr_t>(As[i]) & 15) == 0 &&
+                             (reinterpret_cast<uintptr_t>(Gs[i]) & 15) == 0,
+                         "gemm_wgrad_h2_dual_planes: K %% 4, N %% 8, lda %% 4, ldg %% 8, plo %% 8 (>= N) and 16-byte "
+                         "aligned operands required");
+        else
+            MSAT_REQUIRE(msat_wgrad_x3_ok(As[i], ldas[i], (const float *)Gs[i], ldgs[i], Ks[i], Ns[i]),
+                         "gemm_wgrad_h2_dual: K %% 4, N %% 4, ld %% 4 and 16-byte aligned operands required");
     }
     MSAT_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "gemm_wgrad_h2_dual: workspace alignment");
     hipStream_t s = (hipStream_t)stream;
     const int splits = msat_wgrad_dual_splits(M, K0, K1);
     float *part0 = (float *)workspace, *part1 = part0 + (size_t)splits * K0 * N0;
     int *flags = reinterpret_cast<int *>(part1 + (size_t)splits * K1 * N1);
-    int rc = msat_wgrad_h2_dual_launch(A0, lda0, G0, ldg0, part0, K0, N0, rot0, A1, lda1, G1, ldg1, part1, K1, N1, rot1,
-                                       rexp, M, splits, flags, s);
+    int rc = pl ? msat_wgrad_h2_dual_pl_launch(A0, lda0, G0, ldg0, part0, K0, N0, rot0, A1, lda1, G1, ldg1, part1, K1,
+                                               N1, rot1, plo, rexp, M, splits, flags, s)
+                : msat_wgrad_h2_dual_launch(A0, lda0, (const float *)G0, ldg0, part0, K0, N0, rot0, A1, lda1,
+                                            (const float *)G1, ldg1, part1, K1, N1, rot1, rexp, M, splits, flags, s);
     if (rc) return rc;
     const bool v0 = N0 % 4 == 0 && ldw0 % 4 == 0 && (reinterpret_cast<uintptr_t>(W0) & 15) == 0;
     const bool v1 = N1 % 4 == 0 && ldw1 % 4 == 0 && (reinterpret_cast<uintptr_t>(W1) & 15) == 0;
@@ -680,6 +695,27 @@ extern "C" int msat_gemm_wgrad_h2_dual(const float *A0, int32_t lda0, const floa
     rc = wgrad_reduce(part0, splits, K0, N0, W0, ldw0, accumulate, s);
     if (rc) return rc;
     return wgrad_reduce(part1, splits, K1, N1, W1, ldw1, accumulate, s);
+}
+
+extern "C" int msat_gemm_wgrad_h2_dual(const float *A0, int32_t lda0, const float *G0, int32_t ldg0, float *W0,
+                                       int32_t ldw0, int32_t K0, int32_t N0, int32_t rot0, const float *A1,
+                                       int32_t lda1, const float *G1, int32_t ldg1, float *W1, int32_t ldw1,
+                                       int32_t K1, int32_t N1, int32_t rot1, const int32_t *rexp, int32_t M,
+                                       int32_t accumulate, void *workspace, void *stream) {
+    return wgrad_h2_dual_impl(A0, lda0, G0, ldg0, W0, ldw0, K0, N0, rot0, A1, lda1, G1, ldg1, W1, ldw1, K1, N1, rot1, 0,
+                              0, rexp, M, accumulate, workspace, stream);
+}
+
+// Same products with G0 / G1 the GRU backward's packed rows as fp16x2 planes (msat_gru_ln_bwd_g4fe, flags bit
+// 3): ldg in fp16 elements (% 8), the lo plane plo elements after the hi plane, N % 8 == 0.  Workspace as
+// msat_gemm_wgrad_dual_workspace_bytes.
+extern "C" int msat_gemm_wgrad_h2_dual_planes(const float *A0, int32_t lda0, const void *G0, int32_t ldg0, float *W0,
+                                              int32_t ldw0, int32_t K0, int32_t N0, int32_t rot0, const float *A1,
+                                              int32_t lda1, const void *G1, int32_t ldg1, float *W1, int32_t ldw1,
+                                              int32_t K1, int32_t N1, int32_t rot1, int32_t plo, const int32_t *rexp,
+                                              int32_t M, int32_t accumulate, void *workspace, void *stream) {
+    return wgrad_h2_dual_impl(A0, lda0, G0, ldg0, W0, ldw0, K0, N0, rot0, A1, lda1, G1, ldg1, W1, ldw1, K1, N1, rot1, 1,
+                              plo, rexp, M, accumulate, workspace, stream);
 }
 
 extern "C" int msat_set_precision(int32_t mode) {

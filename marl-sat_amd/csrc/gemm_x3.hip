@@ -17,6 +17,7 @@
 // are too short to cover an HBM load issued one slab ahead).
 
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "split3.h"
@@ -397,21 +398,27 @@ gemm_x3r16_kernel(const float *__restrict__ A, int lda, const __bf16 *__restrict
 // bf16x3 body on the bf16x3 planes instead (same grid and LDS).
 constexpr int kDgW = 10;  // weight scale 2^10: |W| < 32 fits
 
-template <int RT, int NP, int NWV = 4>
-__device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int lda, const int *__restrict__ rexp,
+// PL: A is the GRU backward's packed rows as fp16x2 planes (gnn_kernels.hip, flags bit 3): row r at
+// A + r lda fp16 elements, hi there and lo plo elements further, both already at the row exponent -- the
+// fp16x2 body takes them as its MFMA operands as loaded (bit for bit the split it makes of fp32 rows);
+// the bf16x3 body rebuilds each element as (hi + lo) 2^-e (22 significant bits) before its split.
+template <int RT, int NP, int NWV = 4, bool PL = false>
+__device__ __forceinline__ void gemm_r16_body(const void *__restrict__ Av, int lda, const int *__restrict__ rexp,
                                               const uint16_t *__restrict__ Wp, float *__restrict__ C, int ldc,
                                               const float *__restrict__ bias, int M, int N, int K, int accumulate,
-                                              int m0, int n0, int vec_out, uint4 (*lds_w)[3][kX3M * 4], int kr = 0) {
+                                              int m0, int n0, int vec_out, uint4 (*lds_w)[3][kX3M * 4], int kr = 0,
+                                              int plo = 0) {
     typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
     const int t = threadIdx.x, w = t >> 6, lane = t & 63, l16 = lane & 15, g = lane >> 4;
     const int wr = w * 16 * RT;
-    const float *arow[RT];
-    int ea[RT];  // fp16x2: the scale exponent of this lane's activation row in each tile
+    constexpr int ESZ = PL ? 2 : 4;  // bytes per A element
+    const char *arow[RT];
+    int ea[RT];  // fp16x2 / planes: the scale exponent of this lane's activation row in each tile
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
         const int r = min(m0 + wr + 16 * i + l16, M - 1);
-        arow[i] = A + (size_t)r * lda + 8 * g;
-        if constexpr (NP == 2) {
+        arow[i] = reinterpret_cast<const char *>(Av) + ((size_t)r * lda + 8 * g) * ESZ;
+        if constexpr (NP == 2 || PL) {
             const int e = rexp[r];
             ea[i] = e == kExpZero ? 0 : e;
         }
@@ -445,11 +452,12 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
     // the bf16x3 body keeps one set (its split needs the registers)
     constexpr int PF = (NP == 2 && RT <= 2) ? 2 : 1;  // 256-row tiles: twice the MFMAs per step, one set ahead
     float4 ras[PF][RT][2];
-    auto loadA = [&](int d, float4 (&ra)[RT][2]) {
+    auto loadA = [&](int d, float4 (&ra)[RT][2]) {  // PL: [0] = 8 hi, [1] = 8 lo fp16 (bits)
 #pragma unroll
         for (int i = 0; i < RT; ++i)
 #pragma unroll
-            for (int e = 0; e < 2; ++e) ra[i][e] = *reinterpret_cast<const float4 *>(arow[i] + 32 * d + 4 * e);
+            for (int e = 0; e < 2; ++e)
+                ra[i][e] = *reinterpret_cast<const float4 *>(arow[i] + (PL ? (e * plo + 32 * d) * 2 : (32 * d + 4 * e) * 4));
     };
     const int slot = g ^ x3swz16((l16 >> 2) & 3);
     const int nd = K / 32;
@@ -467,10 +475,21 @@ __device__ __forceinline__ void gemm_r16_body(const float *__restrict__ A, int l
         uint4 fa[RT][NP];
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
-            if constexpr (NP == 3) {
+            if constexpr (NP == 3 && PL) {
+                const f16x8v hv = __builtin_bit_cast(f16x8v, ra[i][0]), lv = __builtin_bit_cast(f16x8v, ra[i][1]);
+                float x[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[j] = ldexpf((float)hv[j] + (float)lv[j], -ea[i]);
+                const Split8 sp = split8(make_float4(x[0], x[1], x[2], x[3]), make_float4(x[4], x[5], x[6], x[7]));
+#pragma unroll
+                for (int q = 0; q < 3; ++q) fa[i][q] = sp.p[q];
+            } else if constexpr (NP == 3) {
                 const Split8 sp = split8(ra[i][0], ra[i][1]);
 #pragma unroll
                 for (int q = 0; q < 3; ++q) fa[i][q] = sp.p[q];
+            } else if constexpr (PL) {
+                fa[i][0] = __builtin_bit_cast(uint4, ra[i][0]);
+                fa[i][1] = __builtin_bit_cast(uint4, ra[i][1]);
             } else {
                 const float4 u = ra[i][0], v = ra[i][1];
                 const int e = ea[i];
@@ -629,8 +648,8 @@ gemm_h2r16_kernel(const float *__restrict__ A, int lda, const int *__restrict__ 
 // 128-row block the n tiles of both products are consecutive workgroup ids, so the workgroups that read
 // the same rows of the packed buffer run together on one XCD and all but the first read them from L2.
 struct DgradProblem {
-    const float *A;
-    int lda;
+    const void *A;  // fp32 rows, or (planes launches) fp16x2 planes with the lo plane plo elements after hi
+    int lda, plo;
     const uint16_t *Wh2, *Wx3;
     const int *wbad;
     float *C;
@@ -638,7 +657,7 @@ struct DgradProblem {
     int kr;  // first double slab of the k walk (aligns the two products' reads of the shared rows)
 };
 
-template <int RT, int NWV = 4>
+template <int RT, int NWV = 4, bool PL = false>
 __global__ void __launch_bounds__(64 * NWV, NWV == 4 ? (RT == 2 ? 3 : 2) : 1)
 gemm_h2r16_dual_kernel(DgradProblem p0, DgradProblem p1, const int *__restrict__ rexp, int M, int K) {
     // the weight buffers, and the epilogue's per-wave stage (8 KiB per wave) in the same memory
@@ -652,11 +671,11 @@ gemm_h2r16_dual_kernel(DgradProblem p0, DgradProblem p1, const int *__restrict__
     const DgradProblem &p = first ? p0 : p1;
     const int n0 = (first ? sub : sub - p0.ntn) * kX3M;
     if (*p.wbad)
-        gemm_r16_body<RT, 3, NWV>(p.A, p.lda, nullptr, p.Wx3, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0,
-                                  p.vec_out, lds_w, p.kr);
+        gemm_r16_body<RT, 3, NWV, PL>(p.A, p.lda, PL ? rexp : nullptr, p.Wx3, p.C, p.ldc, nullptr, M, p.N, K,
+                                      p.accumulate, m0, n0, p.vec_out, lds_w, p.kr, p.plo);
     else
-        gemm_r16_body<RT, 2, NWV>(p.A, p.lda, rexp, p.Wh2, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0,
-                                  p.vec_out, lds_w, p.kr);
+        gemm_r16_body<RT, 2, NWV, PL>(p.A, p.lda, rexp, p.Wh2, p.C, p.ldc, nullptr, M, p.N, K, p.accumulate, m0, n0,
+                                      p.vec_out, lds_w, p.kr, p.plo);
 }
 
 // planes[q][r][c] = part q of 2^kDgW W[r][(c + rot) % cols] (fp16x2, q = 0, 1); *bad = 1 if a scaled
@@ -836,11 +855,14 @@ typedef unsigned short WwLds[2][12][kW3Plane];  // [buf][A planes | G planes]: 9
 
 // one workgroup's share: split sp (rows sp * rows_per_split ..), k tile k0; flag: this workgroup's
 // range flag (fp16x2), lds: the kernel's WwLds
-template <int NP, bool IL>
-__device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int lda, const float *__restrict__ G, int ldg,
+// PLG (the fixup of the planes launch, NP = 3 only): G is fp16x2 planes at the row exponents (ldg in fp16
+// elements, lo plane plo elements after hi), rebuilt per element as (hi + lo) 2^-e (22 significant bits).
+template <int NP, bool IL, bool PLG = false>
+__device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int lda, const void *__restrict__ Gv, int ldg,
                                              const int *__restrict__ rexp, float *__restrict__ part, int M, int K,
                                              int N, int rot, int rows_per_split, int sp, int k0, int *flag,
-                                             WwLds &ldsr) {
+                                             WwLds &ldsr, int plo = 0) {
+    static_assert(!PLG || NP == 3, "planes G: the bf16x3 fixup only");
     // [buf][A planes 0 .. NP-1 | G plane q, column block u at NP + 3 q + u]
     unsigned short (*lds)[4 * NP][kW3Plane] = reinterpret_cast<unsigned short (*)[4 * NP][kW3Plane]>(&ldsr[0][0][0]);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -870,11 +892,12 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
     const bool kok = k0 + sc < K;
     bool nok[3];
     const float *pa = A + (kok ? k0 + sc : 0);
-    const float *pg[3];
+    constexpr int GSZ = PLG ? 2 : 4;  // bytes per G element
+    const char *pg[3];
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
         nok[u] = sc + 128 * u < N;
-        pg[u] = G + (nok[u] ? sc + 128 * u : 0);
+        pg[u] = reinterpret_cast<const char *>(Gv) + (nok[u] ? sc + 128 * u : 0) * GSZ;
     }
     struct Stage {
         float4 a, g[3];
@@ -883,8 +906,20 @@ __device__ __forceinline__ void wgrad_w_body(const float *__restrict__ A, int ld
         const int m = rb + s * 16 + srow;
         const size_t mc = m < re ? m : re - 1;
         r.a = *reinterpret_cast<const float4 *>(pa + mc * lda);
+        if constexpr (PLG) {
+            typedef _Float16 f16x4g __attribute__((ext_vector_type(4)));
+            const int e = rexp[mc], es = e == kExpZero ? 0 : e;
 #pragma unroll
-        for (int u = 0; u < 3; ++u) r.g[u] = *reinterpret_cast<const float4 *>(pg[u] + mc * ldg);
+            for (int u = 0; u < 3; ++u) {
+                const f16x4g hv = *reinterpret_cast<const f16x4g *>(pg[u] + mc * ldg * 2);
+                const f16x4g lv = *reinterpret_cast<const f16x4g *>(pg[u] + (mc * ldg + plo) * 2);
+                r.g[u] = make_float4(ldexpf((float)hv[0] + (float)lv[0], -es), ldexpf((float)hv[1] + (float)lv[1], -es),
+                                     ldexpf((float)hv[2] + (float)lv[2], -es), ldexpf((float)hv[3] + (float)lv[3], -es));
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 3; ++u) r.g[u] = *reinterpret_cast<const float4 *>(pg[u] + mc * ldg * 4);
+        }
     };
     float amax = 0.f;  // fp16x2: largest |operand| staged by this thread (range check)
     const int off = w3off(srow, sc >> 3) + 8 * ((sc >> 2) & 1);
@@ -1052,16 +1087,16 @@ wgrad_w_kernel(const float *__restrict__ A, int lda, const float *__restrict__ G
 struct WgradProblem {
     const float *A;
     int lda;
-    const float *G;
+    const void *G;  // fp32 rows, or (planes launches) fp16x2 planes, ldg in fp16 elements
     int ldg;
     float *part;
     int K, N, rot, ktiles;
 };
 
-template <int NP>
+template <int NP, bool PLG = false>
 __global__ void __launch_bounds__(kWWT, 1)
 wgrad_w_dual_kernel(WgradProblem p0, WgradProblem p1, const int *__restrict__ rexp, int M, int rows_per_split,
-                    int *__restrict__ flags) {
+                    int *__restrict__ flags, int plo = 0) {
     __shared__ __attribute__((aligned(16))) WwLds lds;
     const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
     if (NP == 3 && flags[id] == 0) return;  // fixup launch: only the flagged workgroups
@@ -1069,8 +1104,222 @@ wgrad_w_dual_kernel(WgradProblem p0, WgradProblem p1, const int *__restrict__ re
     const bool first = sub < p0.ktiles;
     const WgradProblem &p = first ? p0 : p1;
     const int k0 = (first ? sub : sub - p0.ktiles) * kX3M;
-    wgrad_w_body<NP, true>(p.A, p.lda, p.G, p.ldg, rexp, p.part, M, p.K, p.N, p.rot, rows_per_split, sp, k0, flags + id,
-                           lds);
+    wgrad_w_body<NP, true, PLG>(p.A, p.lda, p.G, p.ldg, rexp, p.part, M, p.K, p.N, p.rot, rows_per_split, sp, k0,
+                                flags + id, lds, plo);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Planes weight gradient (msat_gemm_wgrad_h2_dual_planes): the same two products as wgrad_w_dual_kernel<2>
+// with G the GRU backward's packed rows as fp16x2 planes, each row already split at its own exponent e_r.
+// G is therefore staged with no vector work at all: LDS-DMA (global_load_lds_dwordx4) writes the planes
+// straight into the swizzled [16 rows][128 cols] images the transposed fragment reads expect (lane l of a
+// 1 KiB piece fetches the source chunk that w3off maps to position l).  The split-wide scale moves to A:
+// with ge the split's smallest row exponent, a' = a 2^(kPlA + ge - e_r) (range-checked as before) and
+// sum_r a'_r g'_r = 2^(ge + kPlA) sum_r a_r g_r, rescaled on store.  A's raw fp32 slabs arrive by
+// LDS-DMA too (ring of three), each thread splits its 4 elements from LDS into the A images, interleaved
+// with the previous slab's MFMAs.  Every global access in the k walk is an asm DMA, so its counted waits
+// (4 per wave and slab: 3 G pieces + 1 A piece) are exact.  Per slab and wave: 18 MFMAs, ~30 vector
+// instructions (the A split), against ~100 in wgrad_w_body<2> (A and G split per k tile).
+// Ring discipline at iteration s: DMA group s + 2 (G(s + 2) -> g[(s + 2) % 3], raw A(s + 3) -> raw[s % 3]) in
+// flight; MFMAs read a[s & 1], g[s % 3]; the split reads raw[(s + 1) % 3] into a[(s + 1) & 1]; the end waits for
+// group s + 1 (vmcnt 4) and a barrier.  Row deltas e_r - ge (capped at 63: with |a'| < 2^15 a larger shift
+// leaves a' below fp16's smallest subnormal either way) sit in LDS for the whole split (<= kPlRows rows).
+constexpr int kPlRows = 24576;  // rows per split the planes kernel's LDS delta table holds
+// A's headroom exponent in the planes kernel: a' = a 2^(kPlA + ge - e_r).  With G at full scale in every row, a
+// row whose G is 2^d below the split's largest carries a' = a 2^(kPlA - d); once a' is an fp16 subnormal its
+// absolute error (2^-25) multiplies a full-scale g (2^14): relative to the split's dominant term |a_0| 2^14 that
+// is 2^-(25 + kPlA) / |a_0| per such row (the fp32-row form's G-side scale: 2^-39 |a_r / a_0|).  kPlA = 0 failed
+// the 4e-6 bound at |a_0| < 2^-7 on rows spread over 43 binades (tests/test_planes_gpu.py); kPlA = 8 moves that to
+// |a_0| < 2^-15.  The price: the range check flags |a| >= 2^(15 - kPlA) = 128 in the split's largest rows (a
+// flagged workgroup is recomputed in bf16x3, correct either way).
+constexpr int kPlA = 8;
+
+struct WpLds {
+    unsigned short a[2][2][kW3Plane];  // A images (hi, lo) by slab parity: 16 KiB
+    unsigned short g[3][6][kW3Plane];  // G images [ring][q * 3 + u] (q: hi / lo, u: 128-column block): 72 KiB
+    float raw[3][16 * kX3M];           // raw fp32 A slabs: 24 KiB
+    unsigned char dl[kPlRows];         // e_r - ge per row of the split: 24 KiB
+    int red[8];
+};
+
+__device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int lda, const _Float16 *__restrict__ G,
+                                              int ldg, int plo, const int *__restrict__ rexp, float *__restrict__ part,
+                                              int M, int K, int N, int rot, int rows_per_split, int sp, int k0,
+                                              int *flag, WpLds &L) {
+    const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const int wk = (w & 1) * 64, wn = (w >> 1) * 96;
+    const int rb = sp * rows_per_split, re = min(M, rb + rows_per_split), nr = re - rb;
+    const int ns = (nr + 15) / 16;
+    // the split's smallest row exponent, then each row's delta
+    int mn = kExpZero;
+    for (int r = rb + t; r < re; r += kWWT) mn = min(mn, rexp[r]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mn = min(mn, __shfl_xor(mn, o, 64));
+    if (lane == 0) L.red[w] = mn;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kWWT / 64; ++i) mn = min(mn, L.red[i]);
+    const int ge = mn == kExpZero ? 0 : mn;
+    for (int r = t; r < nr; r += kWWT) {
+        const int e = rexp[rb + r];
+        L.dl[r] = (unsigned char)(e == kExpZero ? 0 : min(e - ge, 63));
+    }
+    f32x16v acc[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = f32x16v{};
+    // per-lane DMA pieces: G piece x = 3 w + e (plane block x >> 2 = q * 3 + u, rows 4 (x & 3) ..), raw A rows
+    // 2 w, 2 w + 1
+    int grow[3], gco[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        const int x = 3 * w + e, pb = x >> 2, row = 4 * (x & 3) + (lane >> 4);
+        const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        const int col = 128 * (pb % 3) + 8 * ch;
+        grow[e] = row;
+        gco[e] = (pb / 3) * plo + (col < N ? col : 0);
+    }
+    const int arow = 2 * w + (lane >> 5), kc = k0 + 4 * (lane & 31), aco = kc < K ? kc : 0;
+    // ring slots are compile-time (RA = k % 3 for G / raw A, the image k & 1): the k walk is unrolled by six, so
+    // every LDS address below is a per-lane constant plus an instruction offset
+    auto issue_a = [&](int k, auto RA) {  // raw A slab min(k, ns - 1) -> raw[RA], RA == k % 3
+        const int kk = min(k, ns - 1), lim = nr - 1 - 16 * kk;
+        const float *base = A + (size_t)(rb + 16 * kk) * lda;
+        glds16_async_s(base, (unsigned)((min(arow, lim) * lda + aco) * 4), &L.raw[decltype(RA)::value][w * 256]);
+    };
+    auto issue = [&](int k, auto RG) {  // group k: G(k) -> g[RG], raw A(k + 1); RG == k % 3
+        constexpr int rg = decltype(RG)::value;
+        const int kk = min(k, ns - 1), lim = nr - 1 - 16 * kk;
+        const _Float16 *base = G + (size_t)(rb + 16 * kk) * ldg;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+            const int x = 3 * w + e;
+            glds16_async_s(base, (unsigned)((min(grow[e], lim) * ldg + gco[e]) * 2), &L.g[rg][x >> 2][512 * (x & 3)]);
+        }
+        issue_a(k + 1, std::integral_constant<int, (rg + 1) % 3>{});
+    };
+    const int srow = t >> 5, sc = (t & 31) * 4;
+    const int off = w3off(srow, sc >> 3) + 8 * ((sc >> 2) & 1);
+    float amax = 0.f;
+    auto split_a = [&](int k, auto RK) {  // raw[k % 3] -> a[k & 1]; RK == k % 6
+        constexpr int rk = decltype(RK)::value;
+        const float4 v = *reinterpret_cast<const float4 *>(&L.raw[rk % 3][srow * kX3M + sc]);
+        const int rel = 16 * k + srow;
+        const int sh = kPlA - (int)L.dl[rel < kPlRows ? rel : 0];
+        // rows past the split are zeroed by a mask, not a branch (a branch would sink the LDS reads into it
+        // and out of the scheduling groups)
+        const unsigned keep = rel < nr ? 0xffffffffu : 0u;
+        auto z = [&](float f) { return __uint_as_float(__float_as_uint(ldexpf(f, sh)) & keep); };
+        const float4 x = make_float4(z(v.x), z(v.y), z(v.z), z(v.w));
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+        const SplitH4 xs = splith4(x);
+        *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(L.a[rk & 1][0]) + off) = xs.p[0];
+        *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(L.a[rk & 1][1]) + off) = xs.p[1];
+    };
+    const int h = lane >> 5, g = (lane >> 4) & 1;
+    auto slab = [&](auto RS) {  // RS == s % 6
+        constexpr int rs = decltype(RS)::value;
+        bf16x8 fa[2][2], fb[3][2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fa[i][q] = tr_frag(L.a[rs & 1][q], 8 * h, (wk + 32 * i + 16 * g) >> 3, lane);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int n = wn + 32 * j;
+                fb[j][q] = tr_frag(L.g[rs % 3][3 * q + (n >> 7)], 8 * h, ((n & 127) + 16 * g) >> 3, lane);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                typedef _Float16 f16x8w __attribute__((ext_vector_type(8)));
+                const f16x8w a0 = __builtin_bit_cast(f16x8w, fa[i][0]), a1 = __builtin_bit_cast(f16x8w, fa[i][1]);
+                const f16x8w b0 = __builtin_bit_cast(f16x8w, fb[j][0]), b1 = __builtin_bit_cast(f16x8w, fb[j][1]);
+                f32x16v c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, c, 0, 0, 0);  // h l
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, c, 0, 0, 0);  // l h
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, c, 0, 0, 0);  // h h
+                acc[i][j] = c;
+            }
+    };
+    __syncthreads();  // the delta table
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    auto iter = [&](int s, auto RS) {  // RS == s % 6
+        constexpr int rs = decltype(RS)::value;
+        issue(s + 2, std::integral_constant<int, (rs + 2) % 3>{});
+        __builtin_amdgcn_sched_barrier(0);
+        slab(RS);
+        // unconditional (one basic block for the scheduling groups): at s = ns - 1 it splits the clamped
+        // slab of the last group into the unused image, every row of it past the split (zeros)
+        split_a(s + 1, std::integral_constant<int, (rs + 1) % 6>{});
+        __builtin_amdgcn_sched_group_barrier(0x100, 22, 0);  // fragment reads + the raw A / delta reads
+#pragma unroll
+        for (int k = 0; k < 18; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // vector ALU
+            if (k == 9 || k == 13) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // A image store
+        }
+        wait_vmcnt<4>();  // group s + 1
+        barrier_lds();
+    };
+    if (ns > 0) {
+        issue_a(0, I0{});
+        issue(0, I0{});
+        issue(1, I1{});
+        wait_vmcnt<8>();  // raw A(0) (this wave's own rows)
+        split_a(0, I0{});
+        wait_vmcnt<4>();  // group 0
+        barrier_lds();
+        int s = 0;
+        for (; s + 6 <= ns; s += 6) {
+            iter(s, I0{});
+            iter(s + 1, I1{});
+            iter(s + 2, std::integral_constant<int, 2>{});
+            iter(s + 3, std::integral_constant<int, 3>{});
+            iter(s + 4, std::integral_constant<int, 4>{});
+            iter(s + 5, std::integral_constant<int, 5>{});
+        }
+        if (s < ns) iter(s, I0{});
+        if (s + 1 < ns) iter(s + 1, I1{});
+        if (s + 2 < ns) iter(s + 2, std::integral_constant<int, 2>{});
+        if (s + 3 < ns) iter(s + 3, std::integral_constant<int, 3>{});
+        if (s + 4 < ns) iter(s + 4, std::integral_constant<int, 4>{});
+        wait_vmcnt<0>();  // the last (clamped, unused) groups land before the workgroup's LDS is released
+    }
+    const int bad = __syncthreads_or(!(amax < 32768.0f));
+    if (t == 0) *flag = bad;
+    if (bad) return;
+    float *P = part + (size_t)sp * K * N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int n = wn + 32 * j + (lane & 31);
+            if (n >= N) continue;
+            const int oc = n + rot < N ? n + rot : n + rot - N;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = k0 + wk + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                if (row < K) P[(size_t)row * N + oc] = ldexpf(acc[i][j][reg], -(ge + kPlA));
+            }
+        }
+}
+
+__global__ void __launch_bounds__(kWWT, 1)
+wgrad_w_dual_pl_kernel(WgradProblem p0, WgradProblem p1, int plo, const int *__restrict__ rexp, int M,
+                       int rows_per_split, int *__restrict__ flags) {
+    __shared__ __attribute__((aligned(16))) WpLds lds;
+    const int id = xcd_remap_x3(blockIdx.x, gridDim.x);
+    const int T = p0.ktiles + p1.ktiles, sub = id % T, sp = id / T;
+    const bool first = sub < p0.ktiles;
+    const WgradProblem &p = first ? p0 : p1;
+    const int k0 = (first ? sub : sub - p0.ktiles) * kX3M;
+    wgrad_pl_body(p.A, p.lda, reinterpret_cast<const _Float16 *>(p.G), p.ldg, plo, rexp, p.part, M, p.K, p.N, p.rot,
+                  rows_per_split, sp, k0, flags + id, lds);
 }
 
 static bool a16x3(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -1150,9 +1399,29 @@ int msat_wgrad_x3w_launch(const float *A, int lda, const float *G, int ldg, floa
     return check_launch("wgrad_w_kernel<3> (bf16x3)");
 }
 
+// (at most kPlRows - 15 rows per split: the planes kernel's row-delta table)
 int msat_wgrad_dual_splits(int M, int K0, int K1) {
     const int T = (K0 + kX3M - 1) / kX3M + (K1 + kX3M - 1) / kX3M;
-    return std::max(1, std::min(std::max(1, 256 / T), (M + 511) / 512));
+    const int s = std::max(1, std::min(std::max(1, 256 / T), (M + 511) / 512));
+    return std::max(s, (M + kPlRows - 16) / (kPlRows - 15));
+}
+
+// the planes form (wgrad_w_dual_pl_kernel) + its bf16x3 fixup over the flagged workgroups; G0 / G1 fp16x2
+// planes (ldg in fp16 elements, lo plane plo elements after hi)
+int msat_wgrad_h2_dual_pl_launch(const float *A0, int lda0, const void *G0, int ldg0, float *part0, int K0, int N0,
+                                 int rot0, const float *A1, int lda1, const void *G1, int ldg1, float *part1, int K1,
+                                 int N1, int rot1, int plo, const int *rexp, int M, int splits, int *flags,
+                                 hipStream_t s) {
+    WgradProblem p0 = {A0, lda0, G0, ldg0, part0, K0, N0, rot0, (K0 + kX3M - 1) / kX3M};
+    WgradProblem p1 = {A1, lda1, G1, ldg1, part1, K1, N1, rot1, (K1 + kX3M - 1) / kX3M};
+    const int rows = (M + splits - 1) / splits, rows16 = ((rows + 15) / 16) * 16;
+    MSAT_REQUIRE(rows16 <= kPlRows, "wgrad planes: %d rows per split (at most %d)", rows16, kPlRows);
+    const dim3 grid(splits * (p0.ktiles + p1.ktiles));
+    hipLaunchKernelGGL(wgrad_w_dual_pl_kernel, grid, dim3(kWWT), 0, s, p0, p1, plo, rexp, M, rows16, flags);
+    const int rc = check_launch("wgrad_w_dual_pl_kernel (fp16x2 planes)");
+    if (rc) return rc;
+    hipLaunchKernelGGL((wgrad_w_dual_kernel<3, true>), grid, dim3(kWWT), 0, s, p0, p1, rexp, M, rows16, flags, plo);
+    return check_launch("wgrad_w_dual_kernel<3> (planes fixup)");
 }
 
 // both products of a cell (wgrad_w_dual_kernel, fp16x2) + the bf16x3 fixup over the flagged workgroups
@@ -1215,20 +1484,24 @@ extern "C" int msat_gemm_h2(const float *A, int32_t lda, const int32_t *rexp, co
 
 // C0 (+)= A0 @ W0^T and C1 (+)= A1 @ W1^T over the same M rows (one row-exponent array), in one launch
 // (gemm_h2r16_dual_kernel).  Conditions of msat_gemm_h2 for each product; no bias.
-extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h2, const void *W0_x3,
-                                 const int32_t *wbad0, float *C0, int32_t ldc0, int32_t N0, int32_t acc0,
-                                 const float *A1, int32_t lda1, const void *W1_h2, const void *W1_x3,
-                                 const int32_t *wbad1, float *C1, int32_t ldc1, int32_t N1, int32_t acc1,
-                                 const int32_t *rexp, int32_t M, int32_t K, void *stream) {
+// pl: A0 / A1 are fp16x2 planes (element size 2, lo plane plo elements after hi), else fp32 rows
+static int gemm_h2_dual_impl(const void *A0, int32_t lda0, const void *W0_h2, const void *W0_x3,
+                             const int32_t *wbad0, float *C0, int32_t ldc0, int32_t N0, int32_t acc0,
+                             const void *A1, int32_t lda1, const void *W1_h2, const void *W1_x3,
+                             const int32_t *wbad1, float *C1, int32_t ldc1, int32_t N1, int32_t acc1, int pl,
+                             int32_t plo, const int32_t *rexp, int32_t M, int32_t K, void *stream) {
     if (M == 0) return MSAT_OK;
     MSAT_REQUIRE(A0 && A1 && W0_h2 && W0_x3 && W1_h2 && W1_x3 && wbad0 && wbad1 && C0 && C1 && rexp && M > 0 &&
                      N0 > 0 && N1 > 0 && K > 0,
                  "bad gemm_h2_dual args");
-    MSAT_REQUIRE(K % 32 == 0 && lda0 % 4 == 0 && lda1 % 4 == 0 && lda0 >= K && lda1 >= K && ldc0 >= N0 && ldc1 >= N1 &&
-                     a16x3(A0) && a16x3(A1) && a16x3(W0_h2) && a16x3(W0_x3) && a16x3(W1_h2) && a16x3(W1_x3),
-                 "gemm_h2_dual: K %% 32, lda %% 4 and 16-byte aligned operands required");
+    const int la = pl ? 8 : 4;  // elements per 16 bytes
+    MSAT_REQUIRE(K % 32 == 0 && lda0 % la == 0 && lda1 % la == 0 && lda0 >= K && lda1 >= K && ldc0 >= N0 &&
+                     ldc1 >= N1 && a16x3(A0) && a16x3(A1) && a16x3(W0_h2) && a16x3(W0_x3) && a16x3(W1_h2) &&
+                     a16x3(W1_x3),
+                 "gemm_h2_dual: K %% 32, lda %% 4 (planes: %% 8) and 16-byte aligned operands required");
+    MSAT_REQUIRE(!pl || (plo % 8 == 0 && plo >= K), "gemm_h2_dual_planes: plo %% 8 and plo >= K required");
     DgradProblem p[2];
-    const float *As[2] = {A0, A1};
+    const void *As[2] = {A0, A1};
     const int ldas[2] = {lda0, lda1}, ldcs[2] = {ldc0, ldc1}, Ns[2] = {N0, N1}, accs[2] = {acc0, acc1};
     const void *W2[2] = {W0_h2, W1_h2}, *W3[2] = {W0_x3, W1_x3};
     const int32_t *wb[2] = {wbad0, wbad1};
@@ -1236,6 +1509,7 @@ extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h
     for (int i = 0; i < 2; ++i) {
         p[i].A = As[i];
         p[i].lda = ldas[i];
+        p[i].plo = pl ? plo : 0;
         p[i].Wh2 = reinterpret_cast<const uint16_t *>(W2[i]);
         p[i].Wx3 = reinterpret_cast<const uint16_t *>(W3[i]);
         p[i].wbad = wb[i];
@@ -1253,14 +1527,40 @@ extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h
     // row block fetch those bytes from HBM once (their walks are otherwise offset by H columns, which at
     // 96 resident workgroups per XCD and 2 KiB rows is enough to lose the L2 copy: 1.33x fetch, round 2).
     {
-        const long off = (long)(A0 - A1);
-        if (lda0 == lda1 && off > 0 && off % 32 == 0 && off / 32 < K / 32) p[1].kr = (int)(off / 32);
+        const long diff = (long)((const char *)A0 - (const char *)A1);
+        const long off = diff / (pl ? 2 : 4);  // in elements
+        if (lda0 == lda1 && diff % (pl ? 2 : 4) == 0 && off > 0 && off % 32 == 0 && off / 32 < K / 32)
+            p[1].kr = (int)(off / 32);
     }
     // 384-row workgroups of 12 waves (one per CU, three per SIMD as before): each weight slab fetched into
     // LDS serves 384 rows instead of 128, a third of the weight DMA pieces per output; bitwise the same
     // result as 128-row workgroups, 1-2 % faster (profiles/r04w_ab_dgrad_waves.log)
     const int ntm = (M + 383) / 384;
-    hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2, 12>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(768), 0,
-                       (hipStream_t)stream, p[0], p[1], rexp, M, K);
-    return check_launch("gemm_h2r16_dual_kernel");
+    if (pl)
+        hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2, 12, true>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(768), 0,
+                           (hipStream_t)stream, p[0], p[1], rexp, M, K);
+    else
+        hipLaunchKernelGGL((gemm_h2r16_dual_kernel<2, 12>), dim3(ntm * (p[0].ntn + p[1].ntn)), dim3(768), 0,
+                           (hipStream_t)stream, p[0], p[1], rexp, M, K);
+    return check_launch(pl ? "gemm_h2r16_dual_kernel (planes)" : "gemm_h2r16_dual_kernel");
+}
+
+extern "C" int msat_gemm_h2_dual(const float *A0, int32_t lda0, const void *W0_h2, const void *W0_x3,
+                                 const int32_t *wbad0, float *C0, int32_t ldc0, int32_t N0, int32_t acc0,
+                                 const float *A1, int32_t lda1, const void *W1_h2, const void *W1_x3,
+                                 const int32_t *wbad1, float *C1, int32_t ldc1, int32_t N1, int32_t acc1,
+                                 const int32_t *rexp, int32_t M, int32_t K, void *stream) {
+    return gemm_h2_dual_impl(A0, lda0, W0_h2, W0_x3, wbad0, C0, ldc0, N0, acc0, A1, lda1, W1_h2, W1_x3, wbad1, C1, ldc1,
+                             N1, acc1, 0, 0, rexp, M, K, stream);
+}
+
+// Same products with A0 / A1 the GRU backward's packed rows as fp16x2 planes (msat_gru_ln_bwd_g4fe, flags bit
+// 3): lda in fp16 elements (% 8), the lo plane plo elements after the hi plane, rows already at rexp's scale.
+extern "C" int msat_gemm_h2_dual_planes(const void *A0, int32_t lda0, const void *W0_h2, const void *W0_x3,
+                                        const int32_t *wbad0, float *C0, int32_t ldc0, int32_t N0, int32_t acc0,
+                                        const void *A1, int32_t lda1, const void *W1_h2, const void *W1_x3,
+                                        const int32_t *wbad1, float *C1, int32_t ldc1, int32_t N1, int32_t acc1,
+                                        int32_t plo, const int32_t *rexp, int32_t M, int32_t K, void *stream) {
+    return gemm_h2_dual_impl(A0, lda0, W0_h2, W0_x3, wbad0, C0, ldc0, N0, acc0, A1, lda1, W1_h2, W1_x3, wbad1, C1, ldc1,
+                             N1, acc1, 1, plo, rexp, M, K, stream);
 }

@@ -300,13 +300,39 @@ __device__ __forceinline__ void stv(float *__restrict__ p, const float *o) {
     }
 }
 
+// PL (flags bit 3): the packed row [dan | dar | daz | dan r] is written as fp16x2 planes at its row exponent
+// e (f16x2_row_exp; kExpZero -> 0): the row's 4H floats of buffer hold [hi (4H fp16) | lo (4H fp16)],
+// hi = fp16(x 2^e), lo = fp16(x 2^e - hi) -- bit for bit the split the fp16x2 data gradient makes of the fp32
+// row (gemm_x3.hip gemm_r16_body), done once here instead of once per consumer and k tile.  The weight
+// gradient then stages G with LDS-DMA and no vector work (wgrad_pl_body).
+__device__ __forceinline__ void put_h2(_Float16 *__restrict__ ph, int c, float v, int es, int lo_off) {
+    const float x = ldexpf(v, es);
+    const _Float16 h = (_Float16)x;
+    ph[c] = h;
+    ph[lo_off + c] = (_Float16)(x - (float)h);
+}
+
+template <int N>
+__device__ __forceinline__ void put_h2v(_Float16 *__restrict__ ph, int c, const float *v, int es, int lo_off) {
+    typedef _Float16 hv __attribute__((ext_vector_type(N)));
+    hv h, l;
+#pragma unroll
+    for (int u = 0; u < N; ++u) {
+        const float x = ldexpf(v[u], es);
+        h[u] = (_Float16)x;
+        l[u] = (_Float16)(x - (float)h[u]);
+    }
+    *reinterpret_cast<hv *>(ph + c) = h;
+    *reinterpret_cast<hv *>(ph + lo_off + c) = l;
+}
+
 // One row of the backward in the vector column layout (columns PER * lane + u); same arithmetic per
 // element as the scalar body of gru_ln_bwd_kernel below.  Row means multiply by 1 / H (exact: H is a
 // power of two, so x * 2^-k == x / 2^k bit for bit) instead of an IEEE division each: var cell -3..-8 %,
 // clause cell -2..-3 % (profiles/r03_ab_gru_bwd_recip.log; profiles/r03_ab_gru_bwd_modes.log, mode 0).  Measured there and not kept: the
 // forward's v_exp / v_rcp gate forms (clause cell +5 %: the transcendental unit, not the division
 // sequence, is the contended resource) and DPP wave reductions instead of the shuffles (neutral).
-template <int PER, int NQ, int NF, int NQT>
+template <int PER, int NQ, int NF, int NQT, bool PL>
 __device__ __forceinline__ void bwd_row_vec(const float *__restrict__ gi, const float *__restrict__ h,
                                             const float *__restrict__ g, const float *__restrict__ scale,
                                             float *__restrict__ di, float *__restrict__ dhh, float *__restrict__ dhp,
@@ -388,7 +414,9 @@ __device__ __forceinline__ void bwd_row_vec(const float *__restrict__ gi, const 
             pq[NQ + 3 * k + 2][u] += fw[k] * dan;
         }
     }
-    if (packed) {  // [dan | dar | daz | dan r]
+    if constexpr (PL) {
+        // stored below, once the row exponent is known
+    } else if (packed) {  // [dan | dar | daz | dan r]
         stv<PER>(di + j0, o_an);
         stv<PER>(di + H + j0, o_ar);
         stv<PER>(di + 2 * H + j0, o_az);
@@ -404,11 +432,20 @@ __device__ __forceinline__ void bwd_row_vec(const float *__restrict__ gi, const 
     stv<PER>(dhp + j0, o_dh);
     if (rexp_r) {
         rmax = wave_max_f32(rmax);
-        if (lane == 0) *rexp_r = f16x2_row_exp(rmax);
+        const int e = f16x2_row_exp(rmax);
+        if (lane == 0) *rexp_r = e;
+        if constexpr (PL) {
+            const int es = e == kExpZero ? 0 : e;
+            _Float16 *ph = reinterpret_cast<_Float16 *>(di);
+            put_h2v<PER>(ph, j0, o_an, es, 4 * H);
+            put_h2v<PER>(ph, H + j0, o_ar, es, 4 * H);
+            put_h2v<PER>(ph, 2 * H + j0, o_az, es, 4 * H);
+            put_h2v<PER>(ph, 3 * H + j0, o_anr, es, 4 * H);
+        }
     }
 }
 
-template <int PER, bool G4, int NQ = 2, int NF = 0, bool VEC = false>
+template <int PER, bool G4, int NQ = 2, int NF = 0, bool VEC = false, bool PL = false>
 __global__ void __launch_bounds__(kRowThreads, 1)
 gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict__ Gi, int ldi,
                   const float *__restrict__ Gh, int ldh, const float *__restrict__ hp, int ldp,
@@ -430,7 +467,7 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
         const float *g = dy + (size_t)r * ldy;
         if constexpr (VEC) {
             static_assert(G4, "vector form reads the packed tape");
-            bwd_row_vec<PER, NQ, NF, NQT>(gi, h, g, scale, dGi + (size_t)r * lddi, dGh + (size_t)r * lddh,
+            bwd_row_vec<PER, NQ, NF, NQT, PL>(gi, h, g, scale, dGi + (size_t)r * lddi, dGh + (size_t)r * lddh,
                                           dh + (size_t)r * lddh_prev, H, dh_assign, packed, feat + (size_t)r * ldf,
                                           rexp ? rexp + r : nullptr, lane, pq);
             continue;
@@ -484,6 +521,7 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
         a1 = wave_sum_f32(a1) * (1.0f / (float)H);
         a2 = wave_sum_f32(a2) * (1.0f / (float)H);
         float rmax = 0.f;  // largest |dG| of the row (rexp)
+        float o_an[PL ? PER : 1], o_ar[PL ? PER : 1], o_az[PL ? PER : 1], o_anr[PL ? PER : 1];  // PL: held
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int j = lane + 64 * u;
@@ -495,7 +533,12 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
             const float dar = dr * rg[u] * (1.0f - rg[u]);
             const float daz = dz * zg[u] * (1.0f - zg[u]);
             float *di = dGi + (size_t)r * lddi, *dhh = dGh + (size_t)r * lddh;
-            if (packed) {  // one row [dan | dar | daz | dan r]: dGi = cols 0..3H (gate order n, r, z), dGh = cols H..4H
+            if constexpr (PL) {
+                o_an[u] = dan;
+                o_ar[u] = dar;
+                o_az[u] = daz;
+                o_anr[u] = dan * rg[u];
+            } else if (packed) {  // one row [dan | dar | daz | dan r]: dGi = cols 0..3H (gate order n, r, z), dGh = cols H..4H
                 di[j] = dan;
                 di[H + j] = dar;
                 di[2 * H + j] = daz;
@@ -526,7 +569,20 @@ gru_ln_bwd_kernel(const float *__restrict__ dy, int ldy, const float *__restrict
         }
         if (rexp) {
             rmax = wave_max_f32(rmax);
-            if (lane == 0) rexp[r] = f16x2_row_exp(rmax);
+            const int e = f16x2_row_exp(rmax);
+            if (lane == 0) rexp[r] = e;
+            if constexpr (PL) {
+                const int es = e == kExpZero ? 0 : e;
+                _Float16 *ph = reinterpret_cast<_Float16 *>(dGi + (size_t)r * lddi);
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const int j = lane + 64 * u;
+                    put_h2(ph, j, o_an[u], es, 4 * H);
+                    put_h2(ph, H + j, o_ar[u], es, 4 * H);
+                    put_h2(ph, 2 * H + j, o_az[u], es, 4 * H);
+                    put_h2(ph, 3 * H + j, o_anr[u], es, 4 * H);
+                }
+            }
         }
     }
 #pragma unroll
@@ -990,9 +1046,13 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
     }
     const int dh_assign = (accumulate_ln >> 1) & 1;  // bit 1: dhprev = ..., else dhprev += ...
     const int packed = (accumulate_ln >> 2) & 1;     // bit 2: packed [dan | dar | daz | dan r] rows
+    const int planes = (accumulate_ln >> 3) & 1;     // bit 3: ... as fp16x2 planes at the row exponent
     accumulate_ln &= 1;
     MSAT_REQUIRE(!packed || (dGh == dGi + H && lddi == lddh && lddi >= 4 * H),
                  "gru_ln_bwd_g4: packed rows need dGh = dGi + H and a shared ld >= 4H");
+    MSAT_REQUIRE(!planes || (packed && rexp && bias && (nfeat == 2 || nfeat == 6)),
+                 "gru_ln_bwd_g4: fp16x2 planes (flags bit 3) need the packed rows, rexp, the bias outputs and 2 or 6 "
+                 "features");
     const int NQ = (bias ? 6 : 2) + 3 * nfeat;
     // vector column layout for the var cell (nfeat = 6) when every row start is PER-float aligned (H = 64
     // has PER = 1: same layout).  Measured on the uf50 training shapes (profiles/r02y_ab_bwd_vec.log):
@@ -1004,7 +1064,15 @@ static int gru_ln_bwd_g4_impl(const float *dy, int32_t ldy, const float *g4, int
                                                    (uintptr_t)dhprev) % va == 0 &&
                      (ldy | ldg | ldp | lddi | lddh | lddp) % vper == 0;
 #define MSAT_BWD1(PER, Q, F)                                                                                      \
-    if (vec)                                                                                                      \
+    if (planes && vec)                                                                                            \
+        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2 && F == 6, (Q == 6 && F > 0)>), g, b, 0, s,  \
+                           dy, ldy, g4, ldg, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp,       \
+                           partial, R, H, dh_assign, packed, feat, ldf, rexp, cap);                                   \
+    else if (planes)                                                                                              \
+        hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, false, (Q == 6 && F > 0)>), g, b, 0, s, dy, ldy, g4,  \
+                           ldg, g4, ldg, hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H,     \
+                           dh_assign, packed, feat, ldf, rexp, cap);                                                  \
+    else if (vec)                                                                                                 \
         hipLaunchKernelGGL((gru_ln_bwd_kernel<PER, true, Q, F, PER >= 2 && F == 6>), g, b, 0, s, dy, ldy, g4, ldg, g4, ldg, \
                            hprev, ldp, ln_scale, dGi, lddi, dGh, lddh, dhprev, lddp, partial, R, H, dh_assign,    \
                            packed, feat, ldf, rexp, cap);                                                              \

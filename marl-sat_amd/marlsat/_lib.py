@@ -131,6 +131,9 @@ def _load():
     sig["msat_gemm_h2_dual"] = (I, [P, I, P, P, P, P, I, I, I, P, I, P, P, P, P, I, I, I, P, I, I, P])
     sig["msat_gemm_wgrad_dual_workspace_bytes"] = (c_size_t, [I, I, I, I, I])
     sig["msat_gemm_wgrad_h2_dual"] = (I, [P, I, P, I, P, I, I, I, I, P, I, P, I, P, I, I, I, I, P, I, I, P, P])
+    sig["msat_gemm_h2_dual_planes"] = (I, [P, I, P, P, P, P, I, I, I, P, I, P, P, P, P, I, I, I, I, P, I, I, P])
+    sig["msat_gemm_wgrad_h2_dual_planes"] = (I, [P, I, P, I, P, I, I, I, I, P, I, P, I, P, I, I, I, I, I, P, I, I, P,
+                                                  P])
     sig["msat_clause_gather2"] = (I, [P, P, I, P, P, I, I, I, I, I, P])
     sig["msat_var_gather2"] = (I, [P, P, I, P, P, P, P, I, I, I, I, P])
     sig["msat_gru_ln_fwd"] = (I, [P, I, P, I, P, I, P, P, P, I, I, I, P])
@@ -230,6 +233,8 @@ EXPORTED = (
     "msat_gemm_h2_dual",
     "msat_gemm_wgrad_dual_workspace_bytes",
     "msat_gemm_wgrad_h2_dual",
+    "msat_gemm_h2_dual_planes",
+    "msat_gemm_wgrad_h2_dual_planes",
     "msat_clause_gather2",
     "msat_var_gather2",
     "msat_gru_ln_fwd",

@@ -199,28 +199,47 @@ class GNNActorCritic:
     # the fp16x2 path always takes them: -4 % against separate launches, round 2)
     use_dual = True
 
-    def _dgrad_dual(self, p0, p1, rexp, M, K):
+    # the packed backward rows as fp16x2 planes (gnn_kernels.hip flags bit 3): split once per row in the GRU
+    # backward instead of once per consumer and k tile; the dual products read the planes (round 5)
+    use_planes = os.environ.get("MARLSAT_PLANES", "1") != "0"
+
+    def _dgrad_dual(self, p0, p1, rexp, M, K, pbase=None):
         """p = (A, lda, fp16x2 planes, bf16x3 planes, wbad pointer, C, ldc, N, accumulate): both
-        C (+)= A @ W^T products over the same M rows (row exponents rexp) in one fp16x2 launch."""
+        C (+)= A @ W^T products over the same M rows (row exponents rexp) in one fp16x2 launch.  pbase: the
+        packed buffer's base when it holds fp16x2 planes (A pointers are then its fp32 column addresses)."""
         if M == 0:
             return
         fl = 2.0 * M * K * (p0[7] + p1[7])
         GNNActorCritic.flops += fl
         nb = 4.0 * M * (self._span(p0[0], p1[0], K, p0[1]) + p0[7] * (1 + p0[8]) + p1[7] * (1 + p1[8]) + 1)
+        if pbase is not None:  # fp32 column c of a packed row -> its hi-plane element c (same bytes per row)
+            pa = lambda p: pbase + (p[0] - pbase) // 2
+            self._timed("gemm_h2r16_kernel (dgrad, fp16x2 planes)", fl, lambda: _chk(L_.msat_gemm_h2_dual_planes(
+                pa(p0), 2 * p0[1], p0[2].data_ptr(), p0[3].data_ptr(), p0[4], p0[5], p0[6], p0[7], p0[8],
+                pa(p1), 2 * p1[1], p1[2].data_ptr(), p1[3].data_ptr(), p1[4], p1[5], p1[6], p1[7], p1[8],
+                p0[1], rexp.data_ptr(), M, K, self.stream), "msat_gemm_h2_dual_planes"), nb)
+            return
         self._timed("gemm_h2r16_kernel (dgrad, fp16x2)", fl, lambda: _chk(L_.msat_gemm_h2_dual(
             p0[0], p0[1], p0[2].data_ptr(), p0[3].data_ptr(), p0[4], p0[5], p0[6], p0[7], p0[8],
             p1[0], p1[1], p1[2].data_ptr(), p1[3].data_ptr(), p1[4], p1[5], p1[6], p1[7], p1[8],
             rexp.data_ptr(), M, K, self.stream), "msat_gemm_h2_dual"), nb)
 
-    def _wgrad_h2_dual(self, p0, p1, rexp, M, acc=1):
+    def _wgrad_h2_dual(self, p0, p1, rexp, M, acc=1, pbase=None):
         """p = (A, lda, G, ldg, W, ldw, K, N, rot): both W[:, (n + rot) % N] (+)= (A^T G)[:, n] over the same M
-        rows of G's buffer (row exponents rexp) in one fp16x2 launch."""
+        rows of G's buffer (row exponents rexp) in one fp16x2 launch.  pbase: as _dgrad_dual (G's buffer holds
+        fp16x2 planes)."""
         if M == 0:
             return
         fl = 2.0 * M * (p0[6] * p0[7] + p1[6] * p1[7])
         GNNActorCritic.flops += fl
         ws = self.scr.get_ws(int(L_.msat_gemm_wgrad_dual_workspace_bytes(M, p0[6], p0[7], p1[6], p1[7])))
         nb = 4.0 * M * (p0[6] + p1[6] + self._span(p0[2], p1[2], p0[7], p0[3]) + 1)  # A rows, G rows, rexp
+        if pbase is not None:
+            pg = lambda p: p[:2] + (pbase + (p[2] - pbase) // 2, 2 * p[3]) + p[4:]
+            self._timed("wgrad_w_dual_pl_kernel + fixup + reduce (fp16x2 planes)", fl, lambda: _chk(
+                L_.msat_gemm_wgrad_h2_dual_planes(*pg(p0), *pg(p1), p0[3], rexp.data_ptr(), M, acc, ws.data_ptr(),
+                                                  self.stream), "msat_gemm_wgrad_h2_dual_planes"), nb)
+            return
         self._timed("wgrad_w_kernel<2> + fixup + reduce (fp16x2)", fl, lambda: _chk(L_.msat_gemm_wgrad_h2_dual(
             *p0, *p1, rexp.data_ptr(), M, acc, ws.data_ptr(), self.stream), "msat_gemm_wgrad_h2_dual"), nb)
 
@@ -560,6 +579,9 @@ class GNNActorCritic:
         h2 = packed and self.use_wgrad_h2
         need_rexp = h2 or dh2
         dual = h2 and dh2 and self.use_dual
+        planes = dual and self.use_planes  # the packed rows as fp16x2 planes (read only by the dual products)
+        if planes:
+            flags |= 8
 
         def dF_wgrad(A, lda, dgi, ld, W, R, K, rexp):
             """W (dF rows, ld 3H) += A^T dGi; in packed rows dGi's gate blocks are (n | r z)."""
@@ -604,11 +626,14 @@ class GNNActorCritic:
                 sfx = cell[-2:]
                 fk = "Fp" if half == 0 else "Fn"
                 if dual:  # dh and d(gathered) in one launch, dWh and dF in another (same packed rows)
+                    pb = dgi if planes else None
                     self._dgrad_dual((dgh, ldd, pl2["wh_" + sfx], pl["wh_" + sfx], wbad["wh_" + sfx], dHx0.data_ptr(),
                                       H, H, 1),
-                                     (dgi, ldd, pl2[fk], pl[fk], wbad[fk], pp(dNV, half * H), 2 * H, H, 0), rexp, Nv, W3)
+                                     (dgi, ldd, pl2[fk], pl[fk], wbad[fk], pp(dNV, half * H), 2 * H, H, 0), rexp, Nv, W3,
+                                     pbase=pb)
                     self._wgrad_h2_dual((Hx.data_ptr(), H, dgh, ldd, gwh.data_ptr(), W3, H, W3, 0),
-                                        (pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), W3, H, W3, 2 * H), rexp, Nv)
+                                        (pp(t.NV, half * H), 2 * H, dgi, ldd, gF.data_ptr(), W3, H, W3, 2 * H), rexp, Nv,
+                                        pbase=pb)
                 else:
                     self._dgrad(dgh, ldd, wh, pl["wh_" + sfx], dHx0.data_ptr(), H, Nv, H, W3, 1, hx("wh_" + sfx, rexp))
                     Wh_wgrad(Hx.data_ptr(), dgh, ldd, gwh.data_ptr(), Nv, rexp)
@@ -628,11 +653,13 @@ class GNNActorCritic:
                 pp(gFc[2 * H]), part, Nc, rexp)
             dGIN = e(Nc, 2 * H)
             if dual:
+                pb = dgi if planes else None
                 self._dgrad_dual((dgh, ldd, pl2["wh_c"], pl["wh_c"], wbad["wh_c"], dHc0.data_ptr(), H, H, 1),
                                  (dgi, ldd, pl2["Fc"], pl["Fc"], wbad["Fc"], dGIN.data_ptr(), 2 * H, 2 * H, 0), rexp, Nc,
-                                 W3)
+                                 W3, pbase=pb)
                 self._wgrad_h2_dual((t.Hc.data_ptr(), H, dgh, ldd, self.g("enc.gru_c_wh").data_ptr(), W3, H, W3, 0),
-                                    (t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), W3, 2 * H, W3, 2 * H), rexp, Nc)
+                                    (t.GIN.data_ptr(), 2 * H, dgi, ldd, gFc.data_ptr(), W3, 2 * H, W3, 2 * H), rexp, Nc,
+                                    pbase=pb)
             else:
                 self._dgrad(dgh, ldd, self.p("enc.gru_c_wh"), pl["wh_c"], dHc0.data_ptr(), H, Nc, H, W3, 1,
                             hx("wh_c", rexp))

@@ -28,6 +28,9 @@ ROCPROF_NAMES = {  # bench label -> rocprof kernel names whose launches the benc
     "wgrad_w_kernel<2> + fixup + reduce (fp16x2)": ["wgrad_w_dual_kernel<2", "wgrad_w_dual_kernel<3",
                                                     "wgrad_reduce4_kernel"],
     "gemm_h2r16_kernel (dgrad, fp16x2)": ["gemm_h2r16_dual_kernel"],
+    "gemm_h2r16_kernel (dgrad, fp16x2 planes)": ["gemm_h2r16_dual_kernel"],
+    "wgrad_w_dual_pl_kernel + fixup + reduce (fp16x2 planes)": ["wgrad_w_dual_pl_kernel", "wgrad_w_dual_kernel<3",
+                                                                 "wgrad_reduce4_kernel"],
 }
 launches = {}
 for r in csv.DictReader(open(trace)):
