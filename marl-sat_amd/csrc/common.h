@@ -154,6 +154,17 @@ __device__ __forceinline__ void glds16_async_s2(const void *sbase0, const void *
         : "memory");
 }
 
+// 4 bytes per lane (global_load_lds_dword): LDS at the wave-uniform byte address `lds` + 4 * lane, saddr form.
+__device__ __forceinline__ void glds4_async_s(const void *sbase, unsigned voff, const void *lds) {
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(dst)
+        : "memory");
+}
+
 // s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory operations are done.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

@@ -1115,30 +1115,35 @@ wgrad_w_dual_kernel(WgradProblem p0, WgradProblem p1, const int *__restrict__ re
 // straight into the swizzled [16 rows][128 cols] images the transposed fragment reads expect (lane l of a
 // 1 KiB piece fetches the source chunk that w3off maps to position l).  The split-wide scale moves to A:
 // with ge the split's smallest row exponent, a' = a 2^(kPlA + ge - e_r) (range-checked as before) and
-// sum_r a'_r g'_r = 2^(ge + kPlA) sum_r a_r g_r, rescaled on store.  A's raw fp32 slabs arrive by
-// LDS-DMA too (ring of three), each thread splits its 4 elements from LDS into the A images, interleaved
-// with the previous slab's MFMAs.  Every global access in the k walk is an asm DMA, so its counted waits
-// (4 per wave and slab: 3 G pieces + 1 A piece) are exact.  Per slab and wave: 18 MFMAs, ~30 vector
-// instructions (the A split), against ~100 in wgrad_w_body<2> (A and G split per k tile).
-// Ring discipline at iteration s: DMA group s + 2 (G(s + 2) -> g[(s + 2) % 3], raw A(s + 3) -> raw[s % 3]) in
-// flight; MFMAs read a[s & 1], g[s % 3]; the split reads raw[(s + 1) % 3] into a[(s + 1) & 1]; the end waits for
-// group s + 1 (vmcnt 4) and a barrier.  Row deltas e_r - ge (capped at 63: with |a'| < 2^15 a larger shift
-// leaves a' below fp16's smallest subnormal either way) sit in LDS for the whole split (<= kPlRows rows).
-constexpr int kPlRows = 24576;  // rows per split the planes kernel's LDS delta table holds
-// A's headroom exponent in the planes kernel: a' = a 2^(kPlA + ge - e_r).  With G at full scale in every row, a
-// row whose G is 2^d below the split's largest carries a' = a 2^(kPlA - d); once a' is an fp16 subnormal its
-// absolute error (2^-25) multiplies a full-scale g (2^14): relative to the split's dominant term |a_0| 2^14 that
-// is 2^-(25 + kPlA) / |a_0| per such row (the fp32-row form's G-side scale: 2^-39 |a_r / a_0|).  kPlA = 0 failed
-// the 4e-6 bound at |a_0| < 2^-7 on rows spread over 43 binades (tests/test_planes_gpu.py); kPlA = 8 moves that to
-// |a_0| < 2^-15.  The price: the range check flags |a| >= 2^(15 - kPlA) = 128 in the split's largest rows (a
-// flagged workgroup is recomputed in bf16x3, correct either way).
+// sum_r a'_r g'_r = 2^(ge + kPlA) sum_r a_r g_r, rescaled on store.  A's raw fp32 slabs and the slab's row
+// exponents arrive by LDS-DMA too; each thread splits its 4 A elements from LDS into the A images.  Every global
+// access in the k walk is an asm DMA, so its counted waits (5 per wave and slab: 3 G pieces, 1 A piece, 1 row-
+// exponent piece) are exact.  Per slab and wave: 18 MFMAs, ~45 vector instructions (the A split and the DMA
+// offsets), against ~100 in wgrad_w_body<2> (A and G split per k tile).  Each slab's fragments are read one
+// iteration ahead into registers, so its MFMAs start right after the barrier and the next slab's LDS reads run
+// under them; three DMA groups (96 KiB) are in flight per CU (the ring discipline is at `iter` below).
+//
+// A's headroom exponent kPlA: with G at full scale in every row, a row whose G is 2^d below the split's largest
+// carries a' = a 2^(kPlA - d); once a' is an fp16 subnormal its absolute error (2^-25) multiplies a full-scale g
+// (2^14): relative to the split's dominant term |a_0| 2^14 that is 2^-(25 + kPlA) / |a_0| per such row (the
+// fp32-row form's G-side scale: 2^-39 |a_r / a_0|).  kPlA = 0 failed the 4e-6 bound at |a_0| < 2^-7 on rows
+// spread over 43 binades (tests/test_planes_gpu.py); kPlA = 8 moves that to |a_0| < 2^-15.  The price: the range
+// check flags |a| >= 2^(15 - kPlA) = 128 in the split's largest rows (a flagged workgroup is recomputed in bf16x3,
+// correct either way).  Shifts are capped at 63 (with |a'| < 2^15 a larger one leaves a' below fp16's smallest
+// subnormal either way); an all-zero G row (kExpZero) leaves its a unscaled (the product is zero).
 constexpr int kPlA = 8;
+// Ablation builds only (make ab AB_FLAGS=-DMSAT_WGRAD_ABL=n, timing diagnostics, wrong results): bit 0 drops the
+// MFMAs, bit 1 the fragment reads, bit 2 the DMAs, bit 3 the A split.  0 in every product build.
+#ifndef MSAT_WGRAD_ABL
+#define MSAT_WGRAD_ABL 0
+#endif
+constexpr int kPlSlots = 4;  // G / raw A / row-exponent ring depth: 3 groups in flight + the slab being read
 
 struct WpLds {
-    unsigned short a[2][2][kW3Plane];  // A images (hi, lo) by slab parity: 16 KiB
-    unsigned short g[3][6][kW3Plane];  // G images [ring][q * 3 + u] (q: hi / lo, u: 128-column block): 72 KiB
-    float raw[3][16 * kX3M];           // raw fp32 A slabs: 24 KiB
-    unsigned char dl[kPlRows];         // e_r - ge per row of the split: 24 KiB
+    unsigned short a[2][2][kW3Plane];         // A images (hi, lo) by slab parity: 16 KiB
+    unsigned short g[kPlSlots][6][kW3Plane];  // G images [slot][q * 3 + u] (q: hi / lo, u: 128-column block): 96 KiB
+    float raw[kPlSlots][16 * kX3M];           // raw fp32 A slabs: 32 KiB
+    int rx[kPlSlots][8][64];                  // per wave: its two rows' exponents, lane l -> row 2 w + (l & 1)
     int red[8];
 };
 
@@ -1150,7 +1155,7 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
     const int wk = (w & 1) * 64, wn = (w >> 1) * 96;
     const int rb = sp * rows_per_split, re = min(M, rb + rows_per_split), nr = re - rb;
     const int ns = (nr + 15) / 16;
-    // the split's smallest row exponent, then each row's delta
+    // the split's smallest row exponent
     int mn = kExpZero;
     for (int r = rb + t; r < re; r += kWWT) mn = min(mn, rexp[r]);
 #pragma unroll
@@ -1160,56 +1165,64 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
 #pragma unroll
     for (int i = 0; i < kWWT / 64; ++i) mn = min(mn, L.red[i]);
     const int ge = mn == kExpZero ? 0 : mn;
-    for (int r = t; r < nr; r += kWWT) {
-        const int e = rexp[rb + r];
-        L.dl[r] = (unsigned char)(e == kExpZero ? 0 : min(e - ge, 63));
-    }
     f32x16v acc[2][3];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[i][j] = f32x16v{};
     // per-lane DMA pieces: G piece x = 3 w + e (plane block x >> 2 = q * 3 + u, rows 4 (x & 3) ..), raw A rows
-    // 2 w, 2 w + 1
-    int grow[3], gco[3];
+    // 2 w, 2 w + 1, row exponents of rows 2 w + (lane & 1)
+    int grow[3];
+    unsigned goff[3], gcb[3];
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
         const int x = 3 * w + e, pb = x >> 2, row = 4 * (x & 3) + (lane >> 4);
         const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
         const int col = 128 * (pb % 3) + 8 * ch;
+        const int gco = (pb / 3) * plo + (col < N ? col : 0);
         grow[e] = row;
-        gco[e] = (pb / 3) * plo + (col < N ? col : 0);
+        goff[e] = (unsigned)((row * ldg + gco) * 2);  // a slab's last valid row lim clamps: min(off(row), off(lim))
+        gcb[e] = (unsigned)(gco * 2);
     }
     const int arow = 2 * w + (lane >> 5), kc = k0 + 4 * (lane & 31), aco = kc < K ? kc : 0;
-    // ring slots are compile-time (RA = k % 3 for G / raw A, the image k & 1): the k walk is unrolled by six, so
-    // every LDS address below is a per-lane constant plus an instruction offset
-    auto issue_a = [&](int k, auto RA) {  // raw A slab min(k, ns - 1) -> raw[RA], RA == k % 3
+    const unsigned aoff = (unsigned)((arow * lda + aco) * 4), acb = (unsigned)(aco * 4);
+    const int xrow = 2 * w + (lane & 1);
+    // slots are compile-time: the k walk is unrolled by four (kPlSlots, a multiple of the two A images)
+    auto issue_a = [&](int k, auto RA) {  // raw A slab + row exponents of min(k, ns - 1) -> slot RA == k % 4
+        constexpr int ra = decltype(RA)::value;
+        if constexpr ((MSAT_WGRAD_ABL & 4) != 0) return;
         const int kk = min(k, ns - 1), lim = nr - 1 - 16 * kk;
-        const float *base = A + (size_t)(rb + 16 * kk) * lda;
-        glds16_async_s(base, (unsigned)((min(arow, lim) * lda + aco) * 4), &L.raw[decltype(RA)::value][w * 256]);
+        MSAT_DCHECK(rb + 16 * kk + min(arow, lim), M);  // debug: the clamped source row
+        glds16_async_s(A + (size_t)(rb + 16 * kk) * lda, min(aoff, (unsigned)(lim * lda * 4) + acb),
+                       &L.raw[ra][w * 256]);
+        glds4_async_s(rexp + rb + 16 * kk, (unsigned)(min(xrow, lim) * 4), &L.rx[ra][w][0]);
     };
-    auto issue = [&](int k, auto RG) {  // group k: G(k) -> g[RG], raw A(k + 1); RG == k % 3
+    auto issue = [&](int k, auto RG) {  // group k: G(k) -> g[RG], raw A(k + 1); RG == k % 4
         constexpr int rg = decltype(RG)::value;
+        if constexpr ((MSAT_WGRAD_ABL & 4) != 0) return;
         const int kk = min(k, ns - 1), lim = nr - 1 - 16 * kk;
         const _Float16 *base = G + (size_t)(rb + 16 * kk) * ldg;
+        const unsigned lb = (unsigned)(lim * ldg * 2);
 #pragma unroll
         for (int e = 0; e < 3; ++e) {
             const int x = 3 * w + e;
-            glds16_async_s(base, (unsigned)((min(grow[e], lim) * ldg + gco[e]) * 2), &L.g[rg][x >> 2][512 * (x & 3)]);
+            MSAT_DCHECK(rb + 16 * kk + min(grow[e], lim), M);  // debug: the clamped source row
+            glds16_async_s(base, min(goff[e], lb + gcb[e]), &L.g[rg][x >> 2][512 * (x & 3)]);
         }
-        issue_a(k + 1, std::integral_constant<int, (rg + 1) % 3>{});
+        issue_a(k + 1, std::integral_constant<int, (rg + 1) % kPlSlots>{});
     };
     const int srow = t >> 5, sc = (t & 31) * 4;
     const int off = w3off(srow, sc >> 3) + 8 * ((sc >> 2) & 1);
     float amax = 0.f;
-    auto split_a = [&](int k, auto RK) {  // raw[k % 3] -> a[k & 1]; RK == k % 6
+    auto split_a = [&](int k, auto RK) {  // raw[k % 4] -> a[k & 1]; RK == k % 4
         constexpr int rk = decltype(RK)::value;
-        const float4 v = *reinterpret_cast<const float4 *>(&L.raw[rk % 3][srow * kX3M + sc]);
-        const int rel = 16 * k + srow;
-        const int sh = kPlA - (int)L.dl[rel < kPlRows ? rel : 0];
+        if constexpr ((MSAT_WGRAD_ABL & 8) != 0) return;
+        const float4 v = *reinterpret_cast<const float4 *>(&L.raw[rk][srow * kX3M + sc]);
+        const int e = L.rx[rk][w][srow & 1];
+        const int sh = e == kExpZero ? 0 : kPlA - min(e - ge, 63);
         // rows past the split are zeroed by a mask, not a branch (a branch would sink the LDS reads into it
         // and out of the scheduling groups)
-        const unsigned keep = rel < nr ? 0xffffffffu : 0u;
+        const unsigned keep = 16 * k + srow < nr ? 0xffffffffu : 0u;
         auto z = [&](float f) { return __uint_as_float(__float_as_uint(ldexpf(f, sh)) & keep); };
         const float4 x = make_float4(z(v.x), z(v.y), z(v.z), z(v.w));
         amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
@@ -1218,26 +1231,42 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
         *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(L.a[rk & 1][1]) + off) = xs.p[1];
     };
     const int h = lane >> 5, g = (lane >> 4) & 1;
-    auto slab = [&](auto RS) {  // RS == s % 6
+    struct Frags {
+        bf16x8 fa[2][2], fb[3][2];  // [tile][hi, lo]
+    };
+    auto read_frags = [&](Frags &F, auto RS, bool first = false) {  // the slab's A image and G slot, RS == slab % 4
         constexpr int rs = decltype(RS)::value;
-        bf16x8 fa[2][2], fb[3][2];
+        if ((MSAT_WGRAD_ABL & 2) != 0 && !first) return;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) fa[i][q] = tr_frag(L.a[rs & 1][q], 8 * h, (wk + 32 * i + 16 * g) >> 3, lane);
+            for (int i = 0; i < 2; ++i) F.fa[i][q] = tr_frag(L.a[rs & 1][q], 8 * h, (wk + 32 * i + 16 * g) >> 3, lane);
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 const int n = wn + 32 * j;
-                fb[j][q] = tr_frag(L.g[rs % 3][3 * q + (n >> 7)], 8 * h, ((n & 127) + 16 * g) >> 3, lane);
+                F.fb[j][q] = tr_frag(L.g[rs][3 * q + (n >> 7)], 8 * h, ((n & 127) + 16 * g) >> 3, lane);
             }
+        }
+    };
+    auto mfmas = [&](const Frags &F) {
+        if constexpr ((MSAT_WGRAD_ABL & 1) != 0) {  // keep the fragment reads alive: one add per fragment
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) acc[i][0][q] += __builtin_bit_cast(float4, F.fa[i][q]).x;
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) acc[1][j][4 + q] += __builtin_bit_cast(float4, F.fb[j][q]).x;
+            return;
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 typedef _Float16 f16x8w __attribute__((ext_vector_type(8)));
-                const f16x8w a0 = __builtin_bit_cast(f16x8w, fa[i][0]), a1 = __builtin_bit_cast(f16x8w, fa[i][1]);
-                const f16x8w b0 = __builtin_bit_cast(f16x8w, fb[j][0]), b1 = __builtin_bit_cast(f16x8w, fb[j][1]);
+                const f16x8w a0 = __builtin_bit_cast(f16x8w, F.fa[i][0]), a1 = __builtin_bit_cast(f16x8w, F.fa[i][1]);
+                const f16x8w b0 = __builtin_bit_cast(f16x8w, F.fb[j][0]), b1 = __builtin_bit_cast(f16x8w, F.fb[j][1]);
                 f32x16v c = acc[i][j];
                 c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, c, 0, 0, 0);  // h l
                 c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, c, 0, 0, 0);  // l h
@@ -1245,51 +1274,67 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
                 acc[i][j] = c;
             }
     };
-    __syncthreads();  // the delta table
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
-    auto iter = [&](int s, auto RS) {  // RS == s % 6
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    // Iteration s (RS == s % 4): slab s's fragments are already in registers (Fc, read during iteration s - 1), so
+    // its MFMAs start at once; slab s + 1's fragment reads (Fn) run under them, as does the split of raw A(s + 2)
+    // into image (s + 2) & 1 == s & 1 (slab s's image, read out during s - 1).  DMA group s + 4 (5 per wave) goes
+    // into G slot s % 4 (read out during s - 1) and raw / exponent slot (s + 5) % 4 (split during s - 1).  The end
+    // waits for group s + 2 (vmcnt 10: groups s + 3 and s + 4 may fly) and a barrier: iteration s + 1 reads slab
+    // s + 2's fragments from G(s + 2) and the image written here, and splits raw A(s + 3) (group s + 2).
+    auto iter = [&](int s, auto RS, const Frags &Fc, Frags &Fn) {
         constexpr int rs = decltype(RS)::value;
-        issue(s + 2, std::integral_constant<int, (rs + 2) % 3>{});
+        issue(s + 4, RS);
         __builtin_amdgcn_sched_barrier(0);
-        slab(RS);
-        // unconditional (one basic block for the scheduling groups): at s = ns - 1 it splits the clamped
-        // slab of the last group into the unused image, every row of it past the split (zeros)
-        split_a(s + 1, std::integral_constant<int, (rs + 1) % 6>{});
-        __builtin_amdgcn_sched_group_barrier(0x100, 22, 0);  // fragment reads + the raw A / delta reads
+        mfmas(Fc);
+        read_frags(Fn, std::integral_constant<int, (rs + 1) % kPlSlots>{});
+        // unconditional (one basic block for the scheduling groups): near the end it splits clamped slabs into
+        // the unused image, every row of them past the split (zeros)
+        split_a(s + 2, std::integral_constant<int, (rs + 2) % kPlSlots>{});
 #pragma unroll
         for (int k = 0; k < 18; ++k) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+            if (k < 11) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // fragment / raw A / exponent reads
             __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // vector ALU
-            if (k == 9 || k == 13) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // A image store
+            if (k == 13 || k == 15) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // A image store
         }
-        wait_vmcnt<4>();  // group s + 1
+        wait_vmcnt<10>();  // group s + 2
         barrier_lds();
     };
     if (ns > 0) {
+        Frags F0, F1;
         issue_a(0, I0{});
         issue(0, I0{});
         issue(1, I1{});
-        wait_vmcnt<8>();  // raw A(0) (this wave's own rows)
+        issue(2, I2{});
+        wait_vmcnt<15>();  // raw A(0) + exponents (this wave's own rows)
         split_a(0, I0{});
-        wait_vmcnt<4>();  // group 0
+        // this wave's reads of slot 0 are done before group 3 refills it with raw A(4) (each wave reads only the
+        // rows its own DMA pieces write)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(3, I3{});
+        wait_vmcnt<15>();  // group 0: G(0), raw A(1)
+        split_a(1, I1{});
+        wait_vmcnt<10>();  // group 1: G(1), raw A(2)
         barrier_lds();
+        read_frags(F0, I0{}, true);
+        if ((MSAT_WGRAD_ABL & 2) != 0) F1 = F0;
+        barrier_lds();  // every wave's slab-0 reads are done before group 4 refills G slot 0
         int s = 0;
-        for (; s + 6 <= ns; s += 6) {
-            iter(s, I0{});
-            iter(s + 1, I1{});
-            iter(s + 2, std::integral_constant<int, 2>{});
-            iter(s + 3, std::integral_constant<int, 3>{});
-            iter(s + 4, std::integral_constant<int, 4>{});
-            iter(s + 5, std::integral_constant<int, 5>{});
+        for (; s + 4 <= ns; s += 4) {
+            iter(s, I0{}, F0, F1);
+            iter(s + 1, I1{}, F1, F0);
+            iter(s + 2, I2{}, F0, F1);
+            iter(s + 3, I3{}, F1, F0);
         }
-        if (s < ns) iter(s, I0{});
-        if (s + 1 < ns) iter(s + 1, I1{});
-        if (s + 2 < ns) iter(s + 2, std::integral_constant<int, 2>{});
-        if (s + 3 < ns) iter(s + 3, std::integral_constant<int, 3>{});
-        if (s + 4 < ns) iter(s + 4, std::integral_constant<int, 4>{});
+        if (s < ns) iter(s, I0{}, F0, F1);
+        if (s + 1 < ns) iter(s + 1, I1{}, F1, F0);
+        if (s + 2 < ns) iter(s + 2, I2{}, F0, F1);
         wait_vmcnt<0>();  // the last (clamped, unused) groups land before the workgroup's LDS is released
     }
+    if (MSAT_WGRAD_ABL) amax = 0.f;  // ablation builds: never the fixup (its time is not the kernel's)
     const int bad = __syncthreads_or(!(amax < 32768.0f));
     if (t == 0) *flag = bad;
     if (bad) return;
@@ -1399,11 +1444,9 @@ int msat_wgrad_x3w_launch(const float *A, int lda, const float *G, int ldg, floa
     return check_launch("wgrad_w_kernel<3> (bf16x3)");
 }
 
-// (at most kPlRows - 15 rows per split: the planes kernel's row-delta table)
 int msat_wgrad_dual_splits(int M, int K0, int K1) {
     const int T = (K0 + kX3M - 1) / kX3M + (K1 + kX3M - 1) / kX3M;
-    const int s = std::max(1, std::min(std::max(1, 256 / T), (M + 511) / 512));
-    return std::max(s, (M + kPlRows - 16) / (kPlRows - 15));
+    return std::max(1, std::min(std::max(1, 256 / T), (M + 511) / 512));
 }
 
 // the planes form (wgrad_w_dual_pl_kernel) + its bf16x3 fixup over the flagged workgroups; G0 / G1 fp16x2
@@ -1415,7 +1458,6 @@ int msat_wgrad_h2_dual_pl_launch(const float *A0, int lda0, const void *G0, int 
     WgradProblem p0 = {A0, lda0, G0, ldg0, part0, K0, N0, rot0, (K0 + kX3M - 1) / kX3M};
     WgradProblem p1 = {A1, lda1, G1, ldg1, part1, K1, N1, rot1, (K1 + kX3M - 1) / kX3M};
     const int rows = (M + splits - 1) / splits, rows16 = ((rows + 15) / 16) * 16;
-    MSAT_REQUIRE(rows16 <= kPlRows, "wgrad planes: %d rows per split (at most %d)", rows16, kPlRows);
     const dim3 grid(splits * (p0.ktiles + p1.ktiles));
     hipLaunchKernelGGL(wgrad_w_dual_pl_kernel, grid, dim3(kWWT), 0, s, p0, p1, plo, rexp, M, rows16, flags);
     const int rc = check_launch("wgrad_w_dual_pl_kernel (fp16x2 planes)");

@@ -9,8 +9,8 @@ its row exponent instead of fp32.  Pinned here:
     and its bf16x3 body (an overflowing weight split) stays inside the fp32 bound;
   * msat_gemm_wgrad_h2_dual_planes (G by LDS-DMA, the split-wide scale moved to A) against fp64 at the bound of
     the fp32-row form (rtol 4e-6 of sum |a g|), with rows spread over 10^-12 .. 10^1, zero rows, a split whose A
-    rows pass 2^15 (the bf16x3 fixup rebuilds G from the planes), one-row and ragged last slabs, and a row
-    count past the delta table (kPlRows rows per split) -- and bitwise repeatable.
+    rows pass 2^15 (the bf16x3 fixup rebuilds G from the planes), one-row and ragged last slabs, and 2.2 M rows
+    (24 K rows per split, 1.5 K slabs through the four-slot DMA rings) -- and bitwise repeatable.
 """
 import pytest
 import torch
