@@ -1133,7 +1133,8 @@ wgrad_w_dual_kernel(WgradProblem p0, WgradProblem p1, const int *__restrict__ re
 // subnormal either way); an all-zero G row (kExpZero) leaves its a unscaled (the product is zero).
 constexpr int kPlA = 8;
 // Ablation builds only (make ab AB_FLAGS=-DMSAT_WGRAD_ABL=n, timing diagnostics, wrong results): bit 0 drops the
-// MFMAs, bit 1 the fragment reads, bit 2 the DMAs, bit 3 the A split.  0 in every product build.
+// MFMAs, bit 1 the fragment reads, bit 2 the DMAs, bit 3 the A split, bit 4 the k walk's barriers (with bits
+// 1-3 only).  0 in every product build.
 #ifndef MSAT_WGRAD_ABL
 #define MSAT_WGRAD_ABL 0
 #endif
@@ -1146,6 +1147,32 @@ struct WpLds {
     int rx[kPlSlots][8][64];                  // per wave: its two rows' exponents, lane l -> row 2 w + (l & 1)
     int red[8];
 };
+
+// One DMA group of a wave: its three G pieces (consecutive 1 KiB of one G slot), its raw A piece and its row-
+// exponent piece (4 B per lane), M0 saved and restored once for the five.
+__device__ __forceinline__ void pl_group_dma(const void *gbase, unsigned gv0, unsigned gv1, unsigned gv2, unsigned gdst,
+                                             const void *abase, unsigned av, unsigned adst, const void *xbase,
+                                             unsigned xv, unsigned xdst) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %7\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %7\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %7\n\t"
+        "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %9\n\t"
+        "s_mov_b32 m0, %10\n\ts_nop 0\n\tglobal_load_lds_dword %5, %11\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gv0), "v"(gv1), "v"(gv2), "v"(av), "v"(xv), "s"(gdst), "s"(gbase), "s"(adst), "s"(abase), "s"(xdst),
+          "s"(xbase)
+        : "memory");
+}
+
+__device__ __forceinline__ float vsub_f32(float a, float b) {  // one v_sub_f32 (not SLP-packed beside the MFMAs)
+    float r;
+    asm volatile("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int lda, const _Float16 *__restrict__ G,
                                               int ldg, int plo, const int *__restrict__ rexp, float *__restrict__ part,
@@ -1170,8 +1197,8 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[i][j] = f32x16v{};
-    // per-lane DMA pieces: G piece x = 3 w + e (plane block x >> 2 = q * 3 + u, rows 4 (x & 3) ..), raw A rows
-    // 2 w, 2 w + 1, row exponents of rows 2 w + (lane & 1)
+    // per-lane DMA pieces: G piece x = 3 w + e (plane block x >> 2 = q * 3 + u, rows 4 (x & 3) ..; the three are
+    // consecutive 1 KiB of a G slot), raw A rows 2 w, 2 w + 1, row exponents of rows 2 w + (lane & 1)
     int grow[3];
     unsigned goff[3], gcb[3];
 #pragma unroll
@@ -1181,54 +1208,89 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
         const int col = 128 * (pb % 3) + 8 * ch;
         const int gco = (pb / 3) * plo + (col < N ? col : 0);
         grow[e] = row;
-        goff[e] = (unsigned)((row * ldg + gco) * 2);  // a slab's last valid row lim clamps: min(off(row), off(lim))
+        goff[e] = (unsigned)((row * ldg + gco) * 2);  // the last slab clamps: min(off(row), off(lim))
         gcb[e] = (unsigned)(gco * 2);
     }
     const int arow = 2 * w + (lane >> 5), kc = k0 + 4 * (lane & 31), aco = kc < K ? kc : 0;
     const unsigned aoff = (unsigned)((arow * lda + aco) * 4), acb = (unsigned)(aco * 4);
     const int xrow = 2 * w + (lane & 1);
+    const unsigned xoff = (unsigned)(xrow * 4);
+    const char *gsplit = reinterpret_cast<const char *>(G + (size_t)rb * ldg);  // slab kk at + kk * 16 rows
+    const char *asplit = reinterpret_cast<const char *>(A + (size_t)rb * lda);
+    const char *xsplit = reinterpret_cast<const char *>(rexp + rb);
+    const int gstep = 32 * ldg, astep = 64 * lda;  // bytes per 16-row slab
     // slots are compile-time: the k walk is unrolled by four (kPlSlots, a multiple of the two A images)
-    auto issue_a = [&](int k, auto RA) {  // raw A slab + row exponents of min(k, ns - 1) -> slot RA == k % 4
-        constexpr int ra = decltype(RA)::value;
+    // group k: G(k) -> g[RG], raw A(k + 1) + its row exponents -> slot (RG + 1) % 4; RG == k % 4.  CL: the group
+    // may reach the split's last, partial slab or past it (rows clamped); the main walk runs without
+    auto issue = [&](int k, auto RG, auto CL) {
+        constexpr int rg = decltype(RG)::value, ra = (rg + 1) % kPlSlots;
         if constexpr ((MSAT_WGRAD_ABL & 4) != 0) return;
-        const int kk = min(k, ns - 1), lim = nr - 1 - 16 * kk;
-        MSAT_DCHECK(rb + 16 * kk + min(arow, lim), M);  // debug: the clamped source row
-        glds16_async_s(A + (size_t)(rb + 16 * kk) * lda, min(aoff, (unsigned)(lim * lda * 4) + acb),
-                       &L.raw[ra][w * 256]);
-        glds4_async_s(rexp + rb + 16 * kk, (unsigned)(min(xrow, lim) * 4), &L.rx[ra][w][0]);
-    };
-    auto issue = [&](int k, auto RG) {  // group k: G(k) -> g[RG], raw A(k + 1); RG == k % 4
-        constexpr int rg = decltype(RG)::value;
-        if constexpr ((MSAT_WGRAD_ABL & 4) != 0) return;
-        const int kk = min(k, ns - 1), lim = nr - 1 - 16 * kk;
-        const _Float16 *base = G + (size_t)(rb + 16 * kk) * ldg;
-        const unsigned lb = (unsigned)(lim * ldg * 2);
+        const int kg = decltype(CL)::value ? min(k, ns - 1) : k, ka = decltype(CL)::value ? min(k + 1, ns - 1) : k + 1;
+        unsigned gv[3], av = aoff, xv = xoff;
 #pragma unroll
-        for (int e = 0; e < 3; ++e) {
-            const int x = 3 * w + e;
-            MSAT_DCHECK(rb + 16 * kk + min(grow[e], lim), M);  // debug: the clamped source row
-            glds16_async_s(base, min(goff[e], lb + gcb[e]), &L.g[rg][x >> 2][512 * (x & 3)]);
+        for (int e = 0; e < 3; ++e) gv[e] = goff[e];
+        if constexpr (decltype(CL)::value) {
+            const int limg = nr - 1 - 16 * kg, lima = nr - 1 - 16 * ka;
+            const unsigned lb = (unsigned)(limg * ldg * 2);
+#pragma unroll
+            for (int e = 0; e < 3; ++e) {
+                MSAT_DCHECK(rb + 16 * kg + min(grow[e], limg), M);  // debug: the clamped source row
+                gv[e] = min(goff[e], lb + gcb[e]);
+            }
+            MSAT_DCHECK(rb + 16 * ka + min(arow, lima), M);
+            av = min(aoff, (unsigned)(lima * lda * 4) + acb);
+            xv = (unsigned)(min(xrow, lima) * 4);
         }
-        issue_a(k + 1, std::integral_constant<int, (rg + 1) % kPlSlots>{});
+        const unsigned gdst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)&L.g[rg][0][0] + 3072u * w);
+        const unsigned adst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)&L.raw[ra][w * 256]);
+        const unsigned xdst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)&L.rx[ra][w][0]);
+        pl_group_dma(gsplit + (size_t)kg * gstep, gv[0], gv[1], gv[2], gdst, asplit + (size_t)ka * astep, av, adst,
+                     xsplit + (size_t)ka * 64, xv, xdst);
+    };
+    auto issue_a0 = [&]() {  // raw A(0) + row exponents -> slot 0 (the prologue)
+        if constexpr ((MSAT_WGRAD_ABL & 4) != 0) return;
+        const int lim = nr - 1;
+        glds16_async_s(asplit, min(aoff, (unsigned)(lim * lda * 4) + acb), &L.raw[0][w * 256]);
+        glds4_async_s(xsplit, (unsigned)(min(xrow, lim) * 4), &L.rx[0][w][0]);
     };
     const int srow = t >> 5, sc = (t & 31) * 4;
     const int off = w3off(srow, sc >> 3) + 8 * ((sc >> 2) & 1);
-    float amax = 0.f;
-    auto split_a = [&](int k, auto RK) {  // raw[k % 4] -> a[k & 1]; RK == k % 4
+    // the split of raw A(k) (slot RK == k % 4) into image k & 1 in two halves: its LDS reads (issued ahead of the
+    // iteration's fragment reads, so waiting for them never waits for those) and the vector work + image store.
+    // a' = ldexp(a, sh), fp16 hi by v_cvt_pk_f16_f32 (RNE, as (_Float16)), lo = fp16(a' - hi) (v_sub_f32 kept
+    // unpacked: packed f32 beside MFMAs costs issue cycles).
+    struct SplitIn {
+        float4 v;
+        int e;
+    };
+    auto split_load = [&](auto RK) {
         constexpr int rk = decltype(RK)::value;
+        SplitIn r;
+        r.v = *reinterpret_cast<const float4 *>(&L.raw[rk][srow * kX3M + sc]);
+        r.e = L.rx[rk][w][srow & 1];
+        return r;
+    };
+    auto split_store = [&](const SplitIn &in, int k, auto RK, auto CL) {
+        constexpr int rk = decltype(RK)::value;
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        int sh = in.e == kExpZero ? 0 : kPlA - min(in.e - ge, 63);  // in [-55, 8]
+        // CL: rows past the split -> 2^-200 (0 for every finite a; a non-finite one stays non-finite and flags)
+        if constexpr (decltype(CL)::value) sh = 16 * k + srow < nr ? sh : -200;
+        const f2 x01 = {ldexpf(in.v.x, sh), ldexpf(in.v.y, sh)}, x23 = {ldexpf(in.v.z, sh), ldexpf(in.v.w, sh)};
+        const h2 h01 = __builtin_convertvector(x01, h2), h23 = __builtin_convertvector(x23, h2);
+        const f2 b01 = __builtin_convertvector(h01, f2), b23 = __builtin_convertvector(h23, f2);
+        const f2 r01 = {vsub_f32(x01[0], b01[0]), vsub_f32(x01[1], b01[1])};
+        const f2 r23 = {vsub_f32(x23[0], b23[0]), vsub_f32(x23[1], b23[1])};
+        const h2 l01 = __builtin_convertvector(r01, h2), l23 = __builtin_convertvector(r23, h2);
+        *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(L.a[rk & 1][0]) + off) =
+            make_uint2(__builtin_bit_cast(unsigned, h01), __builtin_bit_cast(unsigned, h23));
+        *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(L.a[rk & 1][1]) + off) =
+            make_uint2(__builtin_bit_cast(unsigned, l01), __builtin_bit_cast(unsigned, l23));
+    };
+    auto split_a = [&](int k, auto RK) {  // raw[k % 4] -> a[k & 1]; RK == k % 4 (the prologue)
         if constexpr ((MSAT_WGRAD_ABL & 8) != 0) return;
-        const float4 v = *reinterpret_cast<const float4 *>(&L.raw[rk][srow * kX3M + sc]);
-        const int e = L.rx[rk][w][srow & 1];
-        const int sh = e == kExpZero ? 0 : kPlA - min(e - ge, 63);
-        // rows past the split are zeroed by a mask, not a branch (a branch would sink the LDS reads into it
-        // and out of the scheduling groups)
-        const unsigned keep = 16 * k + srow < nr ? 0xffffffffu : 0u;
-        auto z = [&](float f) { return __uint_as_float(__float_as_uint(ldexpf(f, sh)) & keep); };
-        const float4 x = make_float4(z(v.x), z(v.y), z(v.z), z(v.w));
-        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
-        const SplitH4 xs = splith4(x);
-        *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(L.a[rk & 1][0]) + off) = xs.p[0];
-        *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(L.a[rk & 1][1]) + off) = xs.p[1];
+        split_store(split_load(RK), k, RK, std::true_type{});
     };
     const int h = lane >> 5, g = (lane >> 4) & 1;
     struct Frags {
@@ -1260,19 +1322,19 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
                 for (int q = 0; q < 2; ++q) acc[1][j][4 + q] += __builtin_bit_cast(float4, F.fb[j][q]).x;
             return;
         }
+        // pass-major (an accumulator's three products six MFMAs apart; measured the same as accumulator-major)
+        typedef _Float16 f16x8w __attribute__((ext_vector_type(8)));
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int pass = 0; pass < 3; ++pass)
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                typedef _Float16 f16x8w __attribute__((ext_vector_type(8)));
-                const f16x8w a0 = __builtin_bit_cast(f16x8w, F.fa[i][0]), a1 = __builtin_bit_cast(f16x8w, F.fa[i][1]);
-                const f16x8w b0 = __builtin_bit_cast(f16x8w, F.fb[j][0]), b1 = __builtin_bit_cast(f16x8w, F.fb[j][1]);
-                f32x16v c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, c, 0, 0, 0);  // h l
-                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, c, 0, 0, 0);  // l h
-                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, c, 0, 0, 0);  // h h
-                acc[i][j] = c;
-            }
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    // h l, l h, h h (each element's order of accumulation)
+                    const f16x8w a = __builtin_bit_cast(f16x8w, F.fa[i][pass == 1 ? 1 : 0]);
+                    const f16x8w b = __builtin_bit_cast(f16x8w, F.fb[j][pass == 0 ? 1 : 0]);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[i][j], 0, 0, 0);
+                }
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -1284,37 +1346,43 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
     // into G slot s % 4 (read out during s - 1) and raw / exponent slot (s + 5) % 4 (split during s - 1).  The end
     // waits for group s + 2 (vmcnt 10: groups s + 3 and s + 4 may fly) and a barrier: iteration s + 1 reads slab
     // s + 2's fragments from G(s + 2) and the image written here, and splits raw A(s + 3) (group s + 2).
-    auto iter = [&](int s, auto RS, const Frags &Fc, Frags &Fn) {
+    auto iter = [&](int s, auto RS, const Frags &Fc, Frags &Fn, auto CL) {
         constexpr int rs = decltype(RS)::value;
-        issue(s + 4, RS);
+        using RK = std::integral_constant<int, (rs + 2) % kPlSlots>;
+        issue(s + 4, RS, CL);
         __builtin_amdgcn_sched_barrier(0);
+        // unconditional split (straight-line code): near the end it splits clamped slabs into the unused image,
+        // every row of them past the split (zeros)
+        SplitIn si{};
+        if constexpr ((MSAT_WGRAD_ABL & 8) == 0) si = split_load(RK{});
         mfmas(Fc);
         read_frags(Fn, std::integral_constant<int, (rs + 1) % kPlSlots>{});
-        // unconditional (one basic block for the scheduling groups): near the end it splits clamped slabs into
-        // the unused image, every row of them past the split (zeros)
-        split_a(s + 2, std::integral_constant<int, (rs + 2) % kPlSlots>{});
+        if constexpr ((MSAT_WGRAD_ABL & 8) == 0) split_store(si, s + 2, RK{}, CL);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // the split's reads first
 #pragma unroll
         for (int k = 0; k < 18; ++k) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-            if (k < 11) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // fragment / raw A / exponent reads
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // vector ALU
-            if (k == 13 || k == 15) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // A image store
+            if (k < 10) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // fragment reads
+            __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // vector ALU
+            if (k == 13) __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);  // A image store
         }
         wait_vmcnt<10>();  // group s + 2
-        barrier_lds();
+        if constexpr ((MSAT_WGRAD_ABL & 16) == 0) barrier_lds();
     };
     if (ns > 0) {
         Frags F0, F1;
-        issue_a(0, I0{});
-        issue(0, I0{});
-        issue(1, I1{});
-        issue(2, I2{});
+        using T1 = std::true_type;
+        using F_ = std::false_type;
+        issue_a0();
+        issue(0, I0{}, T1{});
+        issue(1, I1{}, T1{});
+        issue(2, I2{}, T1{});
         wait_vmcnt<15>();  // raw A(0) + exponents (this wave's own rows)
         split_a(0, I0{});
         // this wave's reads of slot 0 are done before group 3 refills it with raw A(4) (each wave reads only the
         // rows its own DMA pieces write)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        issue(3, I3{});
+        issue(3, I3{}, T1{});
         wait_vmcnt<15>();  // group 0: G(0), raw A(1)
         split_a(1, I1{});
         wait_vmcnt<10>();  // group 1: G(1), raw A(2)
@@ -1322,20 +1390,40 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
         read_frags(F0, I0{}, true);
         if ((MSAT_WGRAD_ABL & 2) != 0) F1 = F0;
         barrier_lds();  // every wave's slab-0 reads are done before group 4 refills G slot 0
+        // main walk: every group it issues (k <= s + 7, raw A k + 1 <= s + 8) and every slab it splits (<= s + 5)
+        // is a full slab of the split (nfull of them), so no row is clamped or masked
+        const int nfull = nr / 16;
         int s = 0;
-        for (; s + 4 <= ns; s += 4) {
-            iter(s, I0{}, F0, F1);
-            iter(s + 1, I1{}, F1, F0);
-            iter(s + 2, I2{}, F0, F1);
-            iter(s + 3, I3{}, F1, F0);
+        for (; s + 9 <= nfull; s += 4) {
+            iter(s, I0{}, F0, F1, F_{});
+            iter(s + 1, I1{}, F1, F0, F_{});
+            iter(s + 2, I2{}, F0, F1, F_{});
+            iter(s + 3, I3{}, F1, F0, F_{});
         }
-        if (s < ns) iter(s, I0{}, F0, F1);
-        if (s + 1 < ns) iter(s + 1, I1{}, F1, F0);
-        if (s + 2 < ns) iter(s + 2, I2{}, F0, F1);
+        for (; s + 4 <= ns; s += 4) {
+            iter(s, I0{}, F0, F1, T1{});
+            iter(s + 1, I1{}, F1, F0, T1{});
+            iter(s + 2, I2{}, F0, F1, T1{});
+            iter(s + 3, I3{}, F1, F0, T1{});
+        }
+        if (s < ns) iter(s, I0{}, F0, F1, T1{});
+        if (s + 1 < ns) iter(s + 1, I1{}, F1, F0, T1{});
+        if (s + 2 < ns) iter(s + 2, I2{}, F0, F1, T1{});
         wait_vmcnt<0>();  // the last (clamped, unused) groups land before the workgroup's LDS is released
     }
-    if (MSAT_WGRAD_ABL) amax = 0.f;  // ablation builds: never the fixup (its time is not the kernel's)
-    const int bad = __syncthreads_or(!(amax < 32768.0f));
+    // Range: an A element whose scaled value overflows fp16 (|a'| >= 65520) or any non-finite input leaves a
+    // non-finite accumulator (Inf hi, Inf * 0 = NaN), so a workgroup with one is recomputed by the bf16x3 fixup --
+    // which also reproduces a genuine Inf / NaN of the fp32 product.  Below that the split is exact to 2^-22
+    // (|a' - hi| <= 16 is exact in fp32 and its fp16 keeps 11 bits).
+    bool nonfin = false;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) nonfin |= !(fabsf(acc[i][j][reg]) <= 3.402823466e38f);
+    if (MSAT_WGRAD_ABL) nonfin = false;  // ablation builds: never the fixup (its time is not the kernel's)
+    const int bad = __syncthreads_or(nonfin);
     if (t == 0) *flag = bad;
     if (bad) return;
     float *P = part + (size_t)sp * K * N;

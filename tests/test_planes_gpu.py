@@ -150,7 +150,7 @@ def test_dual_dgrad_planes_is_bitwise_the_fp32_row_form(M, K1, wbig):
 
 
 @pytest.mark.parametrize("M,K1,amp", [(1, 128, 0), (17, 256, 0), (385, 256, 0), (4999, 128, 0), (70001, 256, 0),
-                                      (20000, 128, 1), (2200001, 256, 0)])
+                                      (20000, 128, 1), (20000, 256, 2), (2200001, 256, 0)])
 def test_dual_wgrad_planes_match_fp64(M, K1, amp):
     from marlsat import _lib
 
@@ -163,8 +163,10 @@ def test_dual_wgrad_planes_match_fp64(M, K1, amp):
     P = host_planes(D, rexp)
     hx = torch.randn(M, H, device="cuda", generator=g)
     xx = torch.randn(M, K1, device="cuda", generator=g)
-    if amp:  # |a| >= 2^15 in one split's rows: flagged, recomputed by the bf16x3 fixup from the planes
+    if amp == 1:  # a' past fp16's range in one split's rows: flagged, recomputed by the bf16x3 fixup from the planes
         hx[M // 3: M // 3 + 5] *= 1e6
+    if amp == 2:  # |a| up to ~250: a' = a 2^8 up to fp16's largest finite values, still the fp16x2 path
+        xx[M // 2: M // 2 + 7] *= 60.0
     W0 = torch.randn(H, 3 * H, device="cuda", generator=g)
     W1 = torch.randn(K1, 3 * H, device="cuda", generator=g)
     ws = torch.empty(int(L.msat_gemm_wgrad_dual_workspace_bytes(M, H, 3 * H, K1, 3 * H)) // 4 + 1, device="cuda")
