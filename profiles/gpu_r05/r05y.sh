@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 5, call y: the planes in 16-byte chunks alternating hi and lo (a lane's 8 columns are 32 contiguous bytes, as
+# in the fp32 rows) -- planes / gemm / GRU-backward / MAPPO tests, both dual forms (clause / var, three alternations),
+# and the MAPPO leg's kernel trace (collect_mappo.sh) beside calls w (planes split in halves) and x (fp32 rows)
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
+T="python -u -m pytest -m gpu --timeout 600 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 600 $T -q tests/test_planes_gpu.py tests/test_gemm_gpu.py tests/test_gru_bwd_reduction_gpu.py tests/test_mappo_gpu.py > gpurun_out/r05y_tests.log 2>&1
+rc=$?; echo "tests rc $rc"; tail -2 gpurun_out/r05y_tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u profiles/dual_bench.py 1316000 10 256 3 > gpurun_out/r05y_dual_clause.log 2>&1 || exit 4
+timeout -k 10 300 python -u profiles/dual_bench.py 560000 10 128 3 > gpurun_out/r05y_dual_var.log 2>&1 || exit 5
+grep '^{' gpurun_out/r05y_dual_clause.log gpurun_out/r05y_dual_var.log | cut -d: -f2- | cut -c1-110
+timeout -k 10 900 bash profiles/collect_mappo.sh r05y > gpurun_out/r05y_collect.log 2>&1 || exit 6
+grep -E "wgrad_w_dual|gemm_h2r16_dual|gru_ln_bwd" gpurun_out/keep/r05y_mappo_uf100-430_kernel_stats.csv | cut -d, -f1-4 | cut -c1-150
+grep -o '"s_min_med_max": \[[^]]*\]' gpurun_out/keep/r05y_mappo_uf100-430_bench.json
