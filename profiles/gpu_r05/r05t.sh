@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5, call t: final validation -- the whole GPU test suite and smoke() on the committed tree
+# round 5, call t (and tb): final validation -- the whole GPU test suite and smoke() on the committed tree
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 T="python -u -m pytest -m gpu --timeout 600 --timeout-method thread -p no:cacheprovider"
 timeout -k 10 900 $T -q tests > gpurun_out/r05t_gpu_tests.log 2>&1
