@@ -102,9 +102,9 @@ def _cpu_worker(args):
 
 def host_cpu() -> dict:
     """The host the CPU baselines run on: model name (/proc/cpuinfo, as lscpu prints it), the cores
-    this process may run on (sched_getaffinity) and the cores used.  The default cap is the box's CPU
-    share: OMP_NUM_THREADS (16 per GPU on the GPU pool, where the affinity mask shows the whole
-    machine); MARLSAT_CPU_BASELINE_CORES overrides it."""
+    this process may run on (sched_getaffinity) and the cores used: min(affinity, the cgroup's CPU quota,
+    the cap).  The cap is OMP_NUM_THREADS (16 per GPU on the GPU pool, where the affinity mask shows the
+    whole machine but the cgroup allows 16 CPUs); MARLSAT_CPU_BASELINE_CORES overrides it."""
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -121,8 +121,14 @@ def host_cpu() -> dict:
     cap_src = "MARLSAT_CPU_BASELINE_CORES" if os.environ.get("MARLSAT_CPU_BASELINE_CORES") else (
         "OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS") else "affinity")
     cap = int(os.environ.get("MARLSAT_CPU_BASELINE_CORES") or os.environ.get("OMP_NUM_THREADS") or affinity)
-    return {"cpu_model": model, "affinity_cores": affinity, "cores": max(1, min(affinity, cap)),
-            "cap_source": cap_src, "cgroup_cpus": cgroup_cpus()}
+    quota = cgroup_cpus()
+    cores = min(affinity, cap)
+    if quota:  # more processes than the quota only time-share it
+        if int(quota) < cores:
+            cap_src = "cgroup quota"
+        cores = min(cores, int(quota))
+    return {"cpu_model": model, "affinity_cores": affinity, "cores": max(1, cores),
+            "cap_source": cap_src, "cgroup_cpus": quota}
 
 
 def cgroup_cpus():
@@ -151,39 +157,65 @@ def cpu_baseline(V, C, vpa, pool, budget_s=12.0, nenv=16, cores=None):
     import multiprocessing as mp
 
     host = host_cpu()
-    if cores is None:
-        cores = host["cores"]
-    else:
-        host = dict(host, cores=cores, cap_source="all affinity cores")
+    procs = host["cores"] if cores is None else cores
     ctx = mp.get_context("fork")  # forked before any GPU initialisation
-    with ctx.Pool(cores) as p:
-        res = p.map(_cpu_worker, [(V, C, vpa, nenv, budget_s, w, pool) for w in range(cores)])
+    with ctx.Pool(procs) as p:
+        res = p.map(_cpu_worker, [(V, C, vpa, nenv, budget_s, w, pool) for w in range(procs)])
     total = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
+    # cores = CPUs the processes actually had: never more than the cgroup quota, however many processes ran
+    used = min(procs, host["cores"]) if cores is None else min(procs, int(host["cgroup_cpus"] or procs))
+    over = procs > used
     return {
         "value": total / wall,
         "unit": "env-steps/s",
-        "cores": cores,
+        "cores": used,
+        "processes": procs,
+        "oversubscribed": over,
         "kind": "port",
         "host": host,
         "sample": f"oracle/sat_env.py step_autoreset (reference algorithm: full rescan, dense int32 obs, "
-                  f"reset-all-then-select) on {cores} processes x {nenv} envs of the same workload, "
+                  f"reset-all-then-select) on {procs} single-thread processes x {nenv} envs of the same workload, "
                   f"{budget_s:.0f} s each ({total} env-steps); host {host['cpu_model']}, "
-                  f"{host['affinity_cores']} cores in the affinity mask, {cores} used ({host['cap_source']})",
+                  f"{host['affinity_cores']} cores in the affinity mask, cgroup quota {host['cgroup_cpus']} CPUs, "
+                  f"{used} CPUs used ({host['cap_source'] if cores is None else 'explicit process count'})"
+                  + (f"; OVERSUBSCRIBED: {procs} processes time-share {used} CPUs" if over else ""),
     }
 
 
 # ------------------------------------------------------------------- PMC ----
-def load_pmc_traffic(workload: str):
-    """HBM bytes per launch of the step kernel from the committed rocprofv3 PMC summary, if any."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+def _round_of(path: str) -> int:
+    """The round a committed profile belongs to, from its path (profiles/r05/..., profiles/r04_pmc.json)."""
+    import re
+
+    tags = re.findall(r"(?:^|[/_])r(\d\d)", os.path.relpath(path, ROOT))
+    return max((int(t) for t in tags), default=0)
+
+
+def load_pmc_traffic(workload: str, kernel: str, default_shape: bool = True):
+    """HBM bytes per launch of the step kernel from the newest committed rocprofv3 PMC summary under
+    profiles/ (any depth, archives excluded): either {"workload", "hbm_bytes_per_launch"} records
+    (profiles/collect.sh) or per-kernel tables {kernel: {"per_launch_bytes": {"total"}}}
+    (profiles/pmc_env_summary.py), matched on the kernel instantiation the leg launches; a table without a
+    "workload" key was collected on the bench's default legs, so it serves only default_shape runs."""
+    files = [f for f in glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True)
+             if "archive" not in f]
+    files.sort(key=lambda f: (_round_of(f), f))
+    want = kernel.replace(" ", "")
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:
             continue
+        if not isinstance(d, dict):
+            continue
         if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
-            return float(d["hbm_bytes_per_launch"]), os.path.basename(f)
+            return float(d["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+        if d.get("workload", workload if default_shape else None) != workload:
+            continue
+        for k, v in d.items():
+            if isinstance(v, dict) and k.replace(" ", "") == want and (v.get("per_launch_bytes") or {}).get("total"):
+                return float(v["per_launch_bytes"]["total"]), os.path.relpath(f, ROOT)
     return None, None
 
 
@@ -319,8 +351,46 @@ def progress(rank: int, msg: str) -> None:
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
-    """One timed MAPPO train cycle (after one warm-up cycle) on the stated config."""
+def _timed_cycle(learner, rs, gen, dist):
+    """One MAPPO train cycle from runner state rs, phase by phase: (wall s, [rollout, gae, ppo_update, metrics]
+    ms, metrics, the new runner state)."""
+    import torch
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record()
+    rs = learner.rollout(rs)
+    ev[1].record()
+    learner.compute_advantages(rs)
+    ev[2].record()
+    losses, ent = learner.ppo_update(1, gen)
+    ev[3].record()
+    met = learner.metrics(losses, ent)
+    ev[4].record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    return time.perf_counter() - t0, [ev[i].elapsed_time(ev[i + 1]) for i in range(4)], met, rs
+
+
+def _max_over_ranks(cycles, dist):
+    """The slowest rank's wall time and phases, per cycle."""
+    import torch
+
+    if dist is None:
+        return cycles
+    t = torch.tensor([v for c in cycles for v in [c[0]] + c[1]], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [(r[0], r[1:]) for r in t.view(len(cycles), 5).tolist()]
+
+
+def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int, fp32_cycles: int = 0):
+    """Timed MAPPO train cycles (after one warm-up cycle) on the stated config; with fp32_cycles, that many
+    more cycles on the fp32 path (MARLSAT_PRECISION=fp32: fp32 MFMA in the reference's operation order) of the
+    same learner, reported beside the default path's time."""
     import torch
 
     from marlsat import SATEnv
@@ -361,43 +431,44 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
     GNNActorCritic.ktimer = {}  # per-launch HIP events over every timed cycle
     cycles = []  # (wall s, [rollout, gae, ppo_update, metrics] ms) per timed cycle
     for _ in range(args.mappo_cycles):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        ev[0].record()
-        rs = learner.rollout(rs)
-        ev[1].record()
-        learner.compute_advantages(rs)
-        ev[2].record()
-        losses, ent = learner.ppo_update(1, gen)
-        ev[3].record()
-        met = learner.metrics(losses, ent)
-        ev[4].record()
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        cycles.append((time.perf_counter() - t0, [ev[i].elapsed_time(ev[i + 1]) for i in range(4)]))
+        wall, ph, met, rs = _timed_cycle(learner, rs, gen, dist)
+        cycles.append((wall, ph))
     flops = float(GNNActorCritic.flops) / len(cycles)
     kernels = kernel_table(GNNActorCritic.ktimer)
     GNNActorCritic.ktimer = None
     dom = next(k for k in kernels if k["peak"])  # the matrix kernel with the most time in the cycles
     rank_ms = [0.0] * world  # each rank's dominant-kernel average launch time
     rank_ms[rank] = dom["ms_avg"]
+    cycles = _max_over_ranks(cycles, dist)
     per_cycle = [c[0] for c in cycles]
-    if dist is not None:  # the slowest rank's wall time and phases, per cycle
-        t = torch.tensor([v for c in cycles for v in [c[0]] + c[1]], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t = t.view(len(cycles), 5).tolist()
-        cycles = [(r[0], r[1:]) for r in t]
-        per_cycle = [c[0] for c in cycles]
+    if dist is not None:
         rk = torch.tensor(rank_ms, dtype=torch.float64, device="cuda")
         dist.all_reduce(rk)  # every rank fills its own slot: SUM = gather
         rank_ms = [float(v) for v in rk]
     elapsed = statistics.median(per_cycle)
     phases = [statistics.median(c[1][i] for c in cycles) for i in range(4)]
     cycle_ms = sum(sum(c[1]) for c in cycles)
+    fp32 = None
+    if fp32_cycles:  # the same learner on the fp32 path: what the split arithmetic buys (BASELINE.md:57)
+        from marlsat.learners import gnn as gnn_mod
+
+        progress(rank, f"mappo {workload}: {fp32_cycles} fp32-path cycle(s)")
+        prev = gnn_mod.set_precision("fp32")
+        try:
+            c32 = []
+            for _ in range(fp32_cycles):
+                wall, ph, _, rs = _timed_cycle(learner, rs, gen, dist)
+                c32.append((wall, ph))
+            c32 = _max_over_ranks(c32, dist)
+        finally:
+            gnn_mod.restore_precision(prev)
+        s32 = statistics.median(c[0] for c in c32)
+        fp32 = {"s_per_update": s32, "s_per_update_cycles": [c[0] for c in c32],
+                "phase_ms": dict(zip(("rollout", "gae", "ppo_update", "metrics"),
+                                     [statistics.median(c[1][i] for c in c32) for i in range(4)])),
+                "speedup_of_default": s32 / elapsed,
+                "note": "MARLSAT_PRECISION=fp32 (fp32 MFMA throughout, phi not folded: the reference's operation "
+                        "order), same learner and config, timed after the default path's cycles (no extra warm-up)"}
     replicas = replica_check(net, dist)
     if type(comm).__name__ == "CapiComm":
         comm.destroy()
@@ -431,6 +502,7 @@ def mappo_bench(args, rank, world, dist, workload: str, B: int, T: int):
         "solve_rate": met["solve_rate"],
         "params_check": replicas,
         "peak_hbm_gb": torch.cuda.max_memory_allocated() / 1e9,
+        "fp32_path": fp32,
     }
     side = write_side_file(f"mappo_{workload}_n{world}_rank{rank}", full)
     return compact_leg(full, side)
@@ -447,7 +519,7 @@ def compact_leg(full: dict, side: Optional[str]) -> dict:
     c, r = full["config"], full["roofline"]
     ph = full["phase_ms"]
     cyc = full.get("s_per_update_cycles", [full["s_per_update"]])
-    return {
+    out = {
         "value": _sig(full["value"]),
         # min / median / max over the timed cycles (each cycle's time, in order, and Adam steps/s: side file)
         "s_min_med_max": [_sig(min(cyc)), _sig(full["s_per_update"]), _sig(max(cyc))],
@@ -464,8 +536,11 @@ def compact_leg(full: dict, side: Optional[str]) -> dict:
                      # the dominant kernel's launch ms, min and max over ranks (every rank's in the side file)
                      "rank_ms": [_sig(min(r["per_rank_kernel_ms"])), _sig(max(r["per_rank_kernel_ms"]))]},
         "params_check": {k: v for k, v in (full.get("params_check") or {}).items() if k != "checksum"},
-        "detail": os.path.basename(side) if side else side,  # under gpurun_out/
+        "detail": os.path.basename(side)[6:-5] if side else side,  # gpurun_out/bench_<detail>.json
     }
+    if full.get("fp32_path"):  # the fp32 path's s / update on the same learner (side file: its phases)
+        out["fp32_s"] = _sig(full["fp32_path"]["s_per_update"])
+    return out
 
 
 def replica_check(net, dist):
@@ -614,11 +689,6 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
         e0 = classes[0]
         lanes = int(os.environ.get("MARLSAT_ENV_THREADS", "0")) or env_lanes(e0.num_agents, 2 * e0.num_vars + e0.num_clauses)
         kernel = f"env_kernel<2,{'int' if obs_dtype == torch.int32 else 'signed char'},{lanes}>"
-    # steady state: the episode-step counters start uniform over [0, MAX_STEPS), so ~B/512 envs time
-    # out (and auto-reset: new pool instance + assignment drawn in-kernel) in every launch, as in a
-    # long-running rollout; a fresh reset would keep the reset branch idle for 511 steps
-    for st in states:
-        st.step.copy_(torch.randint(0, 512, (st.num_envs,), generator=gen, device="cuda", dtype=torch.int32))
     counter = 1
     # the same launches with the kernel's clock stamps on (a second out record carrying the stamp buffers)
     nclk = args.clock_launches
@@ -660,6 +730,11 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
             n_pre += 1
         torch.cuda.synchronize()
     preroll = {"s": round(time.perf_counter() - t_pre, 3), "launches": n_pre}
+    # steady state: after the pre-roll the episode-step counters are set uniform over [0, MAX_STEPS), so
+    # ~B/512 envs time out (and auto-reset: new pool instance + assignment drawn in-kernel) in every launch,
+    # as in a long-running rollout (solved envs reset on top of that)
+    for st in states:
+        st.step.copy_(torch.randint(0, 512, (st.num_envs,), generator=gen, device="cuda", dtype=torch.int32))
     for i in range(args.warmup):
         step(i, counter)
         counter += 1
@@ -780,12 +855,13 @@ def run_cpu_baselines(args) -> dict:
                        sample=" | ".join(r["sample"] for r in rates))
         return cpu
 
-    # one worker per host core of the box (the affinity mask); beside it the run capped
-    # at the box's CPU share (OMP_NUM_THREADS), when that is smaller
-    cpu = leg(host["affinity_cores"] if args.cpu_all_cores else None)
+    # one worker per host core the box gives this process (its cgroup CPU quota; the
+    # affinity mask shows the whole machine)
+    cpu = leg(None)
     if args.cpu_all_cores and host["cores"] < host["affinity_cores"]:
-        capped = leg(None)
-        cpu["capped"] = {"value": capped["value"], "cores": capped["cores"], "cap_source": host["cap_source"]}
+        wide = leg(host["affinity_cores"])
+        cpu["all_affinity"] = {"value": wide["value"], "processes": wide["processes"], "cores": wide["cores"],
+                               "oversubscribed": wide["oversubscribed"]}
     out = {"env": cpu, "mappo": None}
     legs = [s for s in args.mappo.split(",") if s]
     if legs:
@@ -851,6 +927,9 @@ def main():
     ap.add_argument("--mappo-cycles", type=int, default=3,
                     help="timed train cycles per MAPPO leg (after one warm-up cycle); value = 1 / their median "
                          "(min / median / max reported)")
+    ap.add_argument("--mappo-fp32-cycles", type=int, default=1,
+                    help="cycles of the headline MAPPO leg rerun on the fp32 path (MARLSAT_PRECISION=fp32, the reference's "
+                         "operation order) after its timed cycles: 'fp32_s' beside the default (0: skip)")
     ap.add_argument("--preroll-s", type=float, default=1.0,
                     help="seconds of untimed back-to-back env launches before the --warmup steps of the headline env "
                          "leg (the side legs run 0.25 s), so the timed region starts at the clock a long rollout "
@@ -858,9 +937,10 @@ def main():
     ap.add_argument("--clock-launches", type=int, default=8,
                     help="env launches with the kernel's clock stamps on, right after the timed region (0: none): "
                          "sclk_mhz in the line")
-    ap.add_argument("--cpu-all-cores", type=int, default=1,
-                    help="1: the env CPU baseline runs one worker per affinity core (BASELINE.md section 2), with the "
-                         "capped run (OMP_NUM_THREADS) beside it; 0: capped only")
+    ap.add_argument("--cpu-all-cores", type=int, default=0,
+                    help="0: the env CPU baseline runs one single-thread worker per CPU the box gives this process "
+                         "(min of affinity, cgroup quota, OMP_NUM_THREADS); 1: one per affinity core as well, "
+                         "labelled oversubscribed when that exceeds the quota (side record 'all_affinity')")
     ap.add_argument("--env-legs", default="uf50-218:1024,uf100-430:4096,mixed:1024,mixed:8192",
                     help="env side legs 'workload:envs_per_gpu,...' ('' skips): BASELINE configs 2 and 3 and config 5 "
                          "(1024 envs per GPU = its 8-GPU share of 8192, and all 8192 on one GPU)")
@@ -911,16 +991,18 @@ def main():
     r = env_leg(args, rank, world, dist)
     side_env = env_side_legs(args, rank, world, dist)
     legs = []
-    for spec in filter(None, args.mappo.split(",")):
+    for i, spec in enumerate(filter(None, args.mappo.split(","))):
         wl, envs, T = spec.split(":")
-        legs.append(mappo_bench(args, rank, world, dist, wl, int(envs), int(T)))
+        legs.append(mappo_bench(args, rank, world, dist, wl, int(envs), int(T),
+                                fp32_cycles=args.mappo_fp32_cycles if i == 0 else 0))
     mappo = legs[0] if legs else None
 
     if rank == 0:
         B, K, elapsed, kern_ms = sum(r["sizes"]), r["K"], r["elapsed"], r["kern_ms"]
         achieved = r["launch_bytes"] / (kern_ms * 1e-3) / 1e9
         wl_key = args.workload if args.workload != "mixed" else "mixed"
-        traffic, traffic_src = load_pmc_traffic(f"{wl_key}/B{B}/{args.obs_dtype}")
+        traffic, traffic_src = load_pmc_traffic(f"{wl_key}/B{B}/{args.obs_dtype}", r["kernel"],
+                                                default_shape=args.envs is None and args.pool == 1024)
         sids = ",".join(str(WORKLOADS[n][4]) for n in r["names"])
         cfg = {
             "workload": f"{args.workload} SATEnv.step_env + rollout auto-reset (fused "
@@ -959,7 +1041,7 @@ def main():
             "mappo_cpu_baseline": base["mappo"] if base else None,
             "done_fraction_last_step": r["done_frac"],
             "auto_resets_in_timed_region": r["resets"],
-            "steady_state": "episode-step counters staggered uniformly over [0, 512) before warm-up",
+            "steady_state": "episode-step counters staggered uniformly over [0, 512) after the pre-roll, before warm-up",
             # the shader clock the env kernel ran at (per-workgroup s_memtime / s_memrealtime deltas of stamped
             # launches right after the timed region; cold = the process's first env launch), and the untimed
             # time-based pre-roll ahead of the --warmup steps

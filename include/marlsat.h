@@ -119,7 +119,7 @@ typedef struct msat_step_out {
 } msat_step_out;
 
 const char *msat_last_error(void);
-int msat_version(void);
+int msat_version(void); /* 2: msat_step_out carries clock_stamps (version 1 had no such field) */
 
 /* Pack an int32 literal tensor (N,C,K) (signed, 1-based, 0 = null literal) into
  * the device pool layout uint16 (N,C,4).  Literals with |l| > V set *err_flag

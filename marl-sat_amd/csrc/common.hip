@@ -22,4 +22,6 @@ int check_launch_plain(const char *what) {
 }  // namespace msat
 
 extern "C" const char *msat_last_error(void) { return msat::g_err; }
-extern "C" int msat_version(void) { return 1; }
+// ABI version: 2 since msat_step_out gained clock_stamps (round 5); a caller built against the version-1 header
+// passes a struct without that field, so it must check msat_version() >= 2
+extern "C" int msat_version(void) { return 2; }

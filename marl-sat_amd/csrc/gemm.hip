@@ -655,10 +655,10 @@ static int wgrad_h2_dual_impl(const float *A0, int32_t lda0, const void *G0, int
         MSAT_REQUIRE(rots[i] >= 0 && rots[i] < Ns[i] && rots[i] % 4 == 0, "gemm_wgrad_h2_dual: bad rot");
         if (pl)  // whole 16-byte chunks of both planes (the DMA pieces)
             MSAT_REQUIRE(Ks[i] % 4 == 0 && Ns[i] % 8 == 0 && ldas[i] % 4 == 0 && ldgs[i] % 8 == 0 && plo % 8 == 0 &&
-                             plo >= Ns[i] && (reinterpret_cast<uintptr_t>(As[i]) & 15) == 0 &&
+                             plo >= Ns[i] && plo + Ns[i] <= ldgs[i] && (reinterpret_cast<uintptr_t>(As[i]) & 15) == 0 &&
                              (reinterpret_cast<uintptr_t>(Gs[i]) & 15) == 0,
-                         "gemm_wgrad_h2_dual_planes: K %% 4, N %% 8, lda %% 4, ldg %% 8, plo %% 8 (>= N) and 16-byte "
-                         "aligned operands required");
+                         "gemm_wgrad_h2_dual_planes: K %% 4, N %% 8, lda %% 4, ldg %% 8, plo %% 8 (>= N, plo + N <= "
+                         "ldg) and 16-byte aligned operands required");
         else
             MSAT_REQUIRE(msat_wgrad_x3_ok(As[i], ldas[i], (const float *)Gs[i], ldgs[i], Ks[i], Ns[i]),
                          "gemm_wgrad_h2_dual: K %% 4, N %% 4, ld %% 4 and 16-byte aligned operands required");

@@ -1629,7 +1629,10 @@ static int gemm_h2_dual_impl(const void *A0, int32_t lda0, const void *W0_h2, co
                      ldc1 >= N1 && a16x3(A0) && a16x3(A1) && a16x3(W0_h2) && a16x3(W0_x3) && a16x3(W1_h2) &&
                      a16x3(W1_x3),
                  "gemm_h2_dual: K %% 32, lda %% 4 (planes: %% 8) and 16-byte aligned operands required");
-    MSAT_REQUIRE(!pl || (plo % 8 == 0 && plo >= K), "gemm_h2_dual_planes: plo %% 8 and plo >= K required");
+    // the lo plane of a row's K columns lies inside the row: plo + K <= lda (a layout whose column offset pushes it
+    // further is the caller's to rule out; the learner's rows are [hi 4H | lo 4H] with K <= 3H at offsets <= H)
+    MSAT_REQUIRE(!pl || (plo % 8 == 0 && plo >= K && plo + K <= lda0 && plo + K <= lda1),
+                 "gemm_h2_dual_planes: plo %% 8, plo >= K and plo + K <= lda required");
     DgradProblem p[2];
     const void *As[2] = {A0, A1};
     const int ldas[2] = {lda0, lda1}, ldcs[2] = {ldc0, ldc1}, Ns[2] = {N0, N1}, accs[2] = {acc0, acc1};

@@ -737,406 +737,6 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
 
 __global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2s_kernel(GruX3rArgs a) { gru_h2s_tile(a, blockIdx.x); }
 
-// ---------------------------------------------------------------------------------------------
-// Unit-half GRU forward (msat_gru_ln_fused_fwd_h2r with MARLSAT_GRU_FORM=h2u): 256-row tiles, each computed
-// in two passes over the k walk, one per half of the hidden units (64 of 128, all four gate groups).  Against
-// the 128-row x 128-unit tile of gru_h2s_tile: the same 128 accumulator registers per wave, but every weight
-// slab DMA'd into LDS serves 256 rows instead of 128, so per row the texture path carries half the weight
-// bytes (2 x 24 KiB per 256 rows and step instead of 48 KiB per 128) and twice the activation bytes (each
-// row is read once per pass): 448 instead of 512 B per row and 32-k step, -12.5 %; and each weight
-// fragment read from LDS feeds two 16-row MFMA tiles, so the wave's fragment reads per step halve (24 + 4
-// ds_read_b128 instead of 48 + 2).
-//   wave w: rows 32 w .. 32 w + 31 of the tile (two 16-row tiles rt); per pass acc[gate][4 column tiles][rt].
-//   LDS: two weight buffers of 6 (plane, gate) images [64 units][4 chunks] (24 KiB each), three activation
-//   slots [256 rows][8 chunks] (32 KiB each: step s in slot s % 3, fetched two steps ahead by the wave that
-//   reads them -- its own 32 rows -- and split in the middle of the step before their use after a counted
-//   wait), the pass-0 LayerNorm row sums (2 KiB) and the range flags.
-//   k walk per pass: the input steps, then h's quarters with the pass's own two last, so the epilogue reads
-//   its h values from the slots.  Pass 0's epilogue writes its tape columns and keeps h' of its 64 units in
-//   registers (32 per lane) and its LayerNorm row sums in LDS; pass 1's finishes the row statistics over all
-//   128 units and writes both halves.  Range flags as gru_h2s_tile, per 128-row fixup tile (both set).
-constexpr int kUDmaLate = 4;  // waves 4..7 issue a step's DMA before this block of 12 (SIMD-partner stagger)
-
-// Each pass is its own copy of the code, and both start from a laundered thread index and a laundered kernarg
-// pointer (an empty asm the compiler cannot see through), so nothing per-lane or per-argument computed in pass 0
-// is hoisted and held across pass 1's k loop (held, they spilled: 217 VGPRs, with scratch loads inside the k
-// loop that the counted vmcnt waits do not count).
-template <int HF>
-__device__ __forceinline__ bool gru_h2u_pass(int tile, f32x4g (&h0)[4][2]) {
-    constexpr int NW = 8, H = 128, HU = 64;  // waves, hidden units, units per pass
-    constexpr int IMG = HU * 4;              // uint4 per (plane, gate) image: 64 units x 4 chunks = 4 KiB
-    constexpr int NI = 6;                    // (plane, gate) images per step
-    constexpr int NPW = NI * 4 / NW;         // 1 KiB weight pieces per wave and step (3)
-    constexpr int TR = 32 * NW;              // tile rows (256)
-    constexpr int ASL = TR * 8;              // uint4 per activation slot (32 KiB)
-    constexpr int NSL = 3;                   // activation slots
-    constexpr int LMAIN = 2 * NI * IMG + NSL * ASL;  // 144 KiB: weight buffers + slots (the final stage reuses it)
-    extern __shared__ uint4 L[];                     // LMAIN + pass-0 row sums (256 x float2) + range flags
-    uint4 *const Bs = L, *const As = L + 2 * NI * IMG;
-    float2 *const rsum = reinterpret_cast<float2 *>(L + LMAIN);
-    int *const wflag = reinterpret_cast<int *>(L + LMAIN + TR / 2);
-    constexpr int SW = 132;  // stage row stride (floats): [32 rows][128 units] per wave
-    static_assert(NW * 32 * SW * 4 <= LMAIN * 16, "the output stage fits the weight buffers + slots");
-    typedef __attribute__((address_space(4))) const GruX3rArgs KArgs;
-    KArgs *ka = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(ka));
-    const GruX3rArgs &a = *(const GruX3rArgs *)ka;
-    int t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    const int lane = t & 63, l16 = lane & 15, g = lane >> 4;
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int row0 = tile * TR, wr = 32 * w;
-    constexpr int nsh = H / 32;
-    const int nin = a.kxp / 32, ns = nin + nsh;
-    const float *const hp = a.hp, *const sg0 = a.seg[0], *const sg1 = a.seg[1], *const sg2 = a.seg[2];
-    const int w0 = a.seg_w[0], w01 = a.seg_w[0] + a.seg_w[1], kx_end = a.Kx;
-    const unsigned lpart = (unsigned)(lane >> 2) * 2u, chb = 16u * ((lane & 3) ^ gswz16((lane >> 4) & 3));
-    const int slot = g ^ gswz16((l16 >> 2) & 3);
-    // hidden step i of the pass walks quarter (i + 2 + 2 HF) & 3: the other half's quarters first, its own last
-    auto hq = [&](int st) { return (st - nin + 2 + 2 * HF) & 3; };
-    // piece x = NPW w + e of a step fills image x >> 2 (plane q, gate gt), units 16 (x & 3) .. + 15 of the pass's
-    // half: W^T row q 3H + gt H + 64 HF + 16 (x & 3) + (lane >> 2), LDS bytes [1 KiB x, +1 KiB) of the buffer
-    auto issueW = [&](int st, int buf) {
-        const bool hid = st >= nin;
-        const int Kp = hid ? H : a.kxp;
-        const uint16_t *base = (hid ? a.whT + 32 * hq(st) : a.wiT + 32 * st);
-        const unsigned voff = lpart * (unsigned)Kp + chb;
-#pragma unroll
-        for (int e = 0; e < NPW; ++e) {
-            const int x = NPW * w + e, img = x >> 2, q = img / 3, gt = img - 3 * q;
-            const uint16_t *src = base + (size_t)(q * 3 * H + gt * H + HU * HF + 16 * (x & 3)) * Kp;
-            glds16_async_s(src, voff, &Bs[buf * NI * IMG + 64 * x]);
-        }
-    };
-    // activation DMA: 4 pieces per wave and step, piece e = rows wr + 8 e .. + 7 (lane -> row + (lane >> 3), LDS
-    // position lane & 7 holding chunk (lane & 7) ^ ((row >> 1) & 5)); rows past R read row R - 1, k past Kx a
-    // valid address (zeroed at the split)
-    auto issueA = [&](int st) {
-        uint4 *dst = &As[(st % NSL) * ASL + 64 * 4 * w];
-        const bool hid = st >= nin;
-        const int k = st * 32;
-        if (row0 + TR <= a.R && (hid || k + 32 <= w0)) {
-            const int ld = hid ? a.ldp : a.seg_ld[0];
-            const float *b = (hid ? hp + 32 * hq(st) : sg0 + k) + (size_t)row0 * ld;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = wr + 8 * e + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 5);
-                glds16_async_s(b, (unsigned)(r * ld + 4 * c) * 4u, dst + 64 * e);
-            }
-            return;
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int r = wr + 8 * e + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 5);
-            const int rr = row0 + r, rc = rr < a.R ? rr : a.R - 1;
-            const float *src;
-            if (hid) {
-                src = hp + (size_t)rc * a.ldp + 32 * hq(st) + 4 * c;
-            } else {
-                const int kx = k + 4 * c;
-                if (kx < w0) src = sg0 + (size_t)rc * a.seg_ld[0] + kx;
-                else if (kx < w01) src = sg1 + (size_t)rc * a.seg_ld[1] + (kx - w0);
-                else if (kx < kx_end) src = sg2 + (size_t)rc * a.seg_ld[2] + (kx - w01);
-                else src = hp;  // padding k (zeroed at the split)
-            }
-            glds16_async(src, dst + 64 * e);
-        }
-    };
-    float amax = 0.f;  // largest |activation| this lane split (pass 0: the range check)
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    // split step st's activations of row tile rt from its slot (own rows)
-    auto lsplit = [&](int st, int rt, uint4 (&f)[2]) {
-        const int r = wr + 16 * rt + l16, sw = (r >> 1) & 5;
-        const uint4 *row = &As[(st % NSL) * ASL + 8 * r];
-        const int kx = st * 32 + 8 * g;
-        const bool z0 = st < nin && kx >= kx_end, z1 = st < nin && kx + 4 >= kx_end;
-        const f4v zero = {0.f, 0.f, 0.f, 0.f};
-        const float4 v0 = __builtin_bit_cast(float4, z0 ? zero : __builtin_bit_cast(f4v, row[(2 * g) ^ sw]));
-        const float4 v1 = __builtin_bit_cast(float4, z1 ? zero : __builtin_bit_cast(f4v, row[(2 * g + 1) ^ sw]));
-        if (HF == 0) {
-            const float m0 = fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w)));
-            const float m1 = fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w)));
-            amax = fmaxf(amax, fmaxf(m0, m1));
-        }
-        const SplitH8 sp = splith8(v0, v1);
-        f[0] = sp.p[0];
-        f[1] = sp.p[1];
-    };
-    f32x4g acc[4][4][2];
-#pragma unroll
-    for (int G = 0; G < 4; ++G)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt) acc[G][j][rt] = f32x4g{};
-    uint4 fas[2][2], fnx[2][2];
-    // prologue: activation steps 0, 1 and step 0's weights (pass 1: vmcnt(0) also retires pass 0's tape stores,
-    // draining under these loads)
-    issueA(0);
-    if (ns > 1) issueA(1);
-    issueW(0, 0);
-    wait_vmcnt<0>();
-    barrier_lds();
-    lsplit(0, 0, fas[0]);
-    lsplit(0, 1, fas[1]);
-    auto pstep = [&](int st, auto hidc) {
-        constexpr bool hid = decltype(hidc)::value;
-        const int buf = st & 1;
-        const bool late = w >= 4;
-        auto dma = [&]() {
-            if (st + 1 < ns) issueW(st + 1, buf ^ 1);
-            if (st + 2 < ns) issueA(st + 2);
-        };
-        if (!late) dma();
-        auto bfrag = [&](int n, int q) {
-            const int gt = n >> 2, j = n & 3;
-            return Bs[(buf * NI + q * 3 + gt) * IMG + (16 * j + l16) * 4 + slot];
-        };
-        constexpr int LA = 2;
-        uint4 bb[LA][2];
-#pragma unroll
-        for (int q = 0; q < LA; ++q) {
-            bb[q][0] = bfrag(q, 0);
-            bb[q][1] = bfrag(q, 1);
-        }
-#pragma unroll
-        for (int n = 0; n < 12; ++n) {
-            const int gt = n >> 2, j = n & 3;
-            const int G = gt < 2 ? gt : (hid ? 3 : 2);
-            uint4 &b0 = bb[n % LA][0], &b1 = bb[n % LA][1];
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt) {
-                f32x4g c = acc[G][j][rt];
-                c = h2mma(fas[rt][0], b1, c);  // a1 b2
-                c = h2mma(fas[rt][1], b0, c);  // a2 b1
-                c = h2mma(fas[rt][0], b0, c);  // a1 b1
-                acc[G][j][rt] = c;
-            }
-            if (n + LA < 12) {
-                b1 = bfrag(n + LA, 1);
-                b0 = bfrag(n + LA, 0);
-            }
-            if (n == 3 && st + 1 < ns) {
-                // this wave's DMA of step st + 1 (issued a step ago) has landed: all but the pieces it issued
-                // since (this step's weights, 3, and activations of st + 2, 4; none yet for waves 4..7)
-                if (late) wait_vmcnt<0>();
-                else if (st + 2 < ns) wait_vmcnt<7>();
-                else wait_vmcnt<3>();
-                lsplit(st + 1, 0, fnx[0]);
-                lsplit(st + 1, 1, fnx[1]);
-            }
-            if (late && n + 1 == kUDmaLate) dma();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // W(st + 1) landed in every wave (A(st + 2), issued last, may fly); then the buffers flip
-        if (st + 2 < ns) wait_vmcnt<4>();
-        else wait_vmcnt<0>();
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-            fas[rt][0] = fnx[rt][0];
-            fas[rt][1] = fnx[rt][1];
-        }
-        barrier_lds();
-    };
-    {
-        int st = 0;
-#pragma unroll 1
-        for (; st < nin; ++st) pstep(st, std::false_type{});
-#pragma unroll 1
-        for (; st < ns; ++st) pstep(st, std::true_type{});
-    }
-    const int nt128 = (a.R + 127) / 128;
-    if (HF == 0) {  // range check (every activation of the tile was split in pass 0): flags of both 128-row tiles
-        const bool wb = __ballot(!(amax < 32768.0f)) != 0;
-        if (lane == 0) wflag[w] = wb;
-        barrier_lds();
-        int bad = 0;
-#pragma unroll
-        for (int q = 0; q < NW; ++q) bad |= wflag[q];
-        if (t < 2 && 2 * tile + t < nt128) a.flags[2 * tile + t] = bad;
-        if (bad) {
-            wait_vmcnt<0>();
-            return false;
-        }
-    }
-    // ---- pass epilogue.  C/D map: unit 64 HF + 16 j + l16, row wr + 16 rt + 4 g + reg.
-    constexpr float sc = 1.0f / (float)(1 << kH2Shift);
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    constexpr float kL2E = 1.4426950408889634f;
-    auto exp2v = [](f2 x) { return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; };
-    auto rcpv = [](f2 x) { return f2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; };
-    const f2 one = {1.f, 1.f}, ml2e = {-kL2E, -kL2E}, m2l2e = {-2.f * kL2E, -2.f * kL2E}, two = {2.f, 2.f};
-    auto tanhv = [&](f2 x) {  // ftanh_fast on a row pair
-        const f2 u = x * x;
-        auto fm = [](f2 p, f2 q, f2 c) { return __builtin_elementwise_fma(p, q, c); };
-        f2 p = fm(u, f2{kTh5, kTh5}, f2{kTh4, kTh4});
-        p = fm(u, p, f2{kTh3, kTh3});
-        p = fm(u, p, f2{kTh2, kTh2});
-        p = fm(u, p, f2{kTh1, kTh1});
-        const f2 small = fm(x, u * p, x);
-        const f2 ax = {fabsf(x.x), fabsf(x.y)};
-        const f2 big = two * rcpv(one + exp2v(ax * m2l2e)) - one;
-        return f2{ax.x < kThCut ? small.x : copysignf(big.x, x.x), ax.y < kThCut ? small.y : copysignf(big.y, x.y)};
-    };
-    auto row16 = [lane](float v) {  // sum over the 16 lanes of a row group (xor butterfly by DPP)
-        auto dpp = [](float x, auto ctl) {
-            return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), decltype(ctl)::value,
-                                                                      0xF, 0xF, true));
-        };
-        v += dpp(v, std::integral_constant<int, 0xB1>{});
-        v += dpp(v, std::integral_constant<int, 0x4E>{});
-        {
-            const float up = dpp(v, std::integral_constant<int, 0x104>{});
-            const float dn = dpp(v, std::integral_constant<int, 0x114>{});
-            v += (lane & 4) ? dn : up;
-        }
-        {
-            const float up = dpp(v, std::integral_constant<int, 0x108>{});
-            const float dn = dpp(v, std::integral_constant<int, 0x118>{});
-            v += (lane & 8) ? dn : up;
-        }
-        return v;
-    };
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int u = HU * HF + 16 * j + l16;
-        const float br = a.bi[u] + a.bh[u], bz = a.bi[H + u] + a.bh[H + u];
-        const float bni = a.bi[2 * H + u], bnh = a.bh[2 * H + u];
-        const f32x4g s4 = {sc, sc, sc, sc};
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-            acc[0][j][rt] = acc[0][j][rt] * s4 + f32x4g{br, br, br, br};
-            acc[1][j][rt] = acc[1][j][rt] * s4 + f32x4g{bz, bz, bz, bz};
-            acc[2][j][rt] = acc[2][j][rt] * s4 + f32x4g{bni, bni, bni, bni};
-            acc[3][j][rt] = acc[3][j][rt] * s4 + f32x4g{bnh, bnh, bnh, bnh};
-        }
-    }
-    if (a.g4) {  // pre-activations of the pass's units, straight from the accumulators
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = row0 + wr + 16 * rt + 4 * g + r;
-                if (row < a.R) {
-                    float *q = a.g4 + (size_t)row * a.ldg + HU * HF + l16;
-#pragma unroll
-                    for (int G = 0; G < 4; ++G)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) q[G * H + 16 * j] = acc[G][j][rt][r];
-                }
-            }
-    }
-    // gates with h of the pass's units from the slots of its last two steps (own quarters 2 HF, 2 HF + 1)
-    f2 s1v[2][2], s2v[2][2];  // lane partial row sums [rt][row pair]
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) s1v[rt][p] = s2v[rt][p] = f2{0.f, 0.f};
-    const float *Af = reinterpret_cast<const float *>(As);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int kq = 16 * (j & 1) + l16, sb = ((nin + 2 + (j >> 1)) % NSL) * ASL;
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                float hv[2];
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int R = wr + 16 * rt + 4 * g + 2 * p + e;
-                    hv[e] = Af[4 * (sb + 8 * R + ((kq >> 2) ^ ((R >> 1) & 5))) + (kq & 3)];
-                }
-                const f2 rp = {acc[0][j][rt][2 * p], acc[0][j][rt][2 * p + 1]};
-                const f2 zp = {acc[1][j][rt][2 * p], acc[1][j][rt][2 * p + 1]};
-                const f2 gi = {acc[2][j][rt][2 * p], acc[2][j][rt][2 * p + 1]};
-                const f2 gh = {acc[3][j][rt][2 * p], acc[3][j][rt][2 * p + 1]};
-                const f2 h = {hv[0], hv[1]};
-                const f2 rg = rcpv(one + exp2v(rp * ml2e)), zg = rcpv(one + exp2v(zp * ml2e));
-                const f2 ng = tanhv(gi + rg * gh);
-                const f2 hn = (one - zg) * ng + zg * h;
-                acc[0][j][rt][2 * p] = hn.x;
-                acc[0][j][rt][2 * p + 1] = hn.y;
-                s1v[rt][p] += hn;
-                s2v[rt][p] += hn * hn;
-            }
-    }
-    // row sums over the pass's 64 units (butterfly over the row group's 16 lanes)
-    float s1[2][4], s2[2][4];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            s1[rt][r] = row16(r & 1 ? s1v[rt][r >> 1].y : s1v[rt][r >> 1].x);
-            s2[rt][r] = row16(r & 1 ? s2v[rt][r >> 1].y : s2v[rt][r >> 1].x);
-        }
-    if (HF == 0) {  // h' in registers and the row sums in LDS for pass 1; the slot reads done before it refills
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt) h0[j][rt] = acc[0][j][rt];
-        if (l16 == 0)
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) rsum[wr + 16 * rt + 4 * g + r] = make_float2(s1[rt][r], s2[rt][r]);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        return true;
-    }
-    // pass 1: LayerNorm over all 128 units of each row
-    float mean[2][4], rs[2][4];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float2 p0 = rsum[wr + 16 * rt + 4 * g + r];
-            const float t1 = p0.x + s1[rt][r], t2 = p0.y + s2[rt][r];
-            mean[rt][r] = t1 / (float)H;
-            const float var = fmaxf(t2 / (float)H - mean[rt][r] * mean[rt][r], 0.0f);
-            rs[rt][r] = rsqrtf(var + 1e-6f);
-        }
-    barrier_lds();  // every wave has read its slots: the stage below overwrites the weight buffers + slots
-    float *stage = reinterpret_cast<float *>(L) + w * 32 * SW;
-#pragma unroll
-    for (int half = 0; half < 2; ++half)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int u = HU * half + 16 * j + l16;
-            const float scl = a.ln_scale[u], lb = a.ln_bias[u];
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float hn = half ? acc[0][j][rt][r] : h0[j][rt][r];
-                    stage[(16 * rt + 4 * g + r) * SW + u] = (hn - mean[rt][r]) * (rs[rt][r] * scl) + lb;
-                }
-        }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own stage rows (no workgroup barrier)
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-        const int rr = 2 * it + (lane >> 5), c4 = lane & 31;
-        const float4 v = *reinterpret_cast<const float4 *>(stage + rr * SW + 4 * c4);
-        const int row = row0 + wr + rr;
-        if (row < a.R) *reinterpret_cast<float4 *>(a.out + (size_t)row * a.ldo + 4 * c4) = v;
-    }
-    return true;
-}
-
-__device__ __forceinline__ void gru_h2u_tile(const GruX3rArgs &a, int tile) {
-    if (a.wbad[0] | a.wbad[1]) {  // weights out of fp16 range: the bf16x3 launch does every tile
-        const int nt128 = (a.R + 127) / 128;
-        if (threadIdx.x < 2 && 2 * tile + (int)threadIdx.x < nt128) a.flags[2 * tile + threadIdx.x] = 1;
-        return;
-    }
-    f32x4g h0[4][2];  // pass 0's unnormalised h' (units 16 j + l16, rows wr + 16 rt + 4 g + reg)
-    if (!gru_h2u_pass<0>(tile, h0)) return;
-    gru_h2u_pass<1>(tile, h0);
-}
-
-// LDS of the unit-half kernel (bytes): weight buffers + activation slots, the pass-0 row sums, the range flags
-constexpr size_t kH2uLds = (size_t)(2 * 6 * 256 + 3 * 256 * 8 + 128 + 2) * 16;
-
-__global__ void __launch_bounds__(512, 1) gru_ln_fused_fwd_h2u_kernel(GruX3rArgs a) { gru_h2u_tile(a, blockIdx.x); }
-
 // bf16x3 register-A kernel (the fp16x2 kernel above is fp16x2-only: instantiated for bf16x3 it computed
 // wrong results; this is the round-1 kernel).  Activations loaded two steps ahead into registers, weight
 // fragments carried across column blocks, tape stored from the accumulators.
@@ -1585,16 +1185,8 @@ extern "C" int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w
     a.flags = tile_flags;
     a.wbad = wbad;
     const int tiles = (R + 127) / 128;
-    // MARLSAT_GRU_FORM=h2u: the unit-half kernel (256-row tiles, two passes); default h2s (128 x 128 tiles)
-    const char *form = getenv("MARLSAT_GRU_FORM");
-    if (form && form[0] == 'h' && form[1] == '2' && form[2] == 'u') {
-        hipLaunchKernelGGL(gru_ln_fused_fwd_h2u_kernel, dim3((R + 255) / 256), dim3(512), kH2uLds, (hipStream_t)stream,
-                           a);
-        rc = check_launch("gru_ln_fused_fwd_h2u_kernel");
-    } else {
-        hipLaunchKernelGGL(gru_ln_fused_fwd_h2s_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
-        rc = check_launch("gru_ln_fused_fwd_h2s_kernel");
-    }
+    hipLaunchKernelGGL(gru_ln_fused_fwd_h2s_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, a);
+    rc = check_launch("gru_ln_fused_fwd_h2s_kernel");
     if (rc) return rc;
     a.wiT = reinterpret_cast<const uint16_t *>(wiT_x3);
     a.whT = reinterpret_cast<const uint16_t *>(whT_x3);

@@ -183,6 +183,10 @@ def _load():
 
 
 lib = _load()
+ABI_VERSION = 2  # msat_version() of the header this binding follows (msat_step_out with clock_stamps)
+if lib.msat_version() != ABI_VERSION:
+    raise ImportError(f"marlsat: {LIB_PATH} has C-ABI version {lib.msat_version()}, this binding needs {ABI_VERSION}; "
+                      "rebuild it (make -C marl-sat_amd)")
 
 _probe = None
 
@@ -298,6 +302,17 @@ def ptr(t) -> int | None:
     """Device pointer of a tensor (None for None)."""
     if t is None:
         return None
+    return t.data_ptr()
+
+
+def stamps_ptr(t, num_envs: int) -> int | None:
+    """Device pointer of an optional msat_step_out.clock_stamps buffer: int64, contiguous, at least 8 words per
+    env (include/marlsat.h: (B, 8)); the kernel writes all eight, so a smaller buffer is refused here."""
+    if t is None:
+        return None
+    if t.dtype not in (torch.int64, torch.uint64) or not t.is_contiguous() or t.numel() < 8 * num_envs:
+        raise ValueError(f"clock_stamps must be a contiguous int64 tensor of >= 8 * {num_envs} elements ((B, 8)), "
+                         f"got {tuple(t.shape)} {t.dtype}")
     return t.data_ptr()
 
 

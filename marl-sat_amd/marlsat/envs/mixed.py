@@ -82,7 +82,7 @@ class MixedSATEnv:
         couts = (_lib.StepOutC * G)(*[
             _lib.StepOutC(o["reward"].data_ptr(), o["done"].data_ptr(), o["solved"].data_ptr(),
                           o["num_unsatisfied"].data_ptr(), o["episode_step"].data_ptr(),
-                          _lib.ptr(o.get("clock_stamps"))) for o in outs])
+                          _lib.stamps_ptr(o.get("clock_stamps"), b)) for o, b in zip(outs, sizes)])
         cact = (ctypes.c_void_p * G)()
         fn = _lib.lib.msat_env_step_grouped
         s = _lib.stream_ptr(self.device)

@@ -372,7 +372,7 @@ class SATEnv:
         k = as_key(key)
         so = _lib.StepOutC(out["reward"].data_ptr(), out["done"].data_ptr(), out["solved"].data_ptr(),
                            out["num_unsatisfied"].data_ptr(), out["episode_step"].data_ptr(),
-                           _lib.ptr(out.get("clock_stamps")))
+                           _lib.stamps_ptr(out.get("clock_stamps"), B))
         _lib.check(_lib.lib.msat_env_step(self._desc(B, state.pool), state.pool.c(self), state._c(),
                                           a.data_ptr(), 1 if autoreset else 0, _lib.ptr(pidx), _lib.ptr(x), k.seed,
                                           k.counter, so, _lib.ptr(obs), _lib.stream_ptr(self.device)),
@@ -387,10 +387,10 @@ class SATEnv:
         B = state.num_envs
         desc = self._desc(B, state.pool)
         cst = state._c()
-        # out["clock_stamps"] (optional, (B, 2) int64): the kernel's diagnostic clock stamps (bench.py)
+        # out["clock_stamps"] (optional, (B, 8) int64): the kernel's diagnostic clock stamps (bench.py)
         so = _lib.StepOutC(out["reward"].data_ptr(), out["done"].data_ptr(), out["solved"].data_ptr(),
                            out["num_unsatisfied"].data_ptr(), out["episode_step"].data_ptr(),
-                           _lib.ptr(out.get("clock_stamps")))
+                           _lib.stamps_ptr(out.get("clock_stamps"), B))
         fn = _lib.lib.msat_env_step
         cpool = state.pool.c(self)
         obs_p, s = obs.data_ptr(), _lib.stream_ptr(self.device)

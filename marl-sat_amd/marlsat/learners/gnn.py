@@ -443,7 +443,8 @@ class GNNActorCritic:
     # (forward, input-gradient and weight-gradient) disappear and the weight gradients of
     # phi / Wi are recovered from dF once per backward (_unfuse_grads).  Same function,
     # different fp32 association: parity is the 1e-5 fp32 bar, not bitwise.
-    fuse_phi = os.environ.get("MARLSAT_FUSE_PHI", "1") != "0"
+    # the fp32 path is the reference's operation order: phi stays unfolded there unless MARLSAT_FUSE_PHI says so
+    fuse_phi = os.environ.get("MARLSAT_FUSE_PHI", "0" if PRECISION == "fp32" else "1") != "0"
 
     def _fold_views(self):
         """Views of the folded matrices F_c (2H+4 rows), F_v+, F_v- (H+8 rows) and of their gradients
@@ -971,3 +972,33 @@ class GNNActorCritic:
                                   self.adam_v.data_ptr(), self.size, float(lr), b1, b2, eps, self.adam_count,
                                   float(grad_scale), first_bad.data_ptr() if first_bad is not None else None,
                                   self.stream), "adam")
+
+
+def path_switches(precision: str) -> dict:
+    """GNNActorCritic's kernel-path switches for one MARLSAT_PRECISION value (README "Kernel-path switches"):
+    'fp16x2' = phi folded, fp16x2 GRU forward and data / weight gradients (bf16x3 fixups); 'bf16x3' = phi
+    folded, the bf16x3 kernels throughout; 'fp32' = fp32 MFMA kernels in the reference's operation order
+    (phi not folded)."""
+    if precision not in PRECISION_CODES:
+        raise ValueError(f"precision must be one of {sorted(PRECISION_CODES)}, got {precision!r}")
+    split, h2 = precision != "fp32", precision == "fp16x2"
+    return {"fuse_phi": split, "use_x3": split, "use_gru_x3": split, "use_gru_h2": h2, "use_dgrad_h2": h2,
+            "use_wgrad_h2": h2}
+
+
+def set_precision(precision: str) -> dict:
+    """Switch the process's matrix arithmetic (the class switches above and the library's weight-gradient path,
+    msat_set_precision) to one precision path; returns the previous switches (restore_precision undoes it)."""
+    prev = {k: getattr(GNNActorCritic, k) for k in path_switches(precision)}
+    prev["_code"] = int(L_.msat_get_precision())
+    for k, v in path_switches(precision).items():
+        setattr(GNNActorCritic, k, v)
+    _lib.check(L_.msat_set_precision(PRECISION_CODES[precision]), "msat_set_precision")
+    return prev
+
+
+def restore_precision(prev: dict) -> None:
+    for k, v in prev.items():
+        if k != "_code":
+            setattr(GNNActorCritic, k, v)
+    _lib.check(L_.msat_set_precision(prev["_code"]), "msat_set_precision")

@@ -60,6 +60,13 @@ def test_host_cpu_record(monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "2")
     h = bench.host_cpu()
     assert h["cores"] == min(2, h["affinity_cores"]) and h["cap_source"] == "OMP_NUM_THREADS"
+    # the cgroup's CPU quota bounds the cores reported, however many the affinity mask shows (the GPU box:
+    # 256 in the mask, 16 in the quota)
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    monkeypatch.setattr(bench, "cgroup_cpus", lambda: 1.0)
+    h = bench.host_cpu()
+    assert h["cores"] == 1 and h["cgroup_cpus"] == 1.0
+    assert h["cap_source"] == ("cgroup quota" if h["affinity_cores"] > 1 else "affinity")
 
 
 def test_world_from_torchrun_without_gpus_flag():

@@ -21,9 +21,24 @@ LIBDIR = os.path.join(ROOT, "marl-sat_amd", "marlsat", "lib")
 ASAN_BIN = os.path.join(ROOT, "marl-sat_amd", "build", "asan", "capi_host_check")
 
 
+STATUS = os.path.join(LIBDIR, "debug_build_status.json")  # written by __graft_entry__.build()
+
+
+def _require_built(path, what):
+    """Skip only when no build ran here (no status record); a build() whose 'make debug' failed is a failure,
+    not a skip, so a broken debug build cannot silently drop the device bounds checks' coverage."""
+    if os.path.exists(path):
+        return
+    if os.path.exists(STATUS):
+        import json
+
+        st = json.load(open(STATUS))
+        pytest.fail(f"{what} missing: __graft_entry__.build()'s 'make debug' exited {st.get('make_debug_rc')}")
+    pytest.skip(f"{what} not built (make -C marl-sat_amd debug; __graft_entry__.build() does)")
+
+
 def test_capi_host_glue_under_asan():
-    if not os.path.exists(ASAN_BIN):
-        pytest.skip("ASan driver not built (make -C marl-sat_amd debug; __graft_entry__.build() does)")
+    _require_built(ASAN_BIN, "ASan driver build/asan/capi_host_check")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=23")
     r = subprocess.run([ASAN_BIN], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -60,8 +75,7 @@ def test_debug_library_checks_the_gru_backward():
     from marlsat import _lib
 
     path = os.path.join(LIBDIR, "libmarlsat_debug.so")
-    if not os.path.exists(path):
-        pytest.skip("libmarlsat_debug.so not built")
+    _require_built(path, "libmarlsat_debug.so")
     dbg = ctypes.CDLL(path)
     for lib in (dbg,):
         lib.msat_gru_ln_bwd_g4fe.restype = ctypes.c_int32
@@ -147,8 +161,7 @@ def test_debug_library_runs_a_train_cycle():
     import sys
 
     path = os.path.join(LIBDIR, "libmarlsat_debug.so")
-    if not os.path.exists(path):
-        pytest.skip("libmarlsat_debug.so not built")
+    _require_built(path, "libmarlsat_debug.so")
     env = dict(os.environ, MARLSAT_LIB=path, MARLSAT_DEBUG="1")
     r = subprocess.run([sys.executable, "-c", TRAIN_SCRIPT.format(root=ROOT)], capture_output=True, text=True,
                        timeout=600, env=env)

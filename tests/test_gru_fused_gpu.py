@@ -116,17 +116,14 @@ def _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout="plain"):
 def _fwd_cases():
     """(layout, H, R): the fp32 kernel at H 64 / 128 / 256, the register-A bf16x3 and fp16x2 kernels at
     H 128; the 70,000-row case at the production width H = 128 only."""
-    widths = {"plain": (64, 128, 256), "x3r": (128,), "h2r": (128,), "h2u": (128,)}
+    widths = {"plain": (64, 128, 256), "x3r": (128,), "h2r": (128,)}
     return [(lay, H, R) for lay, hs in widths.items() for H in hs for R in (0, 1, 77, 1000, 70000)
             if R != 70000 or H == 128]
 
 
 @pytest.mark.parametrize("layout,H,R", _fwd_cases())
 @pytest.mark.parametrize("kind", ["var", "clause", "var8", "clause4"])
-def test_fused_forward_matches_reference(R, H, kind, layout, monkeypatch):
-    if layout == "h2u":  # the fp16x2 kernel's unit-half form (256-row tiles, two passes over the units)
-        monkeypatch.setenv("MARLSAT_GRU_FORM", "h2u")
-        layout = "h2r"
+def test_fused_forward_matches_reference(R, H, kind, layout):
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=R + H)
     g4 = torch.full((R, 4 * H), float("nan"), device="cuda")
     out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, layout)
@@ -148,16 +145,13 @@ def test_fused_forward_matches_reference(R, H, kind, layout, monkeypatch):
     assert bool((terr <= 2e-6 * ab + 1e-30).all()), float((terr / (ab + 1e-30)).max())
 
 
-@pytest.mark.parametrize("form", ["h2s", "h2u"])
 @pytest.mark.parametrize("R,bad_tiles", [(1000, (1, 6)), (70000, (0, 300, 546))])
 @pytest.mark.parametrize("kind", ["var8", "clause4"])
-def test_h2r_out_of_range_tiles_take_the_bf16x3_path(kind, R, bad_tiles, form, monkeypatch):
+def test_h2r_out_of_range_tiles_take_the_bf16x3_path(kind, R, bad_tiles):
     """fp16x2 range check: activations with |a| >= 2^15 in a row flag exactly its 128-row tile, which the
     fixup launch recomputes in bf16x3 (bitwise the x3r kernel's rows there), the other tiles keep the
     fp16x2 result; weights with |W| >= 32 flag the split and every tile is bf16x3.  70,000 rows: the first
-    tile, one in the middle and the last, partial tile (546).  h2u (256-row tiles) flags both 128-row tiles of a
-    256-row tile that holds an out-of-range activation: those rows are the bf16x3 kernel's."""
-    monkeypatch.setenv("MARLSAT_GRU_FORM", form)
+    tile, one in the middle and the last, partial tile (546)."""
     H = 128
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=3)
     for i, t in enumerate(bad_tiles):
@@ -167,7 +161,7 @@ def test_h2r_out_of_range_tiles_take_the_bf16x3_path(kind, R, bad_tiles, form, m
     out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, "h2r")
     flags, bad = _fwd.last_flags
     assert bad.tolist() == [0, 0]
-    flagged = set(bad_tiles) if form == "h2s" else {2 * (t // 2) + k for t in bad_tiles for k in (0, 1)}
+    flagged = set(bad_tiles)
     assert flags.tolist() == [1 if t in flagged else 0 for t in range((R + 127) // 128)]
     g4x = torch.empty(R, 4 * H, device="cuda")
     ox = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4x, "x3r")

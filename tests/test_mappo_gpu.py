@@ -167,8 +167,20 @@ TRAIN_CYCLE_CASES = [
 ]
 
 
+@pytest.fixture
+def precision_path(request):
+    """Runs the test on one precision path (marlsat.learners.gnn.set_precision: the class switches and the
+    library's weight-gradient path) and restores the process's own afterwards."""
+    from marlsat.learners import gnn
+
+    prev = gnn.set_precision(request.param)
+    yield request.param
+    gnn.restore_precision(prev)
+
+
+@pytest.mark.parametrize("precision_path", ["fp16x2", "bf16x3", "fp32"], indirect=True)
 @pytest.mark.parametrize("V,C,vpa,H,L,mode,shape", TRAIN_CYCLE_CASES)
-def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode, shape):
+def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode, shape, precision_path):
     """Teacher-forced replay of a whole train cycle: for every Adam step the oracle starts from the
     parameters the device started from (recorded by ``MAPPOLearner.trace``), so each minibatch is
     checked at the north_star bar without the drift of an independent replay (next test):
@@ -178,7 +190,9 @@ def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode, shape
         factors of the network depth tests, tests/test_gnn_gpu.py; round 3 allowed 4x / 8x);
       * the Adam step: the device's new parameters vs optax.adam applied in float64 to the device's
         own gradient (1e-5 relative).
-    Mode 1 runs with a padded slot: the parameters must stay finite (the slot counts as 0)."""
+    Mode 1 runs with a padded slot: the parameters must stay finite (the slot counts as 0).
+    Every case runs on each precision path the README offers (fp16x2 = the default, bf16x3, fp32 = fp32 MFMA
+    in the reference's operation order); the margins each path printed are in profiles/r06/."""
     from marlsat import SATEnv
     from marlsat.learners.gnn import GNNActorCritic
     from marlsat.learners.mappo_gnn_sat_learner import MAPPOLearner
@@ -232,7 +246,7 @@ def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode, shape
           f"{np.array2string(np.abs(v32 - v64), precision=2)}, |value| {np.array2string(np.abs(v64), precision=3)}")
     rl = _yard_close(flat(tr["log_prob"]), lp64, lp32, 2.0, "rollout log_prob")
     rv = _yard_close(vdev, v64, v32, 2.0, "rollout value")
-    print(f"margins V{V} C{C} A{A} H{H} L{L} mode{mode} rollout: log_prob worst ratio {rl:.3g}, value worst ratio {rv:.3g}")
+    print(f"margins {precision_path} V{V} C{C} A{A} H{H} L{L} mode{mode} rollout: log_prob worst ratio {rl:.3g}, value worst ratio {rv:.3g}")
     adv, tgt = om.gae(tr["reward"], tr["value"], tr["done"].astype(bool), learner.last_val.cpu().numpy(),
                       cfg["GAMMA"], cfg["GAE_LAMBDA"])
     np.testing.assert_allclose(learner.targets.cpu().numpy(), tgt, rtol=1e-5, atol=1e-7)
@@ -296,19 +310,28 @@ def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode, shape
                                        f"(err {err_l[0]:.3g} > {strict[0]:.3g}) but the fp32 oracle's is within "
                                        f"1e-5 ({e32_l:.3g})")
         g_dev = layout(rec["grads"])
-        gw, gk = 0.0, ""
+        ratios = {}
         for k in P_s:
             g64, g32, g32r = out["f64"][1][k], out["f32"][1][k], out["f32r"][1][k]
             yard = np.where(np.abs(g32r - g64) > np.abs(g32 - g64), g32r, g32)  # elementwise, then max in _yard_close
-            r = _yard_close(g_dev[k], g64, yard, 4.0, f"step {s} grad {k}", extra=kink[k])
-            if r >= gw:
-                gw, gk = r, k
+            ratios[k] = _yard_close(g_dev[k], g64, yard, 4.0, f"step {s} grad {k}", extra=kink[k])
+        top = sorted(ratios.items(), key=lambda kv: -kv[1])[:3]
+        gw, gk = top[0][1], top[0][0]
+        # the worst tensor's worst element: its error, the strict part of its bar and the fp32 yardstick E32
+        g64w = out["f64"][1][gk]
+        e32w = max(np.abs(out["f32"][1][gk] - g64w).max(), np.abs(out["f32r"][1][gk] - g64w).max())
+        errw = np.abs(np.asarray(g_dev[gk], np.float64) - g64w)
+        kw = np.broadcast_to(np.asarray(kink[gk], np.float64), g64w.shape)
+        iw = int(np.argmax(errw / (1e-5 * np.abs(g64w) + 4.0 * e32w + kw + 1e-300)))
+        print(f"  worst {gk}[{iw}]: err {errw.flat[iw]:.3g}, ref {g64w.flat[iw]:.3g}, 1e-5|ref| "
+              f"{1e-5 * abs(g64w.flat[iw]):.3g}, E32 {e32w:.3g} (max |ref| {np.abs(g64w).max():.3g}), "
+              f"kink {kw.flat[iw]:.3g}")
         # margins (printed; profiles/r05*_parity_margins.log): each loss's error over its strict 1e-5 bar and
         # over the bar applied; the worst gradient tensor's error over its bar (1.0 = at the bar)
-        print(f"margins V{V} C{C} A{A} H{H} L{L} mode{mode} step {s}: loss err/strict "
+        print(f"margins {precision_path} V{V} C{C} A{A} H{H} L{L} mode{mode} step {s}: loss err/strict "
               f"{np.array2string(err_l / strict, precision=3)} err/bound {np.array2string(err_l / bound_l, precision=3)} "
               f"value allowance used {used} (fp32 oracle value-loss err/strict {e32_l / strict[0]:.3g}); "
-              f"grad worst ratio {gw:.3g} ({gk})")
+              f"grad worst ratio {gw:.3g} ({gk}); next {', '.join(f'{k} {r:.3g}' for k, r in top[1:])}")
         # optax.adam in float64 on the device's own gradient, from the device's own parameters
         gflat = rec["grads"].double().cpu()
         if m_st["m"] is None:
