@@ -735,6 +735,7 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
     # as in a long-running rollout (solved envs reset on top of that)
     for st in states:
         st.step.copy_(torch.randint(0, 512, (st.num_envs,), generator=gen, device="cuda", dtype=torch.int32))
+        st.invalidate_reset_queue()  # the counters were written directly: the listed timed-out envs are stale
     for i in range(args.warmup):
         step(i, counter)
         counter += 1

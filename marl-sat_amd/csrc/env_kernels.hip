@@ -43,9 +43,49 @@ struct EnvParams {
     // debug builds (MSAT_DCHECK): elements from each caller buffer's pointer to the end of its allocation
     // (dbg_extent); 0 in product builds
     long long dbg_obs, dbg_assign, dbg_sat, dbg_ntrue, dbg_actions;
+    // reset queue (msat_env_state.reset_queue): 0 none; 1 this autoreset launch consumes the list the previous
+    // one made and makes the next one's (launch B + rq_cap workgroups); 2 the launch clears the entries of the
+    // envs it modifies (the other state-modifying calls)
+    int rq_mode, rq_cap;
+    uint32_t rq_serial;
 };
 
 enum : int { kModeReset = 0, kModeStep = 1, kModeStepAutoReset = 2, kModeObs = 3 };
+
+// Reset queue layout (uint32 words): [0, 4) two uint64 claim words {token << 32 | count}, one per parity;
+// [4, 4 + 2B) the pending token of each env, per parity; then [2][cap] env lists.  The launch with serial s
+// reads parity s & 1 (entries whose token is rq_token(s)) and writes parity (s + 1) & 1 with rq_token(s + 1):
+// the two are never the same words within a launch.  Tokens have bit 31 set, so a zeroed queue lists nothing.
+__host__ __device__ __forceinline__ uint32_t rq_token(uint32_t serial) { return 0x80000000u | (serial & 0x7FFFFFFFu); }
+__host__ __device__ __forceinline__ int rq_capacity(int B) { return B / 256 + 8; }  // ~B/512 time out per launch
+__host__ __device__ __forceinline__ size_t rq_words(int B) { return 4 + 2 * (size_t)B + 2 * (size_t)rq_capacity(B); }
+
+struct ResetQueue {
+    uint64_t *cnt;
+    uint32_t *pend;
+    int32_t *list;
+    int B, cap;
+    __device__ __forceinline__ ResetQueue(uint32_t *q, int B_, int cap_) : B(B_), cap(cap_) {
+        cnt = reinterpret_cast<uint64_t *>(q);
+        pend = q + 4;
+        list = reinterpret_cast<int32_t *>(q + 4 + 2 * (size_t)B_);
+    }
+    __device__ __forceinline__ uint32_t *pend_of(int par) const { return pend + (size_t)par * B; }
+    __device__ __forceinline__ int32_t *list_of(int par) const { return list + (size_t)par * cap; }
+    // a slot in parity par's list for this launch's token: the claim word restarts at 0 when it still holds an
+    // older launch's token (device-scope compare-and-swap; a handful of claimants per launch)
+    __device__ __forceinline__ int claim(int par, uint32_t tok) const {
+        uint64_t *w = cnt + par;
+        uint64_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+            const uint32_t c = (uint32_t)(old >> 32) == tok ? (uint32_t)old : 0u;
+            const uint64_t nw = ((uint64_t)tok << 32) | (uint64_t)(c + 1u);
+            if (__hip_atomic_compare_exchange_strong(w, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT))
+                return (int)c;
+        }
+    }
+};
 
 __host__ __device__ __forceinline__ int agent_lo(const EnvParams &p, int i) { return i * p.base + (i < p.rem ? i : p.rem); }
 __host__ __device__ __forceinline__ int agent_size(const EnvParams &p, int i) { return p.base + (i < p.rem ? 1 : 0); }
@@ -129,7 +169,7 @@ __device__ __forceinline__ void clause_slice(const EnvParams &p, const EnvLds &l
         }
         sat = ntrue ? 1u : 0u;
         if (kPbrs) old = sat_g[c];
-        sat_g[c] = (uint8_t)sat;
+        if (sat_g) sat_g[c] = (uint8_t)sat;  // NULL: a step whose reset another workgroup does (reset queue)
         if (ntrue_g) ntrue_g[c] = (uint8_t)ntrue;
     }
     const uint64_t ms = __ballot(sat);
@@ -326,6 +366,101 @@ struct ClockStamp {
     }
 };
 
+// The prefetch of an instance's pool row and agent tables into this lane's registers (one round trip).
+template <int T>
+__device__ __forceinline__ void prefetch_instance(const EnvParams &p, const msat_pool &pool, int n,
+                                                  uint64_t (&w)[kPfClause], uint32_t (&rl)[kPfRel],
+                                                  uint32_t (&nb)[kPfNbr]) {
+    const int tid = threadIdx.x;
+    const uint64_t *prow = reinterpret_cast<const uint64_t *>(pool.lits) + (size_t)n * p.C;
+    const uint32_t *rel_g = pool.rel + (size_t)n * p.A * p.WC;
+    const uint32_t *nbr_g = pool.nbr + (size_t)n * p.A * p.WV;
+#pragma unroll
+    for (int j = 0; j < kPfClause; ++j) {
+        const int c = tid + j * T;
+        w[j] = c < p.C ? prow[c] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kPfRel; ++j) {
+        const int t = tid + j * T;
+        rl[j] = t < p.A * p.WC ? rel_g[t] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kPfNbr; ++j) {
+        const int t = tid + j * T;
+        nb[j] = t < p.A * p.WV ? nbr_g[t] : 0u;
+    }
+}
+
+// The instance a reset of env b draws (env:158-162 via the rollout's reset, learner:426-436): the caller's index,
+// or Philox word block 0 of (seed, ctr, env).
+__device__ __forceinline__ int reset_instance(const EnvParams &p, const int32_t *__restrict__ new_pidx, uint64_t seed,
+                                              uint64_t ctr, int b) {
+    if (new_pidx != nullptr) return new_pidx[b];
+    const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 0u);
+    return (int)(((uint64_t)r.x * (uint64_t)p.N) >> 32);
+}
+
+// The assignment a reset of env b draws into l.x: the caller's bytes, or word t = lane t % 4 of the Philox block
+// 1 + t / 4 (128 vars per block).
+template <int T>
+__device__ __forceinline__ void reset_assignment(const EnvParams &p, const EnvLds &l,
+                                                 const uint8_t *__restrict__ new_assign, uint64_t seed, uint64_t ctr,
+                                                 int b) {
+    if (new_assign != nullptr) {
+        load_x_bits<T>(p, l, new_assign + (size_t)b * p.V);
+        return;
+    }
+    for (int t = threadIdx.x; t < p.WV; t += T) {
+        const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 1u + (uint32_t)(t >> 2));
+        const int lane = t & 3;
+        uint32_t w = lane == 0 ? r.x : lane == 1 ? r.y : lane == 2 ? r.z : r.w;
+        const int hi = p.V - 32 * t;
+        if (hi < 32) w &= hi <= 0 ? 0u : ((1u << hi) - 1u);
+        l.x[t] = w;
+    }
+}
+
+// Stage instance pidx's agent tables in LDS (the first kPf* words from this lane's prefetch registers when pf),
+// build the obs bit images and stream the env's (A, D) block.
+template <typename ObsT, int T>
+__device__ __forceinline__ void stage_and_write_obs(const EnvParams &p, const EnvLds &l, const msat_pool &pool,
+                                                    int pidx, bool pf, const uint32_t (&prel)[kPfRel],
+                                                    const uint32_t (&pnbr)[kPfNbr], ObsT *__restrict__ o,
+                                                    const ClockStamp *cs) {
+    const int tid = threadIdx.x;
+    {
+        const uint32_t *rel_g = pool.rel + (size_t)pidx * p.A * p.WC;
+        const uint32_t *nbr_g = pool.nbr + (size_t)pidx * p.A * p.WV;
+        int t0r = 0, t0n = 0;
+        if (pf) {
+#pragma unroll
+            for (int j = 0; j < kPfRel; ++j)
+                if (tid + j * T < p.A * p.WC) l.rel[tid + j * T] = prel[j];
+#pragma unroll
+            for (int j = 0; j < kPfNbr; ++j)
+                if (tid + j * T < p.A * p.WV) l.nbr[tid + j * T] = pnbr[j];
+            t0r = kPfRel * T;
+            t0n = kPfNbr * T;
+        }
+        for (int t = t0r + tid; t < p.A * p.WC; t += T) l.rel[t] = rel_g[t];
+        for (int t = t0n + tid; t < p.A * p.WV; t += T) l.nbr[t] = nbr_g[t];
+        for (int t = tid; t < 2 * obs_image_words(p); t += T) l.fm[t] = 0u;  // fm, fx contiguous
+    }
+    lds_barrier();
+    if (cs) cs->mark(3);
+    if ((p.ablate & 3) == 0) {
+        build_obs_images<T>(p, l);
+        lds_barrier();
+        if (cs) cs->mark(4);
+        write_obs<T, ObsT>(p, l, o);
+    } else {
+        constexpr int VEC = ObsVec<ObsT>::N;
+        const int n = (p.A * p.D) / VEC;
+        for (int q = tid; q < n; q += T) ObsVec<ObsT>::store(o + q * VEC, 0u, 0u);
+    }
+}
+
 // One environment (index b of its batch) advanced / reset / observed by one workgroup.
 template <int MODE, typename ObsT, int T>
 __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &pool, const msat_env_state &st,
@@ -341,19 +476,27 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
     uint8_t *__restrict__ sat_g = st.clause_sat + (size_t)b * p.C;
     uint8_t *__restrict__ ntrue_g = st.clause_ntrue ? st.clause_ntrue + (size_t)b * p.C : nullptr;
     if (tid < 16) l.red[tid] = 0;
+    // reset queue: rq_fast = this autoreset launch consumes / produces it; rq_mode 2 = clear this env's entries
+    const bool rq_fast = MODE == kModeStepAutoReset && p.rq_mode == 1;
+    const ResetQueue rq(st.reset_queue, p.B, p.rq_cap);
+    if (MODE != kModeObs && p.rq_mode == 2 && tid == 0) {
+        rq.pend_of(0)[b] = 0u;
+        rq.pend_of(1)[b] = 0u;
+    }
 
     bool do_reset = (MODE == kModeReset);
     // the per-lane loads that do not depend on problem_idx, issued together with it (one round trip): this
-    // lane's action and its assignment byte of the first ballot pass (clamped indices, no branches);
-    // problem_idx last, so that waiting for it retires the group.  (step / unsat are wave-uniform values the
-    // compiler moves to scalar registers as soon as they are loaded, which would wait for them: they go
-    // with the second round trip.)
+    // lane's action and its assignment byte of the first ballot pass (clamped indices, no branches), and this
+    // env's entry of the reset queue; problem_idx last, so that waiting for it retires the group.  (step / unsat
+    // are wave-uniform values the compiler moves to scalar registers as soon as they are loaded, which would
+    // wait for them: they go with the second round trip.)
     int step0 = 0, u_old = 0, a0 = 0;
-    uint32_t x0 = 0;
+    uint32_t x0 = 0, pend = 0;
     if (MODE != kModeReset) {
         if (MODE != kModeObs && p.action_mode == 0) a0 = actions[(size_t)b * p.A + min(tid, p.A - 1)];
         x0 = xg[min(tid, p.V - 1)];
     }
+    if (rq_fast) pend = rq.pend_of(p.rq_serial & 1)[b];
     int pidx = st.problem_idx[b];
     if (MSAT_DEBUG_BUILD && tid == 0) {  // this env's rows of every caller buffer, and its pool row
         if (MODE != kModeReset) MSAT_DCHECK(pidx, p.N);
@@ -364,39 +507,13 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         if (MODE == kModeStep || MODE == kModeStepAutoReset)
             MSAT_DCHECK((long long)(b + 1) * p.A * (p.action_mode == 0 ? 1 : p.M) - 1, p.dbg_actions);
     }
-    // the prefetch of an instance's pool row and agent tables into this lane's registers
-    auto prefetch = [&](int n, uint64_t (&w)[kPfClause], uint32_t (&rl)[kPfRel], uint32_t (&nb)[kPfNbr]) {
-        const uint64_t *prow = reinterpret_cast<const uint64_t *>(pool.lits) + (size_t)n * p.C;
-        const uint32_t *rel_g = pool.rel + (size_t)n * p.A * p.WC;
-        const uint32_t *nbr_g = pool.nbr + (size_t)n * p.A * p.WV;
-#pragma unroll
-        for (int j = 0; j < kPfClause; ++j) {
-            const int c = tid + j * T;
-            w[j] = c < p.C ? prow[c] : 0ull;
-        }
-#pragma unroll
-        for (int j = 0; j < kPfRel; ++j) {
-            const int t = tid + j * T;
-            rl[j] = t < p.A * p.WC ? rel_g[t] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < kPfNbr; ++j) {
-            const int t = tid + j * T;
-            nb[j] = t < p.A * p.WV ? nbr_g[t] : 0u;
-        }
-    };
-    // the instance a reset draws (env:158-162 via the rollout's reset, learner:426-436): the caller's index, or
-    // Philox word block 0 of (seed, ctr, env)
-    auto reset_instance = [&]() -> int {
-        if (new_pidx != nullptr) return new_pidx[b];
-        const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 0u);
-        return (int)(((uint64_t)r.x * (uint64_t)p.N) >> 32);
-    };
+    // a reset workgroup of this launch resets this env (it times out now: listed by the previous launch)
+    const bool covered = rq_fast && pend == rq_token(p.rq_serial);
     uint64_t pw[kPfClause];
     uint32_t prel[kPfRel], pnbr[kPfNbr];
     if (MODE != kModeReset) {
         // ---- then the loads that do: the instance's pool row and agent tables (second round trip) --------
-        prefetch(pidx, pw, prel, pnbr);
+        prefetch_instance<T>(p, pool, pidx, pw, prel, pnbr);
         step0 = st.step[b];
         u_old = st.num_unsat[b];
         // ---- assignment + the agents' flips (env:230-250) --------------------
@@ -433,11 +550,14 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
             }
         }
         lds_barrier();
-        // ---- clause scan of the stepped assignment (env:252-254) ------------
+        // ---- clause scan of the stepped assignment (env:252-254); a covered env's clause state is the reset
+        // workgroup's to write
+        uint8_t *const scan_sat = covered ? nullptr : sat_g;
+        uint8_t *const scan_ntrue = covered ? nullptr : ntrue_g;
         if (MODE != kModeObs && p.reward_mode == MSAT_REWARD_PBRS)
-            eval_clauses<T, true, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
+            eval_clauses<T, true, kPfClause>(p, l, pool.lits, pidx, scan_sat, scan_ntrue, pw);
         else
-            eval_clauses<T, false, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
+            eval_clauses<T, false, kPfClause>(p, l, pool.lits, pidx, scan_sat, scan_ntrue, pw);
         lds_barrier();
         cs.mark(2);
         if (MODE != kModeObs && tid == 0) {
@@ -466,12 +586,29 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
             out.solved[b] = solved ? 1 : 0;
             if (out.num_unsat) out.num_unsat[b] = u_new;
             if (out.episode_step) out.episode_step[b] = step0 + 1;
-            const bool reset_now = (MODE == kModeStepAutoReset) && done;
+            // a covered env times out now (its step counter was listed at max_steps - 1): its reset happens in any
+            // case, here and in its reset workgroup, so the state stays whole even for a misused queue
+            MSAT_DCHECK(covered && !done ? 1 : 0, 1);
+            const bool reset_now = (MODE == kModeStepAutoReset) && (done || covered);
             l.red[2] = reset_now ? 1 : 0;
             if (!reset_now) {
                 st.num_unsat[b] = u_new;
                 st.step[b] = step0 + 1;
                 st.done[b] = done ? 1 : 0;
+            }
+            if (rq_fast) {  // list this env for the next launch if its next step times out
+                const int nxt = (p.rq_serial + 1) & 1;
+                const int next_step = reset_now ? 0 : step0 + 1;
+                uint32_t tok = 0u;
+                if (next_step + 1 >= p.max_steps) {
+                    const uint32_t want = rq_token(p.rq_serial + 1u);
+                    const int slot = rq.claim(nxt, want);
+                    if (slot < rq.cap) {
+                        rq.list_of(nxt)[slot] = b;
+                        tok = want;
+                    }
+                }
+                rq.pend_of(nxt)[b] = tok;
             }
         }
         lds_barrier();
@@ -480,20 +617,20 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
 
     if (do_reset) {
         // ---- reset (env:158-181): new problem, new assignment ---------------
-        pidx = reset_instance();
+        pidx = reset_instance(p, new_pidx, seed, ctr, b);
         if (MSAT_DEBUG_BUILD && tid == 0) MSAT_DCHECK(pidx, p.N);  // the reset's pool row
-        if (new_assign != nullptr) {
-            load_x_bits<T>(p, l, new_assign + (size_t)b * p.V);
-        } else {
-            // word t of the assignment = lane t%4 of the Philox block 1 + t/4 (128 vars per block)
-            for (int t = tid; t < p.WV; t += T) {
-                const uint4 r = reset_rng_block(seed, ctr, (uint32_t)b, 1u + (uint32_t)(t >> 2));
-                const int lane = t & 3;
-                uint32_t w = lane == 0 ? r.x : lane == 1 ? r.y : lane == 2 ? r.z : r.w;
-                const int hi = p.V - 32 * t;
-                if (hi < 32) w &= hi <= 0 ? 0u : ((1u << hi) - 1u);
-                l.x[t] = w;
+        reset_assignment<T>(p, l, new_assign, seed, ctr, b);
+        if (covered) {
+            // the reset workgroup scans the new instance and writes its clause state, count and observation;
+            // this one writes the fields it read: assignment, step, done, problem_idx
+            lds_barrier();
+            if (tid == 0) {
+                st.step[b] = 0;
+                st.done[b] = 0;
+                st.problem_idx[b] = pidx;
             }
+            for (int v = tid; v < p.V; v += T) xg[v] = (uint8_t)bit(l.x, v);
+            return;
         }
         if (tid < 2) l.red[tid] = 0;  // red[2] (reset broadcast) may still be read by slower waves
         lds_barrier();
@@ -509,39 +646,47 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
     if (MODE != kModeObs)
         for (int v = tid; v < p.V; v += T) xg[v] = (uint8_t)bit(l.x, v);
     if ((p.ablate & 3) == 2 || obs == nullptr) return;  // NULL obs: state-only step (single-agent SatEnv)
-    // ---- stage the instance's agent tables (built once per pool instance) --
-    {
-        const uint32_t *rel_g = pool.rel + (size_t)pidx * p.A * p.WC;
-        const uint32_t *nbr_g = pool.nbr + (size_t)pidx * p.A * p.WV;
-        const bool pf = (MODE != kModeReset) && !do_reset;  // prefetched words belong to pidx
-        int t0r = 0, t0n = 0;
-        if (pf) {
-#pragma unroll
-            for (int j = 0; j < kPfRel; ++j)
-                if (tid + j * T < p.A * p.WC) l.rel[tid + j * T] = prel[j];
-#pragma unroll
-            for (int j = 0; j < kPfNbr; ++j)
-                if (tid + j * T < p.A * p.WV) l.nbr[tid + j * T] = pnbr[j];
-            t0r = kPfRel * T;
-            t0n = kPfNbr * T;
-        }
-        for (int t = t0r + tid; t < p.A * p.WC; t += T) l.rel[t] = rel_g[t];
-        for (int t = t0n + tid; t < p.A * p.WV; t += T) l.nbr[t] = nbr_g[t];
-        for (int t = tid; t < 2 * obs_image_words(p); t += T) l.fm[t] = 0u;  // fm, fx contiguous
-    }
+    // ---- the instance's agent tables (built once per pool instance), obs images, obs stores ----------------
+    stage_and_write_obs<ObsT, T>(p, l, pool, pidx, (MODE != kModeReset) && !do_reset, prel, pnbr,
+                                 obs + (size_t)b * p.A * p.D, &cs);
+}
+
+// A reset workgroup of an autoreset launch with a reset queue (rq_mode 1): entry j of the list the previous launch
+// made, i.e. an env that times out in this launch.  It draws the env's new instance and assignment (the same draw
+// as its step workgroup's), scans the new instance, and writes the clause state, the unsatisfied count and the
+// observation; its step workgroup writes the transition outputs, the assignment, step, done and problem_idx.
+// Two dependent round trips: {claim word, list entry}, then {pending token, pool row, agent tables}.
+template <typename ObsT, int T>
+__device__ __forceinline__ void env_side_reset(const EnvParams &p, const msat_pool &pool, const msat_env_state &st,
+                                               const int32_t *__restrict__ new_pidx,
+                                               const uint8_t *__restrict__ new_assign, uint64_t seed, uint64_t ctr,
+                                               ObsT *__restrict__ obs, int j, uint32_t *smem) {
+    const EnvLds l = carve(smem, p);
+    const int tid = threadIdx.x;
+    const ResetQueue rq(st.reset_queue, p.B, p.rq_cap);
+    const int cur = p.rq_serial & 1;
+    const uint32_t tok = rq_token(p.rq_serial);
+    const uint64_t cw = rq.cnt[cur];
+    const int bl = rq.list_of(cur)[j];  // read before it is known to be live (same round trip)
+    if ((uint32_t)(cw >> 32) != tok || j >= min((int)(uint32_t)cw, rq.cap) || bl < 0 || bl >= p.B) return;
+    const int b = __builtin_amdgcn_readfirstlane(bl);
+    const uint32_t pend = rq.pend_of(cur)[b];
+    const int pidx = reset_instance(p, new_pidx, seed, ctr, b);
+    if (MSAT_DEBUG_BUILD && tid == 0) MSAT_DCHECK(pidx, p.N);
+    uint64_t pw[kPfClause];
+    uint32_t prel[kPfRel], pnbr[kPfNbr];
+    prefetch_instance<T>(p, pool, min(max(pidx, 0), p.N - 1), pw, prel, pnbr);
+    if (pend != tok) return;  // the env was modified since the list was made (its entry cleared): not ours
+    if (tid < 16) l.red[tid] = 0;
+    reset_assignment<T>(p, l, new_assign, seed, ctr, b);
     lds_barrier();
-    cs.mark(3);
-    ObsT *o = obs + (size_t)b * p.A * p.D;
-    if ((p.ablate & 3) == 0) {
-        build_obs_images<T>(p, l);
-        lds_barrier();
-        cs.mark(4);
-        write_obs<T, ObsT>(p, l, o);
-    } else {
-        constexpr int VEC = ObsVec<ObsT>::N;
-        const int n = (p.A * p.D) / VEC;
-        for (int q = tid; q < n; q += T) ObsVec<ObsT>::store(o + q * VEC, 0u, 0u);
-    }
+    uint8_t *__restrict__ sat_g = st.clause_sat + (size_t)b * p.C;
+    uint8_t *__restrict__ ntrue_g = st.clause_ntrue ? st.clause_ntrue + (size_t)b * p.C : nullptr;
+    eval_clauses<T, false, kPfClause>(p, l, pool.lits, pidx, sat_g, ntrue_g, pw);
+    lds_barrier();
+    if (tid == 0) st.num_unsat[b] = l.red[0];
+    if ((p.ablate & 3) == 2 || obs == nullptr) return;
+    stage_and_write_obs<ObsT, T>(p, l, pool, pidx, true, prel, pnbr, obs + (size_t)b * p.A * p.D, nullptr);
 }
 
 template <int MODE, typename ObsT, int T>
@@ -551,6 +696,10 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
            const uint8_t *__restrict__ new_assign, uint64_t seed, uint64_t ctr, msat_step_out out,
            ObsT *__restrict__ obs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    if (MODE == kModeStepAutoReset && (int)blockIdx.x >= p.B) {  // the reset workgroups, after every step one
+        env_side_reset<ObsT, T>(p, pool, st, new_pidx, new_assign, seed, ctr, obs, (int)blockIdx.x - p.B, smem);
+        return;
+    }
     const int b = xcd_major(blockIdx.x, p.B, p.ablate & 4);
     const ClockStamp cs(out.clock_stamps, b);
     env_run<MODE, ObsT, T>(p, pool, st, actions, reset_mask, new_pidx, new_assign, seed, ctr, out, obs, b, smem, cs);
@@ -854,6 +1003,23 @@ static int make_params(const msat_env_desc *d, EnvParams *p) {
     const char *ab = getenv("MARLSAT_ABLATE");
     p->ablate = ab ? atoi(ab) : 0;
     p->dbg_obs = p->dbg_assign = p->dbg_sat = p->dbg_ntrue = p->dbg_actions = 0;
+    p->rq_mode = 0;
+    p->rq_cap = rq_capacity(p->B);
+    p->rq_serial = 0;
+    return MSAT_OK;
+}
+
+// The reset-queue role of a launch on state st (EnvParams::rq_mode): the autoreset step of the sparse reward mode
+// consumes and produces it; every other state-modifying launch clears the entries of the envs it touches.
+static int set_reset_queue(EnvParams *p, const msat_env_state *st, int mode) {
+    p->rq_mode = 0;
+    if (st->reset_queue == nullptr || mode == kModeObs) return MSAT_OK;
+    MSAT_REQUIRE((reinterpret_cast<uintptr_t>(st->reset_queue) & 7) == 0, "reset_queue must be 8-byte aligned");
+    if (MSAT_DEBUG_BUILD)
+        MSAT_REQUIRE(dbg_extent(st->reset_queue, 4) >= (long long)rq_words(p->B),
+                     "MSAT_DEBUG: reset_queue smaller than msat_reset_queue_words(%d)", p->B);
+    p->rq_serial = st->reset_serial;
+    p->rq_mode = (mode == kModeStepAutoReset && p->reward_mode == MSAT_REWARD_SPARSE) ? 1 : 2;
     return MSAT_OK;
 }
 
@@ -907,14 +1073,17 @@ static int launch_env(const EnvParams &p, const msat_env_desc *d, const msat_poo
     if (out) o = *out;
     if (p.B == 0) return MSAT_OK;
     const int T = env_threads(p);
-    EnvParams pd = p;  // + the buffer extents in debug builds
+    EnvParams pd = p;  // + the buffer extents in debug builds, the reset queue's role
     set_dbg_extents(&pd, st, actions, obs, d->obs_dtype);
+    if (int rc = set_reset_queue(&pd, st, MODE)) return rc;
+    // the reset workgroups of a queue-consuming launch follow every step workgroup (block ids B .. B + cap - 1)
+    const int grid = p.B + (pd.rq_mode == 1 ? pd.rq_cap : 0);
 #define MSAT_ENV_LAUNCH(TT)                                                                                        \
     if (d->obs_dtype == MSAT_OBS_I32)                                                                              \
-        hipLaunchKernelGGL((env_kernel<MODE, int32_t, TT>), dim3(p.B), dim3(TT), lds, s, pd, *pool, *st, actions,   \
+        hipLaunchKernelGGL((env_kernel<MODE, int32_t, TT>), dim3(grid), dim3(TT), lds, s, pd, *pool, *st, actions, \
                            mask, npidx, nassign, seed, ctr, o, (int32_t *)obs);                                    \
     else                                                                                                           \
-        hipLaunchKernelGGL((env_kernel<MODE, int8_t, TT>), dim3(p.B), dim3(TT), lds, s, pd, *pool, *st, actions,    \
+        hipLaunchKernelGGL((env_kernel<MODE, int8_t, TT>), dim3(grid), dim3(TT), lds, s, pd, *pool, *st, actions,  \
                            mask, npidx, nassign, seed, ctr, o, (int8_t *)obs);
     if (T == 64) {
         MSAT_ENV_LAUNCH(64)
@@ -969,6 +1138,9 @@ static int launch_groups(int G, const msat_env_desc *descs, const msat_pool *poo
         }
         e.obs = obs[g];
         set_dbg_extents(&e.p, &e.st, e.actions, e.obs, descs[g].obs_dtype);
+        // the grouped launch keeps every reset in its step workgroup: it only clears the queue's entries
+        if ((rc = set_reset_queue(&e.p, &e.st, MODE))) return rc;
+        if (e.p.rq_mode == 1) e.p.rq_mode = 2;
         total += e.p.B;
         lds = std::max(lds, env_lds_words(e.p) * 4);
         gs.ablate = e.p.ablate;
@@ -1022,6 +1194,8 @@ extern "C" int msat_env_step_grouped(int32_t num_groups, const msat_env_desc *de
     return launch_groups<kModeStep>(num_groups, descs, pools, states, actions, seed, rng_counter, outs, obs,
                                     (hipStream_t)stream);
 }
+
+extern "C" size_t msat_reset_queue_words(int32_t num_envs) { return num_envs < 0 ? 0 : rq_words(num_envs); }
 
 extern "C" int msat_pool_pack(const int32_t *lits, int32_t num_problems, int32_t num_clauses,
                               int32_t clause_width, int32_t num_vars, uint16_t *pool,

@@ -48,6 +48,8 @@ class EnvStateC(ctypes.Structure):
         ("step", c_void_p),
         ("done", c_void_p),
         ("problem_idx", c_void_p),
+        ("reset_queue", c_void_p),  # nullable: timed-out resets in workgroups of their own (include/marlsat.h)
+        ("reset_serial", ctypes.c_uint32),
     ]
 
 
@@ -100,6 +102,7 @@ def _load():
         "msat_clause_sat_features": (c_int32, [POINTER(EnvDesc), POINTER(EnvStateC), P, P]),
         "msat_bc_greedy_labels": (c_int32, [POINTER(EnvDesc), P, P, P, c_float, P, P, P]),
         "msat_static_var_features": (c_int32, [P, c_int32, c_int32, c_int32, P, P]),
+        "msat_reset_queue_words": (c_size_t, [c_int32]),
         "msat_gae_workspace_bytes": (c_size_t, [c_int32, c_int32]),
         "msat_gae": (
             c_int32,
@@ -289,6 +292,7 @@ EXPORTED = (
     "msat_static_var_features",
     "msat_gae_workspace_bytes",
     "msat_gae",
+    "msat_reset_queue_words",
 )
 
 

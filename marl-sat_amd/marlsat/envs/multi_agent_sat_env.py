@@ -143,6 +143,12 @@ class SATState:
     pool: ProblemPool
     env: "SATEnv" = field(repr=False)
     _masks: Optional[tuple] = field(default=None, repr=False)
+    # msat_env_state.reset_queue (include/marlsat.h): each autoreset step lists the envs whose next step times
+    # out, and the next one resets them in workgroups of their own; reset_serial counts those launches.  Not
+    # reference state: results are identical without it.  Code that writes the arrays above directly must call
+    # invalidate_reset_queue().
+    reset_queue: Optional[torch.Tensor] = field(default=None, repr=False)
+    reset_serial: int = field(default=0, repr=False)
 
     @property
     def num_envs(self) -> int:
@@ -191,19 +197,28 @@ class SATState:
         return _lib.EnvStateC(
             self.variable_assignments.data_ptr(), self.clauses_satisfied_status.data_ptr(),
             self.clause_ntrue.data_ptr(), self.num_unsatisfied.data_ptr(), self.step.data_ptr(),
-            self.env_done.data_ptr(), self.problem_idx.data_ptr(),
+            self.env_done.data_ptr(), self.problem_idx.data_ptr(), _lib.ptr(self.reset_queue),
+            self.reset_serial & 0xFFFFFFFF,
         )
+
+    def invalidate_reset_queue(self) -> None:
+        """Forget the listed timed-out envs (after writing state arrays directly, e.g. bench.py's staggered
+        episode counters): the next autoreset step resets every env in its own workgroup and lists afresh."""
+        if self.reset_queue is not None:
+            self.reset_queue.zero_()
 
     def clone(self) -> "SATState":
         return SATState(
             self.variable_assignments.clone(), self.clauses_satisfied_status.clone(), self.clause_ntrue.clone(),
             self.num_unsatisfied.clone(), self.step.clone(), self.env_done.clone(), self.problem_idx.clone(),
-            self.pool, self.env,
+            self.pool, self.env, reset_queue=None if self.reset_queue is None else self.reset_queue.clone(),
+            reset_serial=self.reset_serial,
         )
 
     def replace(self, **kw) -> "SATState":
-        """flax ``struct.replace`` analogue (shallow)."""
-        d = {f: getattr(self, f) for f in self.__dataclass_fields__ if f != "_masks"}
+        """flax ``struct.replace`` analogue (shallow).  The result has no reset queue (its arrays may be
+        other tensors than the ones the queue describes)."""
+        d = {f: getattr(self, f) for f in self.__dataclass_fields__ if f not in ("_masks", "reset_queue", "reset_serial")}
         d.update(kw)
         return SATState(**d)
 
@@ -280,7 +295,8 @@ class SATEnv:
         B, V, C = num_envs, self.num_vars, self.num_clauses
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)
         return SATState(z((B, V), torch.uint8), z((B, C), torch.uint8), z((B, C), torch.uint8), z((B,), torch.int32),
-                        z((B,), torch.int32), z((B,), torch.uint8), z((B,), torch.int32), pool, self)
+                        z((B,), torch.int32), z((B,), torch.uint8), z((B,), torch.int32), pool, self,
+                        reset_queue=z((int(_lib.lib.msat_reset_queue_words(B)),), torch.int32))
 
     def alloc_obs(self, num_envs: int) -> torch.Tensor:
         return torch.empty((num_envs, self.num_agents, self.obs_dim), dtype=self.obs_dtype, device=self.device)
@@ -377,6 +393,8 @@ class SATEnv:
                                           a.data_ptr(), 1 if autoreset else 0, _lib.ptr(pidx), _lib.ptr(x), k.seed,
                                           k.counter, so, _lib.ptr(obs), _lib.stream_ptr(self.device)),
                    "msat_env_step")
+        if autoreset:
+            state.reset_serial += 1
         state._masks = None
         return obs, out
 
@@ -401,10 +419,13 @@ class SATEnv:
         def step(actions: torch.Tensor, counter: int) -> None:
             if actions.shape != want or actions.dtype != torch.int32:
                 raise ValueError(f"actions must be int32 {want}")
+            cst.reset_serial = state.reset_serial & 0xFFFFFFFF
             rc = fn(dref, pref, sref, actions.data_ptr(), ar, None, None, seed, counter, oref, obs_p, s)
             state._masks = None
             if rc:
                 _lib.check(rc, "msat_env_step")
+            if ar:
+                state.reset_serial += 1
 
         step._keepalive = (desc, cpool, cst, so, state, obs, out)
         return step

@@ -521,3 +521,69 @@ def test_clock_stamps_are_inert_and_plausible(V, C, vpa, B):
     for i in range(3, 7):
         assert ((s[:, i] >= start) & (s[:, i] <= end)).all(), i
     assert (np.diff(s[:, 3:7], axis=1) >= 0).all()
+
+
+def _state_arrays(st):
+    return [_np(t).copy() for t in (st.variable_assignments, st.clauses_satisfied_status, st.clause_ntrue,
+                                    st.num_unsatisfied, st.step, st.env_done, st.problem_idx)]
+
+
+@pytest.mark.parametrize("V,C,vpa,B,max_steps,explicit", [
+    (50, 218, 10, 1024, 5, False),  # ~205 time out per step: the first cap (12) in reset workgroups, the rest in place
+    (50, 218, 10, 1024, 512, False),  # the bench's steady state: counters staggered, ~2 per step
+    (20, 91, 10, 64, 3, True),  # caller-given reset instances and assignments (new_problem_idx / new_assign)
+    (200, 860, 8, 512, 7, False),  # 512-lane workgroups
+    (23, 97, 10, 40, 1, False),  # every step times out, and so does the step after a reset
+])
+def test_reset_queue_is_invisible(V, C, vpa, B, max_steps, explicit):
+    """The reset queue (msat_env_state.reset_queue: timed-out envs reset in workgroups of their own, listed by the
+    previous launch) changes no output: two copies of one batch, one stepped with the queue and one without,
+    stay bitwise equal in every state array, obs and step output over a run of RNG auto-resets (solved and timed
+    out), with an env-masked reset, a direct counter write (invalidate_reset_queue) and a non-autoreset step in
+    between; and the queue's launches do run reset workgroups (listed envs are seen)."""
+    env, _ = _mk(V, C, vpa, max_steps=max_steps)
+    N = 16
+    pool = env.make_pool(_pool(V, C, N, seed0=700))
+    rng = np.random.default_rng(B + max_steps)
+    pidx = rng.integers(0, N, B).astype(np.int32)
+    x = rng.integers(0, 2, (B, V)).astype(np.uint8)
+    _, sq = env.reset_from_pool(pool, B, problem_idx=pidx, assignments=x)
+    _, sn = env.reset_from_pool(pool, B, problem_idx=pidx, assignments=x)
+    sn.reset_queue = None
+    if max_steps == 512:  # a long rollout's counters
+        c = torch.from_numpy(rng.integers(0, 512, B).astype(np.int32)).cuda()
+        for s in (sq, sn):
+            s.step.copy_(c)
+        sq.invalidate_reset_queue()
+    listed = 0
+    for t in range(14):
+        if t == 5:  # reset a third of the envs in place: their queue entries are cleared
+            m = rng.random(B) < 0.33
+            for s in (sq, sn):
+                env.reset_from_pool(pool, B, Key(5, 1000 + t), state=s, reset_mask=m)
+        if t == 8:  # counters written directly
+            c = torch.from_numpy(rng.integers(0, max_steps, B).astype(np.int32)).cuda()
+            for s in (sq, sn):
+                s.step.copy_(c)
+            sq.invalidate_reset_queue()
+        a = torch.from_numpy(rng.integers(0, env.max_vars_per_agent + 1, (B, env.num_agents)).astype(np.int32)).cuda()
+        kw = {}
+        if explicit:
+            kw = dict(problem_idx=rng.integers(0, N, B).astype(np.int32),
+                      assignments=rng.integers(0, 2, (B, V)).astype(np.uint8))
+        auto = t != 10  # one plain step_env launch: it clears the entries of every env it steps
+        if sq.reset_queue is not None and auto:
+            q = _np(sq.reset_queue).view(np.uint32)
+            par = sq.reset_serial & 1
+            tok = 0x80000000 | (sq.reset_serial & 0x7FFFFFFF)
+            listed += int((q[4 + par * B: 4 + (par + 1) * B] == tok).sum())
+        outs = []
+        for s in (sq, sn):
+            o, out = env.step_raw(s, a, autoreset=auto, key=Key(9, t), **kw)
+            outs.append((_np(o), {k: _np(v) for k, v in out.items()}))
+        np.testing.assert_array_equal(outs[0][0], outs[1][0], err_msg=f"obs t={t}")
+        for k in outs[0][1]:
+            np.testing.assert_array_equal(outs[0][1][k], outs[1][1][k], err_msg=f"{k} t={t}")
+        for i, (u, v) in enumerate(zip(_state_arrays(sq), _state_arrays(sn))):
+            np.testing.assert_array_equal(u, v, err_msg=f"state array {i} t={t}")
+    assert listed > 0  # the queue path ran
