@@ -19,6 +19,7 @@ signatures and return structures.  Differences, all deliberate:
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -127,6 +128,10 @@ class ProblemPool:
                                                          _lib.stream_ptr(self.device)),
                        "msat_static_var_features")
         return self._svf
+
+
+# MARLSAT_RESET_QUEUE=0: states without a reset queue (every reset in its step workgroup; A/B runs only)
+RESET_QUEUE = os.environ.get("MARLSAT_RESET_QUEUE", "1") != "0"
 
 
 @dataclass
@@ -296,7 +301,7 @@ class SATEnv:
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)
         return SATState(z((B, V), torch.uint8), z((B, C), torch.uint8), z((B, C), torch.uint8), z((B,), torch.int32),
                         z((B,), torch.int32), z((B,), torch.uint8), z((B,), torch.int32), pool, self,
-                        reset_queue=z((int(_lib.lib.msat_reset_queue_words(B)),), torch.int32))
+                        reset_queue=z((int(_lib.lib.msat_reset_queue_words(B)),), torch.int32) if RESET_QUEUE else None)
 
     def alloc_obs(self, num_envs: int) -> torch.Tensor:
         return torch.empty((num_envs, self.num_agents, self.obs_dim), dtype=self.obs_dtype, device=self.device)
