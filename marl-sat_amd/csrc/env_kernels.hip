@@ -371,24 +371,31 @@ template <int T>
 __device__ __forceinline__ void prefetch_instance(const EnvParams &p, const msat_pool &pool, int n,
                                                   uint64_t (&w)[kPfClause], uint32_t (&rl)[kPfRel],
                                                   uint32_t (&nb)[kPfNbr]) {
+    // Branch-free: every lane loads a clamped (valid) address and zeroes what lies past the end.  Loads under a
+    // branch leave the compiler's vmcnt bookkeeping unsure how many are in flight, so the first use of an
+    // EARLIER load (the assignment byte) then waited for all of these (a whole round trip before the flips).
     const int tid = threadIdx.x;
     const uint64_t *prow = reinterpret_cast<const uint64_t *>(pool.lits) + (size_t)n * p.C;
     const uint32_t *rel_g = pool.rel + (size_t)n * p.A * p.WC;
     const uint32_t *nbr_g = pool.nbr + (size_t)n * p.A * p.WV;
+    const int nrel = p.A * p.WC, nnbr = p.A * p.WV;
 #pragma unroll
     for (int j = 0; j < kPfClause; ++j) {
         const int c = tid + j * T;
-        w[j] = c < p.C ? prow[c] : 0ull;
+        const uint64_t v = prow[min(c, p.C - 1)];
+        w[j] = c < p.C ? v : 0ull;
     }
 #pragma unroll
     for (int j = 0; j < kPfRel; ++j) {
         const int t = tid + j * T;
-        rl[j] = t < p.A * p.WC ? rel_g[t] : 0u;
+        const uint32_t v = rel_g[min(t, nrel - 1)];
+        rl[j] = t < nrel ? v : 0u;
     }
 #pragma unroll
     for (int j = 0; j < kPfNbr; ++j) {
         const int t = tid + j * T;
-        nb[j] = t < p.A * p.WV ? nbr_g[t] : 0u;
+        const uint32_t v = nbr_g[min(t, nnbr - 1)];
+        nb[j] = t < nnbr ? v : 0u;
     }
 }
 
@@ -486,18 +493,33 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
 
     bool do_reset = (MODE == kModeReset);
     // the per-lane loads that do not depend on problem_idx, issued together with it (one round trip): this
-    // lane's action and its assignment byte of the first ballot pass (clamped indices, no branches), and this
-    // env's entry of the reset queue; problem_idx last, so that waiting for it retires the group.  (step / unsat
-    // are wave-uniform values the compiler moves to scalar registers as soon as they are loaded, which would
-    // wait for them: they go with the second round trip.)
+    // lane's action and its assignment byte of the first ballot pass (clamped indices, no branches), then
+    // problem_idx, step and unsat.  (step / unsat are wave-uniform values the compiler moves to scalar registers
+    // as soon as they are loaded, i.e. waits for them right there: issued behind problem_idx, that wait retires
+    // the first round trip, which the prefetch needs anyway.  Issued behind the prefetch (round 5), it held the
+    // assignment bits and the flips until the prefetch had landed too.)
     int step0 = 0, u_old = 0, a0 = 0;
     uint32_t x0 = 0, pend = 0;
+    bool covered = false;
+    // the reset-queue entry rides in the action load: lane A of wave 0 (mode 0, A < 64) reads it instead of a
+    // duplicate action, so it costs no round trip of its own; otherwise one load of its own behind the prefetch
+    const bool pend_in_a0 = rq_fast && p.action_mode == 0 && p.A < 64;
     if (MODE != kModeReset) {
-        if (MODE != kModeObs && p.action_mode == 0) a0 = actions[(size_t)b * p.A + min(tid, p.A - 1)];
+        if (MODE != kModeObs && p.action_mode == 0) {
+            const int32_t *ap = actions + (size_t)b * p.A + min(tid, p.A - 1);
+            if (pend_in_a0 && tid == p.A) ap = reinterpret_cast<const int32_t *>(rq.pend_of(p.rq_serial & 1) + b);
+            a0 = *ap;
+        }
         x0 = xg[min(tid, p.V - 1)];
     }
-    if (rq_fast) pend = rq.pend_of(p.rq_serial & 1)[b];
     int pidx = st.problem_idx[b];
+    if (MODE != kModeReset) {
+        step0 = st.step[b];
+        u_old = st.num_unsat[b];
+    }
+    // keep the first round trip's loads ahead of the prefetch (the scheduler sank the assignment byte below it,
+    // and its first use then waited for the prefetch as well)
+    __builtin_amdgcn_sched_barrier(0);
     if (MSAT_DEBUG_BUILD && tid == 0) {  // this env's rows of every caller buffer, and its pool row
         if (MODE != kModeReset) MSAT_DCHECK(pidx, p.N);
         MSAT_DCHECK((long long)(b + 1) * p.V - 1, p.dbg_assign);
@@ -507,15 +529,15 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         if (MODE == kModeStep || MODE == kModeStepAutoReset)
             MSAT_DCHECK((long long)(b + 1) * p.A * (p.action_mode == 0 ? 1 : p.M) - 1, p.dbg_actions);
     }
-    // a reset workgroup of this launch resets this env (it times out now: listed by the previous launch)
-    const bool covered = rq_fast && pend == rq_token(p.rq_serial);
     uint64_t pw[kPfClause];
     uint32_t prel[kPfRel], pnbr[kPfNbr];
     if (MODE != kModeReset) {
         // ---- then the loads that do: the instance's pool row and agent tables (second round trip) --------
         prefetch_instance<T>(p, pool, pidx, pw, prel, pnbr);
-        step0 = st.step[b];
-        u_old = st.num_unsat[b];
+        __builtin_amdgcn_sched_barrier(0);
+        // this env's reset-queue entry, issued behind the prefetch: it is first needed at the scan, which waits for
+        // the prefetched pool row anyway (issued earlier, its wait held up the prefetch by a round trip)
+        if (rq_fast && !pend_in_a0) pend = rq.pend_of(p.rq_serial & 1)[b];
         // ---- assignment + the agents' flips (env:230-250) --------------------
         load_x_bits<T>(p, l, xg, x0);
         lds_barrier();
@@ -523,6 +545,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         if (MODE == kModeObs) {
             // get_obs only: no flips, no state update
         } else if (p.action_mode == 0) {
+            if (pend_in_a0 && tid == 0) l.red[3] = (int)__builtin_amdgcn_readlane(a0, p.A);  // read after the barrier
             for (int i = tid; i < p.A; i += T) {
                 const int a = i == tid ? a0 : actions[(size_t)b * p.A + i];
                 const int n = agent_size(p, i);
@@ -550,8 +573,9 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
             }
         }
         lds_barrier();
-        // ---- clause scan of the stepped assignment (env:252-254); a covered env's clause state is the reset
-        // workgroup's to write
+        // ---- clause scan of the stepped assignment (env:252-254); a covered env (a reset workgroup of this launch
+        // resets it: it times out now, listed by the previous launch) leaves its clause state to that workgroup
+        covered = rq_fast && (pend_in_a0 ? (uint32_t)l.red[3] : pend) == rq_token(p.rq_serial);
         uint8_t *const scan_sat = covered ? nullptr : sat_g;
         uint8_t *const scan_ntrue = covered ? nullptr : ntrue_g;
         if (MODE != kModeObs && p.reward_mode == MSAT_REWARD_PBRS)
@@ -666,10 +690,16 @@ __device__ __forceinline__ void env_side_reset(const EnvParams &p, const msat_po
     const ResetQueue rq(st.reset_queue, p.B, p.rq_cap);
     const int cur = p.rq_serial & 1;
     const uint32_t tok = rq_token(p.rq_serial);
-    const uint64_t cw = rq.cnt[cur];
-    const int bl = rq.list_of(cur)[j];  // read before it is known to be live (same round trip)
-    if ((uint32_t)(cw >> 32) != tok || j >= min((int)(uint32_t)cw, rq.cap) || bl < 0 || bl >= p.B) return;
-    const int b = __builtin_amdgcn_readfirstlane(bl);
+    // the claim word and the list entry in ONE vector load (lanes 0 / 1: the claim word's halves, lane 2: entry j),
+    // so the entry is read before it is known to be live, in the same round trip
+    const int lane = tid & 63;
+    const uint32_t *src = lane < 2 ? reinterpret_cast<const uint32_t *>(rq.cnt + cur) + lane
+                                   : reinterpret_cast<const uint32_t *>(rq.list_of(cur) + j);
+    const uint32_t v = *src;
+    const uint32_t cnt = __builtin_amdgcn_readlane(v, 0), ctok = __builtin_amdgcn_readlane(v, 1);
+    const int bl = (int)__builtin_amdgcn_readlane(v, 2);
+    if (ctok != tok || j >= min((int)cnt, rq.cap) || bl < 0 || bl >= p.B) return;
+    const int b = bl;
     const uint32_t pend = rq.pend_of(cur)[b];
     const int pidx = reset_instance(p, new_pidx, seed, ctr, b);
     if (MSAT_DEBUG_BUILD && tid == 0) MSAT_DCHECK(pidx, p.N);

@@ -308,15 +308,6 @@ __device__ __forceinline__ float ftanh_fast(float x) {
 // weights overflowed at the split (wbad), writes flags[tile] = 1 and no output, and the bf16x3 kernel,
 // launched next with the same flags, recomputes exactly the flagged tiles.
 constexpr int kH2Shift = 10;  // weight scale 2^10: |W| < 32 fits, |W| >= 2^-24 keeps 11 bits
-// A/B builds only (make ab AB_FLAGS=...): MSAT_GRU_A2B2 = 1 adds the fourth product a2 b2; MSAT_GRU_ASCALE = s scales
-// the activations by 2^s before their split (their low halves stay normal down to |a| ~ 2^-(3+s))
-#ifndef MSAT_GRU_A2B2
-#define MSAT_GRU_A2B2 0
-#endif
-#ifndef MSAT_GRU_ASCALE
-#define MSAT_GRU_ASCALE 0
-#endif
-constexpr float kH2AScale = (float)(1 << MSAT_GRU_ASCALE);
 
 
 __device__ __forceinline__ int gswz16(int b) { return (0x78 >> (2 * b)) & 3; }  // {0, 2, 3, 1}
@@ -441,8 +432,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         const float m0 = fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w)));
         const float m1 = fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w)));
         amax = fmaxf(amax, fmaxf(m0, m1));
-        const float4 s4 = {kH2AScale, kH2AScale, kH2AScale, kH2AScale};
-        const SplitH8 sp = MSAT_GRU_ASCALE ? splith8(v0 * s4, v1 * s4) : splith8(v0, v1);
+        const SplitH8 sp = splith8(v0, v1);
         f[0] = sp.p[0];
         f[1] = sp.p[1];
     };
@@ -550,7 +540,6 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
                 const int G = gt < 2 ? gt : (hid ? 3 : 2);
                 uint4 &b0 = bb[n % LA][0], &b1 = bb[n % LA][1];
                 f32x4g c = acc[G][j];
-                if (MSAT_GRU_A2B2) c = h2mma(fa[1], b1, c);  // a2 b2 (A/B builds)
                 c = h2mma(fa[0], b1, c);  // a1 b2
                 if (n + LA < 24) b1 = bfrag(n + LA, 1);
                 c = h2mma(fa[1], b0, c);  // a2 b1
@@ -581,7 +570,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         // the weight buffers are free past the last step's barrier: the flags sit in Bs's last 32 bytes,
         // beyond the epilogue's stage (LDS is full: 96 KiB of weights + 64 KiB of activation slots)
         int *const wbadl = reinterpret_cast<int *>(&Bs[2 * NI * IMG]) - NW;
-        const bool wb = __ballot(!(amax * kH2AScale < 32768.0f)) != 0;
+        const bool wb = __ballot(!(amax < 32768.0f)) != 0;
         if (lane == 0) wbadl[w] = wb;
         barrier_lds();
         int bad = 0;
@@ -615,7 +604,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
             }
         }
     }
-    constexpr float sc = 1.0f / (float)(1 << (kH2Shift + MSAT_GRU_ASCALE));  // exact power of two
+    constexpr float sc = 1.0f / (float)(1 << kH2Shift);  // exact power of two
     // packed fp32 (v_pk_mul / v_pk_add on row pairs): no MFMAs run here, so the packed forms halve the
     // epilogue's vector issue instead of competing with matrix work
     // LayerNorm scale / bias, loaded with the gate biases
