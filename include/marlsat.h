@@ -100,16 +100,16 @@ typedef struct msat_env_state {
     int32_t *step;        /* (B,)    step                                    */
     uint8_t *done;        /* (B,)    done (every agent shares it)            */
     int32_t *problem_idx; /* (B,)    row of the problem pool this env solves */
-    /* Reset queue (nullable; msat_reset_queue_words(B) zeroed uint32 words, owned by the state like the arrays
-     * above): each msat_env_step(autoreset=1) launch lists the envs whose NEXT step times out (their step
-     * counter reaches max_steps - 1; the reference's timed_out, env:256-260), and the next launch resets
-     * those envs in workgroups of their own, beside the step workgroups, instead of serially behind their
-     * step (their step workgroup then writes only the transition outputs, the assignment, step, done and
-     * problem_idx).  Results are identical with or without it.  Used by the sparse reward mode; the other
-     * state-modifying calls clear the entries of the envs they touch.  A caller that writes the state
-     * arrays directly must zero the queue (or pass NULL).  reset_serial: the launch's serial, +1 per
-     * msat_env_step(autoreset=1) call on this state; a launch uses the list only if the previous launch on
-     * the state had serial reset_serial - 1. */
+    /* Reset queue (nullable; msat_reset_queue_words(B) zeroed uint32 words, 16-byte aligned, owned by the state like
+     * the arrays above): each msat_env_step(autoreset=1) launch marks the envs whose NEXT step times out (their step
+     * counter reaches max_steps - 1; the reference's timed_out, env:256-260), and the next launch resets the first
+     * B/256 + 8 of them (in index order) in workgroups of their own, beside the step workgroups, instead of serially
+     * behind their step (their step workgroup then writes only the transition outputs, the assignment, step, done
+     * and problem_idx).  Results are identical with or without it.  Used by the sparse reward mode with mode-0
+     * actions and fewer than 64 agents (B a multiple of 4); the other state-modifying calls clear the entries of the
+     * envs they touch.  A caller that writes the state arrays directly must zero the queue (or pass NULL).
+     * reset_serial: the launch's serial, +1 per msat_env_step(autoreset=1) call on this state; a launch uses the
+     * marks only if the previous launch on the state had serial reset_serial - 1. */
     uint32_t *reset_queue;
     uint32_t reset_serial;
 } msat_env_state;

@@ -52,40 +52,79 @@ struct EnvParams {
 
 enum : int { kModeReset = 0, kModeStep = 1, kModeStepAutoReset = 2, kModeObs = 3 };
 
-// Reset queue layout (uint32 words): [0, 4) two uint64 claim words {token << 32 | count}, one per parity;
-// [4, 4 + 2B) the pending token of each env, per parity; then [2][cap] env lists.  The launch with serial s
-// reads parity s & 1 (entries whose token is rq_token(s)) and writes parity (s + 1) & 1 with rq_token(s + 1):
-// the two are never the same words within a launch.  Tokens have bit 31 set, so a zeroed queue lists nothing.
+// Reset queue (msat_env_state.reset_queue): pend[2][B] uint32 tokens.  The launch with serial s reads parity s & 1 --
+// env b timed out now iff pend[s & 1][b] == rq_token(s), written by the previous launch -- and writes every entry of
+// parity (s + 1) & 1 (rq_token(s + 1) for an env whose next step times out, else 0): never the same words within a
+// launch.  The reset workgroups of launch s take the pending envs in index order: workgroup j the one of rank j,
+// the env of rank r is covered iff r < cap (the others reset in their step workgroup).  Ranks come from a scan of
+// the pending words (one round trip), so no counter, list or atomic is involved: a launch in which every env times
+// out (a batch reset together, every max_steps launches) costs each env one scan of B words from L2.  Tokens have
+// bit 31 set, so a zeroed queue lists nothing.
 __host__ __device__ __forceinline__ uint32_t rq_token(uint32_t serial) { return 0x80000000u | (serial & 0x7FFFFFFFu); }
 __host__ __device__ __forceinline__ int rq_capacity(int B) { return B / 256 + 8; }  // ~B/512 time out per launch
-__host__ __device__ __forceinline__ size_t rq_words(int B) { return 4 + 2 * (size_t)B + 2 * (size_t)rq_capacity(B); }
+__host__ __device__ __forceinline__ size_t rq_words(int B) { return 2 * (size_t)B; }
 
-struct ResetQueue {
-    uint64_t *cnt;
-    uint32_t *pend;
-    int32_t *list;
-    int B, cap;
-    __device__ __forceinline__ ResetQueue(uint32_t *q, int B_, int cap_) : B(B_), cap(cap_) {
-        cnt = reinterpret_cast<uint64_t *>(q);
-        pend = q + 4;
-        list = reinterpret_cast<int32_t *>(q + 4 + 2 * (size_t)B_);
-    }
-    __device__ __forceinline__ uint32_t *pend_of(int par) const { return pend + (size_t)par * B; }
-    __device__ __forceinline__ int32_t *list_of(int par) const { return list + (size_t)par * cap; }
-    // a slot in parity par's list for this launch's token: the claim word restarts at 0 when it still holds an
-    // older launch's token (device-scope compare-and-swap; a handful of claimants per launch)
-    __device__ __forceinline__ int claim(int par, uint32_t tok) const {
-        uint64_t *w = cnt + par;
-        uint64_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (;;) {
-            const uint32_t c = (uint32_t)(old >> 32) == tok ? (uint32_t)old : 0u;
-            const uint64_t nw = ((uint64_t)tok << 32) | (uint64_t)(c + 1u);
-            if (__hip_atomic_compare_exchange_strong(w, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT))
-                return (int)c;
+__device__ __forceinline__ uint32_t *rq_pend(uint32_t *q, int B, int par) { return q + (size_t)par * B; }
+
+// Wave 0 (all 64 lanes, uniform arguments) scans pend[0 .. B): lane l owns the contiguous words [W l, W l + W),
+// W = ceil(B / 64) rounded up to 4 (16-byte loads).  Returns, in every lane, the number of entries equal to tok
+// with index < lim; with want >= 0 also the index of the entry of rank want (-1 if fewer), in *sel.  Each lane keeps
+// its matches as a bit mask (W <= 64, i.e. B <= 4096), so the selection needs no second read; larger batches
+// re-read the owning lane's range.
+__device__ __forceinline__ int rq_scan(const uint32_t *__restrict__ pend, int B, uint32_t tok, int lim, int want,
+                                       int *sel) {
+    const int lane = threadIdx.x & 63;
+    const int W = ((B + 63) / 64 + 3) & ~3;
+    const int lo = lane * W;
+    int below = 0, mine = 0;
+    uint64_t bits = 0;
+    for (int i = 0; i < W; i += 4) {
+        const int k = lo + i;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (k < B) v = *reinterpret_cast<const uint4 *>(pend + k);  // B % 4 == 0 (host-checked)
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool m = k + u < B && w[u] == tok;
+            mine += m;
+            below += m && k + u < lim;
+            if (m && i + u < 64) bits |= 1ull << (i + u);
         }
     }
-};
+    int total_below = below;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) total_below += __shfl_xor(total_below, d, 64);
+    if (want >= 0) {
+        int incl = mine;  // inclusive prefix of mine over the lanes (index order), Hillis-Steele by shuffles
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int up = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += up;
+        }
+        const int excl = incl - mine;
+        int found = -1;
+        if (want >= excl && want < incl) {  // the rank-want entry is in this lane's range
+            int r = want - excl;            // its rank among this lane's matches
+            if (W <= 64) {
+                uint64_t m = bits;
+                for (; r > 0; --r) m &= m - 1;
+                found = lo + __ffsll((unsigned long long)m) - 1;
+            } else {
+                for (int i = 0; i < W && found < 0; i += 4) {
+                    const int k = lo + i;
+                    if (k >= B) break;
+                    const uint4 v = *reinterpret_cast<const uint4 *>(pend + k);
+                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                    for (int u = 0; u < 4 && found < 0; ++u)
+                        if (k + u < B && w[u] == tok && r-- == 0) found = k + u;
+                }
+            }
+        }
+        const uint64_t has = __ballot(found >= 0);
+        *sel = has ? __shfl(found, __ffsll((unsigned long long)has) - 1, 64) : -1;
+    }
+    return total_below;
+}
 
 __host__ __device__ __forceinline__ int agent_lo(const EnvParams &p, int i) { return i * p.base + (i < p.rem ? i : p.rem); }
 __host__ __device__ __forceinline__ int agent_size(const EnvParams &p, int i) { return p.base + (i < p.rem ? 1 : 0); }
@@ -484,11 +523,10 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
     uint8_t *__restrict__ ntrue_g = st.clause_ntrue ? st.clause_ntrue + (size_t)b * p.C : nullptr;
     if (tid < 16) l.red[tid] = 0;
     // reset queue: rq_fast = this autoreset launch consumes / produces it; rq_mode 2 = clear this env's entries
-    const bool rq_fast = MODE == kModeStepAutoReset && p.rq_mode == 1;
-    const ResetQueue rq(st.reset_queue, p.B, p.rq_cap);
+    const bool rq_fast = MODE == kModeStepAutoReset && p.rq_mode == 1;  // host: sparse reward, mode 0, A < 64
     if (MODE != kModeObs && p.rq_mode == 2 && tid == 0) {
-        rq.pend_of(0)[b] = 0u;
-        rq.pend_of(1)[b] = 0u;
+        rq_pend(st.reset_queue, p.B, 0)[b] = 0u;
+        rq_pend(st.reset_queue, p.B, 1)[b] = 0u;
     }
 
     bool do_reset = (MODE == kModeReset);
@@ -499,15 +537,15 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
     // the first round trip, which the prefetch needs anyway.  Issued behind the prefetch (round 5), it held the
     // assignment bits and the flips until the prefetch had landed too.)
     int step0 = 0, u_old = 0, a0 = 0;
-    uint32_t x0 = 0, pend = 0;
+    uint32_t x0 = 0;
     bool covered = false;
     // the reset-queue entry rides in the action load: lane A of wave 0 (mode 0, A < 64) reads it instead of a
-    // duplicate action, so it costs no round trip of its own; otherwise one load of its own behind the prefetch
-    const bool pend_in_a0 = rq_fast && p.action_mode == 0 && p.A < 64;
+    // duplicate action, so it costs no round trip of its own
     if (MODE != kModeReset) {
         if (MODE != kModeObs && p.action_mode == 0) {
             const int32_t *ap = actions + (size_t)b * p.A + min(tid, p.A - 1);
-            if (pend_in_a0 && tid == p.A) ap = reinterpret_cast<const int32_t *>(rq.pend_of(p.rq_serial & 1) + b);
+            if (rq_fast && tid == p.A)
+                ap = reinterpret_cast<const int32_t *>(rq_pend(st.reset_queue, p.B, p.rq_serial & 1) + b);
             a0 = *ap;
         }
         x0 = xg[min(tid, p.V - 1)];
@@ -535,9 +573,6 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         // ---- then the loads that do: the instance's pool row and agent tables (second round trip) --------
         prefetch_instance<T>(p, pool, pidx, pw, prel, pnbr);
         __builtin_amdgcn_sched_barrier(0);
-        // this env's reset-queue entry, issued behind the prefetch: it is first needed at the scan, which waits for
-        // the prefetched pool row anyway (issued earlier, its wait held up the prefetch by a round trip)
-        if (rq_fast && !pend_in_a0) pend = rq.pend_of(p.rq_serial & 1)[b];
         // ---- assignment + the agents' flips (env:230-250) --------------------
         load_x_bits<T>(p, l, xg, x0);
         lds_barrier();
@@ -545,7 +580,15 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         if (MODE == kModeObs) {
             // get_obs only: no flips, no state update
         } else if (p.action_mode == 0) {
-            if (pend_in_a0 && tid == 0) l.red[3] = (int)__builtin_amdgcn_readlane(a0, p.A);  // read after the barrier
+            if (rq_fast && tid < 64) {  // wave 0: is this env covered?  (read by every wave after the barrier)
+                const uint32_t tok = rq_token(p.rq_serial);
+                int cov = 0;
+                if (__builtin_amdgcn_readlane(a0, p.A) == (int)tok) {  // pending: its rank among the pending envs
+                    int unused;
+                    cov = rq_scan(rq_pend(st.reset_queue, p.B, p.rq_serial & 1), p.B, tok, b, -1, &unused) < p.rq_cap;
+                }
+                if (tid == 0) l.red[3] = cov;
+            }
             for (int i = tid; i < p.A; i += T) {
                 const int a = i == tid ? a0 : actions[(size_t)b * p.A + i];
                 const int n = agent_size(p, i);
@@ -575,7 +618,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
         lds_barrier();
         // ---- clause scan of the stepped assignment (env:252-254); a covered env (a reset workgroup of this launch
         // resets it: it times out now, listed by the previous launch) leaves its clause state to that workgroup
-        covered = rq_fast && (pend_in_a0 ? (uint32_t)l.red[3] : pend) == rq_token(p.rq_serial);
+        covered = rq_fast && l.red[3] != 0;
         uint8_t *const scan_sat = covered ? nullptr : sat_g;
         uint8_t *const scan_ntrue = covered ? nullptr : ntrue_g;
         if (MODE != kModeObs && p.reward_mode == MSAT_REWARD_PBRS)
@@ -610,7 +653,7 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
             out.solved[b] = solved ? 1 : 0;
             if (out.num_unsat) out.num_unsat[b] = u_new;
             if (out.episode_step) out.episode_step[b] = step0 + 1;
-            // a covered env times out now (its step counter was listed at max_steps - 1): its reset happens in any
+            // a covered env times out now (the previous launch listed it at max_steps - 1): its reset happens in any
             // case, here and in its reset workgroup, so the state stays whole even for a misused queue
             MSAT_DCHECK(covered && !done ? 1 : 0, 1);
             const bool reset_now = (MODE == kModeStepAutoReset) && (done || covered);
@@ -621,18 +664,9 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
                 st.done[b] = done ? 1 : 0;
             }
             if (rq_fast) {  // list this env for the next launch if its next step times out
-                const int nxt = (p.rq_serial + 1) & 1;
                 const int next_step = reset_now ? 0 : step0 + 1;
-                uint32_t tok = 0u;
-                if (next_step + 1 >= p.max_steps) {
-                    const uint32_t want = rq_token(p.rq_serial + 1u);
-                    const int slot = rq.claim(nxt, want);
-                    if (slot < rq.cap) {
-                        rq.list_of(nxt)[slot] = b;
-                        tok = want;
-                    }
-                }
-                rq.pend_of(nxt)[b] = tok;
+                rq_pend(st.reset_queue, p.B, (p.rq_serial + 1) & 1)[b] =
+                    next_step + 1 >= p.max_steps ? rq_token(p.rq_serial + 1u) : 0u;
             }
         }
         lds_barrier();
@@ -675,11 +709,11 @@ __device__ __forceinline__ void env_run(const EnvParams &p, const msat_pool &poo
                                  obs + (size_t)b * p.A * p.D, &cs);
 }
 
-// A reset workgroup of an autoreset launch with a reset queue (rq_mode 1): entry j of the list the previous launch
-// made, i.e. an env that times out in this launch.  It draws the env's new instance and assignment (the same draw
-// as its step workgroup's), scans the new instance, and writes the clause state, the unsatisfied count and the
-// observation; its step workgroup writes the transition outputs, the assignment, step, done and problem_idx.
-// Two dependent round trips: {claim word, list entry}, then {pending token, pool row, agent tables}.
+// A reset workgroup of an autoreset launch with a reset queue (rq_mode 1): the pending env of rank j, i.e. an env that
+// times out in this launch.  It draws the env's new instance and assignment (the same draw as its step workgroup's),
+// scans the new instance, and writes the clause state, the unsatisfied count and the observation; its step workgroup
+// writes the transition outputs, the assignment, step, done and problem_idx.  Two dependent round trips: the
+// pending words (wave 0's scan), then the pool row and agent tables.
 template <typename ObsT, int T>
 __device__ __forceinline__ void env_side_reset(const EnvParams &p, const msat_pool &pool, const msat_env_state &st,
                                                const int32_t *__restrict__ new_pidx,
@@ -687,27 +721,20 @@ __device__ __forceinline__ void env_side_reset(const EnvParams &p, const msat_po
                                                ObsT *__restrict__ obs, int j, uint32_t *smem) {
     const EnvLds l = carve(smem, p);
     const int tid = threadIdx.x;
-    const ResetQueue rq(st.reset_queue, p.B, p.rq_cap);
-    const int cur = p.rq_serial & 1;
-    const uint32_t tok = rq_token(p.rq_serial);
-    // the claim word and the list entry in ONE vector load (lanes 0 / 1: the claim word's halves, lane 2: entry j),
-    // so the entry is read before it is known to be live, in the same round trip
-    const int lane = tid & 63;
-    const uint32_t *src = lane < 2 ? reinterpret_cast<const uint32_t *>(rq.cnt + cur) + lane
-                                   : reinterpret_cast<const uint32_t *>(rq.list_of(cur) + j);
-    const uint32_t v = *src;
-    const uint32_t cnt = __builtin_amdgcn_readlane(v, 0), ctok = __builtin_amdgcn_readlane(v, 1);
-    const int bl = (int)__builtin_amdgcn_readlane(v, 2);
-    if (ctok != tok || j >= min((int)cnt, rq.cap) || bl < 0 || bl >= p.B) return;
-    const int b = bl;
-    const uint32_t pend = rq.pend_of(cur)[b];
+    if (tid < 64) {
+        int b = -1;
+        rq_scan(rq_pend(st.reset_queue, p.B, p.rq_serial & 1), p.B, rq_token(p.rq_serial), 0, j, &b);
+        if (tid == 0) l.red[4] = b;
+    }
+    if (tid < 4) l.red[tid] = 0;
+    lds_barrier();
+    const int b = l.red[4];
+    if (b < 0) return;  // fewer than j + 1 envs time out in this launch
     const int pidx = reset_instance(p, new_pidx, seed, ctr, b);
     if (MSAT_DEBUG_BUILD && tid == 0) MSAT_DCHECK(pidx, p.N);
     uint64_t pw[kPfClause];
     uint32_t prel[kPfRel], pnbr[kPfNbr];
-    prefetch_instance<T>(p, pool, min(max(pidx, 0), p.N - 1), pw, prel, pnbr);
-    if (pend != tok) return;  // the env was modified since the list was made (its entry cleared): not ours
-    if (tid < 16) l.red[tid] = 0;
+    prefetch_instance<T>(p, pool, pidx, pw, prel, pnbr);
     reset_assignment<T>(p, l, new_assign, seed, ctr, b);
     lds_barrier();
     uint8_t *__restrict__ sat_g = st.clause_sat + (size_t)b * p.C;
@@ -1044,12 +1071,14 @@ static int make_params(const msat_env_desc *d, EnvParams *p) {
 static int set_reset_queue(EnvParams *p, const msat_env_state *st, int mode) {
     p->rq_mode = 0;
     if (st->reset_queue == nullptr || mode == kModeObs) return MSAT_OK;
-    MSAT_REQUIRE((reinterpret_cast<uintptr_t>(st->reset_queue) & 7) == 0, "reset_queue must be 8-byte aligned");
+    MSAT_REQUIRE((reinterpret_cast<uintptr_t>(st->reset_queue) & 15) == 0, "reset_queue must be 16-byte aligned");
     if (MSAT_DEBUG_BUILD)
         MSAT_REQUIRE(dbg_extent(st->reset_queue, 4) >= (long long)rq_words(p->B),
                      "MSAT_DEBUG: reset_queue smaller than msat_reset_queue_words(%d)", p->B);
     p->rq_serial = st->reset_serial;
-    p->rq_mode = (mode == kModeStepAutoReset && p->reward_mode == MSAT_REWARD_SPARSE) ? 1 : 2;
+    // the fast path reads an env's entry in its action load (mode 0, A < 64) and scans the entries 16 bytes at a time
+    p->rq_mode = (mode == kModeStepAutoReset && p->reward_mode == MSAT_REWARD_SPARSE && p->action_mode == 0 &&
+                  p->A < 64 && p->B % 4 == 0) ? 1 : 2;
     return MSAT_OK;
 }
 

@@ -83,17 +83,17 @@ def test_null_state_pointer_rejected():
 
 
 def test_reset_queue_size_and_alignment():
-    """msat_reset_queue_words: two claim words, a pending token per env and parity, two env lists of the
-    capacity B/256 + 8; a queue pointer that is not 8-byte aligned is refused before any launch."""
+    """msat_reset_queue_words: a pending token per env and parity; a queue pointer that is not 16-byte aligned is
+    refused before any launch."""
     from marlsat import _lib
 
     for B in (0, 1, 1024, 4096):
-        assert _lib.lib.msat_reset_queue_words(B) == 4 + 2 * B + 2 * (B // 256 + 8)
+        assert _lib.lib.msat_reset_queue_words(B) == 2 * B
     st = _lib.EnvStateC(8, 8, None, 8, 8, 8, 8, 12, 0)  # never dereferenced: the alignment check fails first
     out = _lib.StepOutC(8, 8, 8, None, None, None)
     rc = _lib.lib.msat_env_step(ctypes.byref(_desc()), ctypes.byref(_lib.PoolC(8, 8, 8)), ctypes.byref(st), 8, 1,
                                 None, None, 0, 0, ctypes.byref(out), None, None)
-    assert rc == -1 and "8-byte aligned" in _lib.lib.msat_last_error().decode()
+    assert rc == -1 and "16-byte aligned" in _lib.lib.msat_last_error().decode()
 
 
 def test_gae_bad_dims_rejected():

@@ -534,6 +534,7 @@ def _state_arrays(st):
     (20, 91, 10, 64, 3, True),  # caller-given reset instances and assignments (new_problem_idx / new_assign)
     (200, 860, 8, 512, 7, False),  # 512-lane workgroups
     (23, 97, 10, 40, 1, False),  # every step times out, and so does the step after a reset
+    (50, 218, 10, 2048, 512, False),  # counters from one reset: the whole batch times out together every 512 steps
 ])
 def test_reset_queue_is_invisible(V, C, vpa, B, max_steps, explicit):
     """The reset queue (msat_env_state.reset_queue: timed-out envs reset in workgroups of their own, listed by the
@@ -550,12 +551,16 @@ def test_reset_queue_is_invisible(V, C, vpa, B, max_steps, explicit):
     _, sq = env.reset_from_pool(pool, B, problem_idx=pidx, assignments=x)
     _, sn = env.reset_from_pool(pool, B, problem_idx=pidx, assignments=x)
     sn.reset_queue = None
-    if max_steps == 512:  # a long rollout's counters
+    if max_steps == 512 and B == 1024:  # a long rollout's counters
         c = torch.from_numpy(rng.integers(0, 512, B).astype(np.int32)).cuda()
         for s in (sq, sn):
             s.step.copy_(c)
         sq.invalidate_reset_queue()
     listed = 0
+    if B == 2048:  # all counters one step short of the limit: the mass timeout at the second launch
+        for s in (sq, sn):
+            s.step.fill_(510)
+        sq.invalidate_reset_queue()
     for t in range(14):
         if t == 5:  # reset a third of the envs in place: their queue entries are cleared
             m = rng.random(B) < 0.33
@@ -576,7 +581,7 @@ def test_reset_queue_is_invisible(V, C, vpa, B, max_steps, explicit):
             q = _np(sq.reset_queue).view(np.uint32)
             par = sq.reset_serial & 1
             tok = 0x80000000 | (sq.reset_serial & 0x7FFFFFFF)
-            listed += int((q[4 + par * B: 4 + (par + 1) * B] == tok).sum())
+            listed += int((q[par * B: (par + 1) * B] == tok).sum())
         outs = []
         for s in (sq, sn):
             o, out = env.step_raw(s, a, autoreset=auto, key=Key(9, t), **kw)
