@@ -103,7 +103,7 @@ typedef struct msat_env_state {
     /* Reset queue (nullable; msat_reset_queue_words(B) zeroed uint32 words, 16-byte aligned, owned by the state like
      * the arrays above): each msat_env_step(autoreset=1) launch marks the envs whose NEXT step times out (their step
      * counter reaches max_steps - 1; the reference's timed_out, env:256-260), and the next launch resets the first
-     * B/256 + 8 of them (in index order) in workgroups of their own, beside the step workgroups, instead of serially
+     * B/256 + 8 of them (rounded up to a multiple of 8; in index order) in workgroups of their own, beside the step workgroups, instead of serially
      * behind their step (their step workgroup then writes only the transition outputs, the assignment, step, done
      * and problem_idx).  Results are identical with or without it.  Used by the sparse reward mode with mode-0
      * actions and fewer than 64 agents (B a multiple of 4); the other state-modifying calls clear the entries of the

@@ -61,7 +61,9 @@ enum : int { kModeReset = 0, kModeStep = 1, kModeStepAutoReset = 2, kModeObs = 3
 // out (a batch reset together, every max_steps launches) costs each env one scan of B words from L2.  Tokens have
 // bit 31 set, so a zeroed queue lists nothing.
 __host__ __device__ __forceinline__ uint32_t rq_token(uint32_t serial) { return 0x80000000u | (serial & 0x7FFFFFFFu); }
-__host__ __device__ __forceinline__ int rq_capacity(int B) { return B / 256 + 8; }  // ~B/512 time out per launch
+// ~B/512 envs time out per launch; a multiple of 8, so the reset workgroups (launched first) leave the step workgroups
+// XCD placement as without them
+__host__ __device__ __forceinline__ int rq_capacity(int B) { return (B / 256 + 8 + 7) & ~7; }
 __host__ __device__ __forceinline__ size_t rq_words(int B) { return 2 * (size_t)B; }
 
 __device__ __forceinline__ uint32_t *rq_pend(uint32_t *q, int B, int par) { return q + (size_t)par * B; }
@@ -753,11 +755,14 @@ env_kernel(EnvParams p, msat_pool pool, msat_env_state st, const int32_t *__rest
            const uint8_t *__restrict__ new_assign, uint64_t seed, uint64_t ctr, msat_step_out out,
            ObsT *__restrict__ obs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    if (MODE == kModeStepAutoReset && (int)blockIdx.x >= p.B) {  // the reset workgroups, after every step one
-        env_side_reset<ObsT, T>(p, pool, st, new_pidx, new_assign, seed, ctr, obs, (int)blockIdx.x - p.B, smem);
+    // the reset workgroups first (block ids 0 .. cap - 1: their chain starts with a scan of the pending marks, and a
+    // place at the end of the dispatch order made them the launch's tail)
+    const int side = (MODE == kModeStepAutoReset && p.rq_mode == 1) ? p.rq_cap : 0;
+    if ((int)blockIdx.x < side) {
+        env_side_reset<ObsT, T>(p, pool, st, new_pidx, new_assign, seed, ctr, obs, (int)blockIdx.x, smem);
         return;
     }
-    const int b = xcd_major(blockIdx.x, p.B, p.ablate & 4);
+    const int b = xcd_major((int)blockIdx.x - side, p.B, p.ablate & 4);
     const ClockStamp cs(out.clock_stamps, b);
     env_run<MODE, ObsT, T>(p, pool, st, actions, reset_mask, new_pidx, new_assign, seed, ctr, out, obs, b, smem, cs);
     cs.finish();
@@ -1135,7 +1140,7 @@ static int launch_env(const EnvParams &p, const msat_env_desc *d, const msat_poo
     EnvParams pd = p;  // + the buffer extents in debug builds, the reset queue's role
     set_dbg_extents(&pd, st, actions, obs, d->obs_dtype);
     if (int rc = set_reset_queue(&pd, st, MODE)) return rc;
-    // the reset workgroups of a queue-consuming launch follow every step workgroup (block ids B .. B + cap - 1)
+    // the reset workgroups of a queue-consuming launch come first (block ids 0 .. cap - 1)
     const int grid = p.B + (pd.rq_mode == 1 ? pd.rq_cap : 0);
 #define MSAT_ENV_LAUNCH(TT)                                                                                        \
     if (d->obs_dtype == MSAT_OBS_I32)                                                                              \
