@@ -1270,6 +1270,7 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
         r.e = L.rx[rk][w][srow & 1];
         return r;
     };
+    float4 cmx = make_float4(0.f, 0.f, 0.f, 0.f);  // largest |a'| of this thread's four columns (small-column check)
     auto split_store = [&](const SplitIn &in, int k, auto RK, auto CL) {
         constexpr int rk = decltype(RK)::value;
         typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -1278,6 +1279,10 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
         // CL: rows past the split -> 2^-200 (0 for every finite a; a non-finite one stays non-finite and flags)
         if constexpr (decltype(CL)::value) sh = 16 * k + srow < nr ? sh : -200;
         const f2 x01 = {ldexpf(in.v.x, sh), ldexpf(in.v.y, sh)}, x23 = {ldexpf(in.v.z, sh), ldexpf(in.v.w, sh)};
+        cmx.x = fmaxf(cmx.x, fabsf(x01[0]));
+        cmx.y = fmaxf(cmx.y, fabsf(x01[1]));
+        cmx.z = fmaxf(cmx.z, fabsf(x23[0]));
+        cmx.w = fmaxf(cmx.w, fabsf(x23[1]));
         const h2 h01 = __builtin_convertvector(x01, h2), h23 = __builtin_convertvector(x23, h2);
         const f2 b01 = __builtin_convertvector(h01, f2), b23 = __builtin_convertvector(h23, f2);
         const f2 r01 = {vsub_f32(x01[0], b01[0]), vsub_f32(x01[1], b01[1])};
@@ -1423,7 +1428,23 @@ __device__ __forceinline__ void wgrad_pl_body(const float *__restrict__ A, int l
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) nonfin |= !(fabsf(acc[i][j][reg]) <= 3.402823466e38f);
     if (MSAT_WGRAD_ABL) nonfin = false;  // ablation builds: never the fixup (its time is not the kernel's)
-    const int bad = __syncthreads_or(nonfin);
+    // Small columns: a column of A whose largest |a'| over the split is below 2^-7 but not zero (a
+    // collapsed LayerNorm unit, say) keeps only fp16-subnormal precision in a' (absolute 2^-25, i.e. > 2^-18 of
+    // its own terms): the workgroup goes to the bf16x3 fixup, whose operands keep fp32's exponent range.  The 16
+    // threads of a column group pool their maxima in the (now free) raw-A slots.
+    __syncthreads();  // every wave is past its last split and fragment reads
+    float *cm = L.raw[0];
+    *reinterpret_cast<float4 *>(&cm[srow * kX3M + sc]) = cmx;
+    __syncthreads();
+    bool small = false;
+    if (t < kX3M && k0 + t < K) {
+        float m = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m = fmaxf(m, cm[r * kX3M + t]);
+        small = m > 0.f && m < 0.0078125f;
+    }
+    if (MSAT_WGRAD_ABL) small = false;
+    const int bad = __syncthreads_or(nonfin || small);
     if (t == 0) *flag = bad;
     if (bad) return;
     float *P = part + (size_t)sp * K * N;

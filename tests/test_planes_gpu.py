@@ -150,7 +150,8 @@ def test_dual_dgrad_planes_is_bitwise_the_fp32_row_form(M, K1, wbig):
 
 
 @pytest.mark.parametrize("M,K1,amp", [(1, 128, 0), (17, 256, 0), (385, 256, 0), (4999, 128, 0), (70001, 256, 0),
-                                      (20000, 128, 1), (20000, 256, 2), (2200001, 256, 0)])
+                                      (20000, 128, 1), (20000, 256, 2), (2200001, 256, 0), (20000, 256, 3),
+                                      (70001, 128, 4)])
 def test_dual_wgrad_planes_match_fp64(M, K1, amp):
     from marlsat import _lib
 
@@ -167,8 +168,18 @@ def test_dual_wgrad_planes_match_fp64(M, K1, amp):
         hx[M // 3: M // 3 + 5] *= 1e6
     if amp == 2:  # |a| up to ~250: a' = a 2^8 up to fp16's largest finite values, still the fp16x2 path
         xx[M // 2: M // 2 + 7] *= 60.0
+    if amp == 3:  # every activation tiny: a' fp16-subnormal in every column -> every workgroup's fixup
+        hx *= 1e-6
+        xx *= 1e-6
+    if amp == 4:  # single collapsed columns (a LayerNorm unit whose scale went to ~0) beside normal ones
+        hx[:, 5] *= 1e-7
+        xx[:, 9] *= 1e-8
+        xx[:, K1 - 1] = 0.0  # an all-zero column needs no fixup (its products are zero)
     W0 = torch.randn(H, 3 * H, device="cuda", generator=g)
     W1 = torch.randn(K1, 3 * H, device="cuda", generator=g)
+    if amp in (3, 4):  # nothing to add to: the bar is then the tiny products' own 4e-6 of sum |a g|
+        W0.zero_()
+        W1.zero_()
     ws = torch.empty(int(L.msat_gemm_wgrad_dual_workspace_bytes(M, H, 3 * H, K1, 3 * H)) // 4 + 1, device="cuda")
     outs = []
     for _ in range(2):
