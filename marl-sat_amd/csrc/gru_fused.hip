@@ -296,18 +296,22 @@ __device__ __forceinline__ float ftanh_fast(float x) {
 // (64-byte rows, chunk c at slot c ^ f((u >> 2) & 3), f = {0, 2, 3, 1}), double-buffered.
 //
 // Operands: x = x1 + x2, x1 = fp16(x), x2 = fp16(x - x1) (x - x1 exact; 22 significant bits while x2
-// stays in fp16's normal range, i.e. |x| >~ 2^-3; the activations are not scaled, so for smaller |x| the
-// low half is subnormal and the representation error is absolute, <= 2^-25 per element); the
-// weights are scaled by 2^kH2Shift before their split (msat_split_f16x2_t) and the sums by 2^-kH2Shift
-// after (both exact).  Three MFMAs per (gate, column tile) block, a1b2 a2b1 a1b1; the dropped a2b2 and
-// the representation residuals are <= 3 * 2^-22 |ab| per product (plus the absolute term above for small
-// activations), under the fp32 accumulation error of
-// a 288..416-deep dot product (tests/test_gnn_gpu.py at L = 16 bounds the network against the fp32 CPU
-// oracle).  Against bf16x3: half the MFMAs (3 vs 6), 48 instead of 72 KiB of weights per step.
-// fp16's range is checked, not assumed: a tile that loads an activation with |a| >= 2^15, or whose
-// weights overflowed at the split (wbad), writes flags[tile] = 1 and no output, and the bf16x3 kernel,
-// launched next with the same flags, recomputes exactly the flagged tiles.
+// stays in fp16's normal range, i.e. |x| >~ 2^-3, below that the representation error is absolute,
+// <= 2^-25); the activations are scaled by 2^kH2AShift and the weights by 2^kH2Shift before their splits
+// (msat_split_f16x2_t), the sums by 2^-(kH2Shift + kH2AShift) after (all exact).  Three MFMAs per (gate,
+// column tile) block, a1b2 a2b1 a1b1; the dropped a2b2 and the representation residuals are <= 3 * 2^-22 |ab|
+// per product, under the fp32 accumulation error of a 288..416-deep dot product.
+// Why the activations are scaled (round 6): unscaled, every activation below 2^-3 (LayerNorm outputs near
+// zero, small message sums) kept only an absolute 2^-25; in the L = 16 train cycle that error, applied to
+// every row, moved the var-negative cell's n-gate bias gradients by up to 10x the fp32 oracle's own error at
+// fixed parameters (profiles/parity_attrib.py + parity_orderings.py).  2^7 keeps 22 bits
+// down to |x| ~ 1e-3 and leaves |x| < 256 inside the range check below.
+// Against bf16x3: half the MFMAs (3 vs 6), 48 instead of 72 KiB of weights per step.
+// fp16's range is checked, not assumed: a tile that loads an activation with |a| 2^kH2AShift >= 2^15 (|a| >=
+// 256), or whose weights overflowed at the split (wbad), writes flags[tile] = 1 and no output, and the
+// bf16x3 kernel, launched next with the same flags, recomputes exactly the flagged tiles.
 constexpr int kH2Shift = 10;  // weight scale 2^10: |W| < 32 fits, |W| >= 2^-24 keeps 11 bits
+constexpr int kH2AShift = 7;  // activation scale 2^7: |a| < 256 fits, |a| >= 2^-10 keeps 22 bits
 
 
 __device__ __forceinline__ int gswz16(int b) { return (0x78 >> (2 * b)) & 3; }  // {0, 2, 3, 1}
@@ -427,8 +431,10 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
         const int kx = st * 32 + 8 * g;
         const bool z0 = st < nin && kx >= kx_end, z1 = st < nin && kx + 4 >= kx_end;
         const f4v zero = {0.f, 0.f, 0.f, 0.f};
-        const float4 v0 = __builtin_bit_cast(float4, z0 ? zero : r[0]);
-        const float4 v1 = __builtin_bit_cast(float4, z1 ? zero : r[1]);
+        const f4v as = {(float)(1 << kH2AShift), (float)(1 << kH2AShift), (float)(1 << kH2AShift),
+                        (float)(1 << kH2AShift)};  // exact power of two
+        const float4 v0 = __builtin_bit_cast(float4, z0 ? zero : r[0] * as);
+        const float4 v1 = __builtin_bit_cast(float4, z1 ? zero : r[1] * as);
         const float m0 = fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w)));
         const float m1 = fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w)));
         amax = fmaxf(amax, fmaxf(m0, m1));
@@ -565,7 +571,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
 #pragma unroll 1
         for (; st < ns; ++st) pstep(st, std::true_type{});
     }
-    {  // range check: |a| < 2^15 keeps a1 = fp16(a) finite with margin.  A ballot per wave and an
+    {  // range check: |a 2^kH2AShift| < 2^15 keeps a1 = fp16(a 2^kH2AShift) finite with margin.  A ballot per wave and an
        // LDS-only barrier: __syncthreads_or's fence would also wait for the h DMA in flight.
         // the weight buffers are free past the last step's barrier: the flags sit in Bs's last 32 bytes,
         // beyond the epilogue's stage (LDS is full: 96 KiB of weights + 64 KiB of activation slots)
@@ -604,7 +610,7 @@ __device__ __forceinline__ void gru_h2s_tile(const GruX3rArgs &a, int tile) {
             }
         }
     }
-    constexpr float sc = 1.0f / (float)(1 << kH2Shift);  // exact power of two
+    constexpr float sc = 1.0f / (float)(1 << (kH2Shift + kH2AShift));  // exact power of two
     // packed fp32 (v_pk_mul / v_pk_add on row pairs): no MFMAs run here, so the packed forms halve the
     // epilogue's vector issue instead of competing with matrix work
     // LayerNorm scale / bias, loaded with the gate biases

@@ -145,17 +145,20 @@ def test_fused_forward_matches_reference(R, H, kind, layout):
     assert bool((terr <= 2e-6 * ab + 1e-30).all()), float((terr / (ab + 1e-30)).max())
 
 
+@pytest.mark.parametrize("big", [4.0e4, 256.0])
 @pytest.mark.parametrize("R,bad_tiles", [(1000, (1, 6)), (70000, (0, 300, 546))])
 @pytest.mark.parametrize("kind", ["var8", "clause4"])
-def test_h2r_out_of_range_tiles_take_the_bf16x3_path(kind, R, bad_tiles):
-    """fp16x2 range check: activations with |a| >= 2^15 in a row flag exactly its 128-row tile, which the
-    fixup launch recomputes in bf16x3 (bitwise the x3r kernel's rows there), the other tiles keep the
-    fp16x2 result; weights with |W| >= 32 flag the split and every tile is bf16x3.  70,000 rows: the first
-    tile, one in the middle and the last, partial tile (546)."""
+def test_h2r_out_of_range_tiles_take_the_bf16x3_path(kind, R, bad_tiles, big):
+    """fp16x2 range check: activations with |a| >= 256 (2^15 after the kernel's 2^7 pre-scale) in a row flag
+    exactly its 128-row tile, which the fixup launch recomputes in bf16x3 (bitwise the x3r kernel's rows
+    there), the other tiles keep the fp16x2 result, also where |a| is just inside the range (255 in tile 2 /
+    200); weights with |W| >= 32 flag the split and every tile is bf16x3.  70,000 rows: the first tile, one
+    in the middle and the last, partial tile (546)."""
     H = 128
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=3)
     for i, t in enumerate(bad_tiles):
-        segs[0][0][min(R - 1, 128 * t + 2 + 37 * i), 5 + 12 * i] = 4.0e4 * (-1) ** i
+        segs[0][0][min(R - 1, 128 * t + 2 + 37 * i), 5 + 12 * i] = big * (-1) ** i
+    segs[0][0][128 * 2 + 9, 3] = -255.0  # inside the range: tile 2 stays fp16x2
     x = torch.cat([segs[0][0][:, segs[0][1]:segs[0][1] + segs[0][3]], segs[1][0]], 1)
     g4 = torch.empty(R, 4 * H, device="cuda")
     out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, "h2r")

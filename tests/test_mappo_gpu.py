@@ -3,6 +3,8 @@ transitions / permutation (JAX RNG streams cannot be reproduced, so the device's
 own random draws are the shared input).  Checks rollout log-probs and values,
 GAE targets / normalised advantages, every minibatch loss, and the parameters
 after all Adam steps."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -260,6 +262,15 @@ def test_train_cycle_every_adam_step_matches_oracle(V, C, vpa, H, L, mode, shape
                            metrics["epoch_entropies"].reshape(-1)], 1)
     assert len(learner.trace) == E * (T * B // MB) == dev_losses.shape[0]
     m_st = {"count": 0, "m": None, "v": None}
+    dump = os.environ.get("MARLSAT_PARITY_DUMP")  # diagnostics (profiles/parity_orderings.py): the inputs
+    if dump:  # of every step's oracle check, saved before the checks run
+        os.makedirs(dump, exist_ok=True)
+        np.savez(os.path.join(dump, f"{precision_path}_V{V}_L{L}_s{seed}.npz"),
+                 **{f"full_{k}": v.numpy() for k, v in full.items()}, av=av.numpy(), am=am.numpy(),
+                 **{f"idx_{s}": r["idx"].numpy() for s, r in enumerate(learner.trace)},
+                 **{f"params_{s}": r["params"].cpu().numpy() for s, r in enumerate(learner.trace)},
+                 **{f"grads_{s}": r["grads"].cpu().numpy() for s, r in enumerate(learner.trace)},
+                 pidx=pidx, x_raw=x, shape=np.array([V, C, vpa, H, L, mode, T, B, MB, E]))
     for s, rec in enumerate(learner.trace):
         idx = rec["idx"].numpy()
         mb = {k: v[idx] for k, v in full.items()}
