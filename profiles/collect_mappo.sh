@@ -7,6 +7,7 @@ TAG=${1:-r02}
 LEG=${2:-uf100-430:4096:8}
 OUT=$R/gpurun_out/profm
 mkdir -p $OUT $R/gpurun_out/keep
+trap 'rm -rf $OUT' EXIT  # the raw trace is far larger than what gpurun copies back
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o m -- python3 $R/bench.py --steps 20 --warmup 5 --cpu-budget 0 --mappo $LEG > $OUT/bench.log 2>&1
 W=${LEG%%:*}

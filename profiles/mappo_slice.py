@@ -16,8 +16,8 @@ if "kernels" not in bench:  # compact leg (round 3): the per-kernel table is in 
     import os
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    det = bench["detail"]  # the side file; since round 4 its name only (it lives under gpurun_out/)
-    bench = json.load(open(os.path.join(root, det if os.sep in det else os.path.join("gpurun_out", det))))
+    det = bench["detail"]  # the side file; since round 4 its name only: gpurun_out/bench_<detail>.json
+    bench = json.load(open(os.path.join(root, det if os.sep in det else os.path.join("gpurun_out", f"bench_{det}.json"))))
 ROCPROF_NAMES = {  # bench label -> rocprof kernel names whose launches the bench's event pair brackets
     "gru_ln_fused_fwd_x3r_kernel (bf16x3)": ["gru_ln_fused_fwd_x3r_kernel"],
     "gru_ln_fused_fwd_h2r_kernel (fp16x2, + x3r fixup launch)": ["gru_ln_fused_fwd_h2r_kernel", "gru_ln_fused_fwd_x3r_kernel"],
