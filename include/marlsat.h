@@ -134,7 +134,8 @@ typedef struct msat_step_out {
 } msat_step_out;
 
 const char *msat_last_error(void);
-int msat_version(void); /* 2: msat_step_out carries clock_stamps (version 1 had no such field) */
+int msat_version(void); /* 3: msat_env_state carries reset_queue / reset_serial (version 2 had neither), 2:
+                         * msat_step_out carries clock_stamps (version 1 had no such field) */
 
 /* Pack an int32 literal tensor (N,C,K) (signed, 1-based, 0 = null literal) into
  * the device pool layout uint16 (N,C,4).  Literals with |l| > V set *err_flag

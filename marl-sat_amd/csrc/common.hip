@@ -22,6 +22,7 @@ int check_launch_plain(const char *what) {
 }  // namespace msat
 
 extern "C" const char *msat_last_error(void) { return msat::g_err; }
-// ABI version: 2 since msat_step_out gained clock_stamps (round 5); a caller built against the version-1 header
-// passes a struct without that field, so it must check msat_version() >= 2
-extern "C" int msat_version(void) { return 2; }
+// ABI version: 2 since msat_step_out gained clock_stamps (round 5), 3 since msat_env_state gained reset_queue /
+// reset_serial (round 6); a caller built against an older header passes structs without those fields, so it must
+// check msat_version() >= 3
+extern "C" int msat_version(void) { return 3; }

@@ -186,7 +186,7 @@ def _load():
 
 
 lib = _load()
-ABI_VERSION = 2  # msat_version() of the header this binding follows (msat_step_out with clock_stamps)
+ABI_VERSION = 3  # msat_version() of the header this binding follows (msat_env_state with the reset queue)
 if lib.msat_version() != ABI_VERSION:
     raise ImportError(f"marlsat: {LIB_PATH} has C-ABI version {lib.msat_version()}, this binding needs {ABI_VERSION}; "
                       "rebuild it (make -C marl-sat_amd)")

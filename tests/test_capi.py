@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(_lib.lib, s), s
     assert sorted(_lib.EXPORTED) == syms
-    assert _lib.lib.msat_version() == 2  # msat_step_out with clock_stamps (include/marlsat.h)
+    assert _lib.lib.msat_version() == 3  # msat_env_state with reset_queue / reset_serial (include/marlsat.h)
 
 
 def test_nm_lists_c_abi_symbols():

@@ -145,6 +145,36 @@ def test_fused_forward_matches_reference(R, H, kind, layout):
     assert bool((terr <= 2e-6 * ab + 1e-30).all()), float((terr / (ab + 1e-30)).max())
 
 
+@pytest.mark.parametrize("kind", ["var8", "clause4"])
+def test_h2r_small_activations_keep_22_bits(kind):
+    """fp16x2 keeps 22 significant bits of an activation only while its low half stays in fp16's normal range;
+    the kernel scales the activations by 2^7 before the split so that this holds down to |a| ~ 1e-3.  Every
+    activation here is ~1e-3 (inputs and h), biases 0: the tape's products must be fp32-precise against float64
+    (<= 1e-7 of sum|terms|).  Split unscaled, each such activation carried an absolute 2^-25 (3% of an fp16 ulp
+    at 1), ~1e-6 of sum|terms| -- the error that moved the headline train cycle's var-negative n-gate bias
+    gradients by 10x fp32's own."""
+    H, R = 128, 1000
+    segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=11)
+    for t, _, _, _ in segs:
+        t.mul_(1e-3)
+    h = h * 1e-3
+    x = x * 1e-3
+    bi, bh = torch.zeros_like(bi), torch.zeros_like(bh)
+    g4 = torch.empty(R, 4 * H, device="cuda")
+    out = _fwd(segs, h, wi, bi, wh, bh, sc, lb, R, H, g4, "h2r")
+    flags, bad = _fwd.last_flags
+    assert int(flags.sum()) == 0 and bad.tolist() == [0, 0]
+    d = lambda t: t.double()
+    ref, gi, gh = _ref_gru_ln(d(x), d(h), d(wi), d(bi), d(wh), d(bh), d(sc), d(lb), H)
+    tape_ref = torch.cat([gi[:, :H] + gh[:, :H], gi[:, H:2 * H] + gh[:, H:2 * H], gi[:, 2 * H:], gh[:, 2 * H:]], 1)
+    absx = torch.cat([d(x).abs() @ d(wi).abs(), d(h).abs() @ d(wh).abs()], 1)
+    ab = torch.cat([absx[:, :H] + absx[:, 3 * H:4 * H], absx[:, H:2 * H] + absx[:, 4 * H:5 * H],
+                    absx[:, 2 * H:3 * H], absx[:, 5 * H:]], 1)
+    rel = ((g4.double() - tape_ref).abs() / ab).max().item()
+    assert rel <= 1e-7, rel
+    assert bool(((out.double() - ref).abs() <= 1e-5 * ref.abs() + 1e-5).all())
+
+
 @pytest.mark.parametrize("big", [4.0e4, 256.0])
 @pytest.mark.parametrize("R,bad_tiles", [(1000, (1, 6)), (70000, (0, 300, 546))])
 @pytest.mark.parametrize("kind", ["var8", "clause4"])
