@@ -149,10 +149,10 @@ def test_fused_forward_matches_reference(R, H, kind, layout):
 def test_h2r_small_activations_keep_22_bits(kind):
     """fp16x2 keeps 22 significant bits of an activation only while its low half stays in fp16's normal range;
     the kernel scales the activations by 2^7 before the split so that this holds down to |a| ~ 1e-3.  Every
-    activation here is ~1e-3 (inputs and h), biases 0: the tape's products must be fp32-precise against float64
-    (<= 1e-7 of sum|terms|).  Split unscaled, each such activation carried an absolute 2^-25 (3% of an fp16 ulp
-    at 1), ~1e-6 of sum|terms| -- the error that moved the headline train cycle's var-negative n-gate bias
-    gradients by 10x fp32's own."""
+    activation here is ~1e-3 (inputs and h), biases 0: the tape must stay within fp32 accumulation error of
+    float64 (<= 5e-7 of sum|terms|).  Split unscaled, each such activation carried an absolute 2^-25, several
+    times that bound -- the error that moved the headline train cycle's var-negative n-gate bias gradients by 10x
+    fp32's own (DESIGN.md section 6; profiles/r06/r06s_* holds both builds' numbers)."""
     H, R = 128, 1000
     segs, x, h, wi, bi, wh, bh, sc, lb = _setup(R, H, kind, seed=11)
     for t, _, _, _ in segs:
@@ -171,7 +171,8 @@ def test_h2r_small_activations_keep_22_bits(kind):
     ab = torch.cat([absx[:, :H] + absx[:, 3 * H:4 * H], absx[:, H:2 * H] + absx[:, 4 * H:5 * H],
                     absx[:, 2 * H:3 * H], absx[:, 5 * H:]], 1)
     rel = ((g4.double() - tape_ref).abs() / ab).max().item()
-    assert rel <= 1e-7, rel
+    print(f"small activations ({kind}): tape error / sum|terms| max {rel:.3g}")
+    assert rel <= 5e-7, rel
     assert bool(((out.double() - ref).abs() <= 1e-5 * ref.abs() + 1e-5).all())
 
 
