@@ -63,10 +63,10 @@ X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 
 
 
-def env_lanes(A: int, D: int) -> int:
+def env_lanes(A: int, D: int, B: int) -> int:
     """Workgroup size the env step launches with (env_kernels.hip env_threads): for the kernel label."""
     n = A * D
-    return 64 if n <= 4096 else (512 if n >= 16384 else 256)
+    return (128 if B <= 1024 else 64) if n <= 4096 else (512 if n >= 16384 else 256)
 
 def step_bytes(V: int, C: int, A: int) -> int:
     """Algorithmic bytes of one env-step (reference API dtypes)."""
@@ -687,7 +687,7 @@ def env_leg(args, rank, world, dist, workload: Optional[str] = None, envs: Optio
         sstep = classes[0].stepper(st, o, outs[0], autoreset=True, seed=seed)
         step = lambda i, c: sstep(acts[0][i % ring], c)
         e0 = classes[0]
-        lanes = int(os.environ.get("MARLSAT_ENV_THREADS", "0")) or env_lanes(e0.num_agents, 2 * e0.num_vars + e0.num_clauses)
+        lanes = int(os.environ.get("MARLSAT_ENV_THREADS", "0")) or env_lanes(e0.num_agents, 2 * e0.num_vars + e0.num_clauses, sizes[0])
         kernel = f"env_kernel<2,{'int' if obs_dtype == torch.int32 else 'signed char'},{lanes}>"
     counter = 1
     # the same launches with the kernel's clock stamps on (a second out record carrying the stamp buffers)
