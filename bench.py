@@ -66,7 +66,11 @@ X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 def env_lanes(A: int, D: int, B: int) -> int:
     """Workgroup size the env step launches with (env_kernels.hip env_threads): for the kernel label."""
     n = A * D
-    return (128 if B <= 1024 else 64) if n <= 4096 else (512 if n >= 16384 else 256)
+    if n >= 16384:
+        return 512
+    if n > 4096:
+        return 256 if B <= 1024 else 128
+    return 128 if B <= 1024 else 64
 
 def step_bytes(V: int, C: int, A: int) -> int:
     """Algorithmic bytes of one env-step (reference API dtypes)."""

@@ -1120,12 +1120,15 @@ static int env_threads(const EnvParams &p) {
         return v == 64 || v == 128 || v == 256 || v == 512 ? v : 0;
     }();
     if (forced) return forced;
-    // uf50 x 4096: 13.4 us at 64 lanes vs 20.0 at 256 (14.1 vs 16.6 at 128); uf100 x 4096: 27.6 us at 256, 34.9 at
-    // 512; uf200 x 4096: 111 us at 512, 113 at 256, 142 at 64.  A small instance in a small batch (a few envs per CU:
-    // each env's chain bounds the launch) takes two waves: uf50 x 1024 7.57 us at 128 vs 7.86 at 64 and 7.88 at 256,
-    // uf50 x 2048 10.1 vs 9.86 at 64 (profiles/r06/r06t_*, r06u_*)
+    // Fewer lanes per env as the batch grows (more envs resident per CU), more while each env's chain bounds the
+    // launch (a few envs per CU).  uf50: x 1024 7.57 us at 128 vs 7.86 at 64, 7.88 at 256; x 2048 9.86 at 64 vs 10.1
+    // at 128; x 4096 14.1 at 64 vs 16.6 at 128.  uf100: x 1024 11.0 at 256 vs 11.6 at 128, 14.6 at 64; x 2048 15.3 at
+    // 128 vs 16.6 at 256; x 4096 25.8 at 128 vs 26.3 at 256.  uf200 x 4096: 107 at 512 vs 109 at 256, 142 at 64
+    // (profiles/r06/r06t_*, r06u_*, r06w_*, r06x_*)
     const long n = (long)p.A * p.D;
-    return n <= 4096 ? (p.B <= 1024 ? 128 : 64) : (n >= 16384 ? 512 : 256);
+    if (n >= 16384) return 512;
+    if (n > 4096) return p.B <= 1024 ? 256 : 128;
+    return p.B <= 1024 ? 128 : 64;
 }
 
 template <int MODE>
