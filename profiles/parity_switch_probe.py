@@ -23,6 +23,7 @@ CASES = {  # label: the switches that differ from the fp16x2 default
     "wgrad": {"use_wgrad_h2": False},  # weight gradients in bf16x3
     "planes0": {"use_planes": False},  # packed rows stored fp32, split by each consumer
     "bf16x3": {"use_gru_h2": False, "use_dgrad_h2": False, "use_wgrad_h2": False},  # the whole bf16x3 path
+    "fp32": "fp32",  # MARLSAT_PRECISION=fp32's path (gnn.set_precision): fp32 MFMA, the reference's order
 }
 SHAPE = (100, 430, 10, 128, 16, 0, (2, 4, 4, 1))
 
@@ -36,11 +37,15 @@ if __name__ == "__main__":
         seeds = [int(x) for x in args[1].split(",")]
         args = args[2:]
     for label in args or list(CASES):
-        saved = {k: getattr(GNNActorCritic, k) for k in CASES[label]}
-        for k, v in CASES[label].items():
-            setattr(GNNActorCritic, k, v)
-        if not GNNActorCritic.use_wgrad_h2:  # the library's weight-gradient path follows
-            _lib.check(_lib.lib.msat_set_precision(gnn.PRECISION_CODES["bf16x3"]), "msat_set_precision")
+        if isinstance(CASES[label], str):  # a whole precision path
+            prev = gnn.set_precision(CASES[label])
+            saved = {k: v for k, v in prev.items() if k != "_code"}
+        else:
+            saved = {k: getattr(GNNActorCritic, k) for k in CASES[label]}
+            for k, v in CASES[label].items():
+                setattr(GNNActorCritic, k, v)
+            if not GNNActorCritic.use_wgrad_h2:  # the library's weight-gradient path follows
+                _lib.check(_lib.lib.msat_set_precision(gnn.PRECISION_CODES["bf16x3"]), "msat_set_precision")
         try:
             for sd in seeds:
                 try:
