@@ -59,7 +59,10 @@ def main():
     params = torch.from_numpy(d[f"params_{s}"]).cuda()
     ent = ent_coef_at(0, cfg)
     res = {}
+    want = os.environ.get("ATTRIB_CASES")  # a comma-separated subset of CASES (default: all)
     for label, sw in CASES.items():
+        if want and label not in want.split(","):
+            continue
         saved = {k: getattr(GNNActorCritic, k) for k in sw if not k.startswith("_")}
         code = int(_lib.lib.msat_get_precision())
         try:
