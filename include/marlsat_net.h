@@ -181,8 +181,9 @@ int msat_gru_ln_fused_fwd_x3r(const float *x0, int32_t ld0, int32_t w0, const fl
  * zero-padded split of a (K, N) weight (row stride ldw) for msat_gru_ln_fused_fwd_x3r. */
 int msat_split_bf16x3_t(const float *W, int32_t K, int32_t N, int32_t ldw, int32_t Kp, void *planes, void *stream);
 /* The same GRU cell with fp16x2 operands (x = x1 + x2, three fp16 MFMAs per product instead of six
- * bf16 ones; weights from msat_split_f16x2_t, scaled by 2^10).  fp16's range is checked per 128-row
- * tile: a tile whose activations reach |a| >= 2^15, or every tile when a weight split flagged wbad[0]
+ * bf16 ones; weights from msat_split_f16x2_t, scaled by 2^10; activations scaled by 2^7 before their split so
+ * that small ones keep 22 bits).  fp16's range is checked per 128-row tile: a tile whose activations reach
+ * |a| >= 256 (2^15 after the scale), or every tile when a weight split flagged wbad[0]
  * (wi) or wbad[1] (wh), is recomputed by the bf16x3 kernel from wiT_x3 / whT_x3 (msat_split_bf16x3_t
  * planes) in a second launch on the same stream.  tile_flags: >= ceil(R / 128) ints of workspace. */
 int msat_gru_ln_fused_fwd_h2r(const float *x0, int32_t ld0, int32_t w0, const float *x1, int32_t ld1, int32_t w1,
